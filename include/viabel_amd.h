@@ -1,0 +1,210 @@
+/*
+ * viabel_amd.h — C ABI of the MI355X (gfx950) Monte Carlo VI hot path.
+ *
+ * This is the drop-in boundary behind which the viabel.vb / viabel.bounds /
+ * psis Python API (mirrored by the `viabel_amd` package) runs on HIP kernels.
+ * Plain C types only: pointers + sizes, no torch / numpy types.  Every pointer
+ * argument may be host memory or device memory (hipMalloc / torch.cuda); the
+ * library detects which with hipPointerGetAttributes and stages host buffers
+ * through the context's device scratch.  The library never retains a caller
+ * pointer after a call returns.
+ *
+ * Error convention: every entry point returns VB_OK (0) or a negative code;
+ * vb_last_error() returns a thread-local message for the last failure.
+ * No C++ exception crosses this boundary.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo):
+ *   vb_family_*            viabel/vb.py:42-82 (mean_field_gaussian_variational_family),
+ *                          viabel/vb.py:140-182 (mean_field_t_variational_family)
+ *   vb_objective_value_grad viabel/vb.py:236-245 (black_box_klvi),
+ *                          viabel/vb.py:248-266 (black_box_chivi)
+ *   vb_run_*               viabel/vb.py:324-389 (learning_rate_schedule, adagrad_optimize)
+ *   vb_adagrad_update      viabel/vb.py:364-374 (one adagrad step for a foreign objective)
+ *   vb_log_weights         notebooks/experiments.py:60-63 (get_samples_and_log_weights)
+ *   vb_divergence_bound    viabel/bounds.py:142-192 (divergence_bound, mean_and_check_mc_error)
+ *   vb_centered_moments    viabel/bounds.py:127-135 (wasserstein_bounds sample moments)
+ *   vb_covariance          viabel/bounds.py:55-56 (np.cov(samples.T), ddof = 1)
+ *   vb_psislw              notebooks/psis.py:112-208 (psislw)
+ *   vb_gpdfit              notebooks/psis.py:211-331 (gpdfitnew)
+ *   vb_gpinv               notebooks/psis.py:334-376 (gpinv)
+ *   vb_sumlogs             notebooks/psis.py:379-395 (sumlogs)
+ */
+#ifndef VIABEL_AMD_H
+#define VIABEL_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VB_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------- */
+enum {
+  VB_OK = 0,
+  VB_EINVAL = -1,       /* bad argument: Python raises ValueError */
+  VB_EDEVICE = -2,      /* HIP runtime failure: RuntimeError */
+  VB_ENOMEM = -3,       /* allocation failure: MemoryError */
+  VB_EUNSUPPORTED = -4  /* valid but not implemented on device: NotImplementedError */
+};
+
+/* ---- descriptors ----------------------------------------------------- */
+enum vb_family_kind {
+  VB_FAMILY_MF_GAUSSIAN = 0, /* lambda = [mean(D), log_std(D)]       vb.py:48-82   */
+  VB_FAMILY_MF_T = 1         /* lambda = [mean(D), log_scale(D)], df  vb.py:140-182 */
+};
+
+enum vb_target_kind {
+  VB_TARGET_ISOGAUSS = 0,       /* N(0, I_D)                                  (separable) */
+  VB_TARGET_MIXTURE = 1,        /* prod_d 0.5 N(-2,1) + 0.5 N(2,1)            (separable) */
+  VB_TARGET_FUNNEL = 2,         /* Neal's funnel, x[1] = log sigma ~ N(0,1.35^2)           */
+  VB_TARGET_EIGHT_SCHOOLS_NCP = 3 /* eight_schools_ncp.stan log_prob, D = 10               */
+};
+
+enum vb_objective_kind {
+  VB_OBJ_KLVI = 0,  /* value = -(entropy + mean log p)            vb.py:236-245 */
+  VB_OBJ_CHIVI = 1  /* value = CUBO_alpha, grad = alpha/N sum w dlw vb.py:248-266 */
+};
+
+enum vb_noise_kind {
+  VB_NOISE_HOST = 0,   /* standardized draws supplied by the caller (numpy legacy RNG parity) */
+  VB_NOISE_PHILOX = 1  /* in-kernel Philox4x32-10, counter = (pair, sample, step, stream) */
+};
+
+typedef struct vb_family {
+  int32_t kind;   /* vb_family_kind */
+  int32_t reserved;
+  int64_t dim;    /* D */
+  double df;      /* degrees of freedom (t family), ignored otherwise */
+} vb_family;
+
+typedef struct vb_target {
+  int32_t kind;   /* vb_target_kind */
+  int32_t reserved;
+  int64_t dim;    /* D (must equal the family's) */
+} vb_target;
+
+typedef struct vb_objective {
+  int32_t kind;      /* vb_objective_kind */
+  int32_t reserved;
+  double alpha;      /* CHIVI order (> 1); ignored for KLVI */
+  int64_t n_samples; /* N Monte Carlo draws per call */
+} vb_objective;
+
+/* Noise source.  HOST: `eps` holds standardized draws laid out
+ * [problem][step][sample][dim] (C order): N(0,1) for the Gaussian family,
+ * standard_t(df) for the t family.  PHILOX: `seed` keys the generator;
+ * `stream` (24 bits) + problem index selects the stream; `step` is the
+ * global step index of the first step of the call. */
+typedef struct vb_noise {
+  int32_t kind;      /* vb_noise_kind */
+  uint32_t stream;
+  uint64_t seed;
+  uint64_t step;
+  const double* eps; /* HOST only */
+} vb_noise;
+
+/* Adagrad settings, vb.py:345-347 defaults: window 10, lr .01, eps .1. */
+typedef struct vb_adagrad_config {
+  int64_t n_iters;
+  int32_t window;
+  int32_t reserved;
+  double learning_rate;
+  double learning_rate_end; /* NaN = None (constant schedule) */
+  double epsilon;
+} vb_adagrad_config;
+
+typedef struct vb_ctx vb_ctx;
+typedef struct vb_run vb_run;
+
+/* ---- context --------------------------------------------------------- */
+int vb_abi_version(void);
+const char* vb_last_error(void);
+/* `hip_stream` may be NULL (the context creates its own stream) or an
+ * existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream). */
+int vb_ctx_create(int device, void* hip_stream, vb_ctx** out);
+int vb_ctx_destroy(vb_ctx* ctx);
+int vb_ctx_synchronize(vb_ctx* ctx);
+void* vb_ctx_stream(vb_ctx* ctx);
+
+/* ---- variational family (vb.py:54-65, 148-162) ------------------------ */
+/* x_out[n, d] = sample of q(lambda); n = 0..n-1.  Noise as above (one problem). */
+int vb_family_sample(vb_ctx* ctx, const vb_family* fam, const double* lam,
+                     int64_t n, const vb_noise* noise, double* x_out);
+/* out[n] = log q(x[n, :]; lambda) with all normalising constants. */
+int vb_family_logdensity(vb_ctx* ctx, const vb_family* fam, const double* lam,
+                         const double* x, int64_t n, double* out);
+/* out[n] = log p(x[n, :]); grad_out (nullable) = d log p / dx, [n, D]. */
+int vb_target_logdensity(vb_ctx* ctx, const vb_target* tgt, const double* x,
+                         int64_t n, double* out, double* grad_out);
+
+/* ---- estimators (vb.py:236-266) -------------------------------------- */
+/* One stochastic objective value and gradient at lambda (P = 2D values). */
+int vb_objective_value_grad(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,
+                            const vb_objective* obj, const double* lam,
+                            const vb_noise* noise, double* value, double* grad);
+
+/* ---- device-resident adagrad (vb.py:324-389) -------------------------- */
+/* n_problems independent restarts share (fam, tgt, obj, cfg); init is
+ * [n_problems][P].  Philox streams are noise.stream + problem. */
+int vb_run_create(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,
+                  const vb_objective* obj, const vb_adagrad_config* cfg,
+                  int64_t n_problems, const double* init, vb_run** out);
+/* Advance every problem by n_steps adagrad iterations (lr schedule and
+ * history bookkeeping as vb.py:356-376).  HOST noise: eps covers
+ * [n_problems][n_steps][N][D]. */
+int vb_run_advance(vb_run* run, int64_t n_steps, const vb_noise* noise);
+int vb_run_steps_done(vb_run* run, int64_t* out);
+/* Results (all nullable): lam_out [n_problems][P]; hist_out
+ * [n_problems][n_iters - 3*n_iters/4][P]; values_out [n_problems][n_iters];
+ * smoothed_out [n_problems][P] = mean of the history rows (vb.py:386-387). */
+int vb_run_result(vb_run* run, double* lam_out, double* hist_out,
+                  double* values_out, double* smoothed_out);
+int vb_run_destroy(vb_run* run);
+
+/* One adagrad step (vb.py:364-374) for a caller-supplied gradient (foreign
+ * objectives).  lam [P] and ring [window][P] are DEVICE pointers holding the
+ * optimiser state; step is the 0-based iteration index (ring slot step % window). */
+int vb_adagrad_update(vb_ctx* ctx, int64_t P, double* lam, const double* grad,
+                      double* ring, int32_t window, int64_t step, double lr,
+                      double epsilon);
+
+/* ---- log weights for bounds / PSIS (experiments.py:60-63) ------------ */
+int vb_log_weights(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,
+                   const double* lam, int64_t m, const vb_noise* noise,
+                   double* lw_out, double* samples_out /* nullable, [m, D] */);
+
+/* ---- bounds (bounds.py:142-192, 127-135) ------------------------------ */
+/* out[0] = d_alpha, out[1] = log_norm_bound (ELBO), out[2] = CUBO mean of
+ * rescaled weights, out[3] = its MC standard error, out[4] = ELBO mean,
+ * out[5] = ELBO MC standard error (NaN when elbo supplied), out[6] = log max. */
+int vb_divergence_bound(vb_ctx* ctx, const double* lw, int64_t n, double alpha,
+                        int32_t has_elbo, double elbo, double* out7);
+/* c2 = mean_n sum_d (x - xbar)^2, c4 = mean_n sum_d (x - xbar)^4. */
+int vb_centered_moments(vb_ctx* ctx, const double* x, int64_t n, int64_t d,
+                        double* c2, double* c4);
+/* column means [d] and covariance [d, d] (ddof = 1, np.cov(x.T)) of x [n, d];
+ * d <= 64. */
+int vb_covariance(vb_ctx* ctx, const double* x, int64_t n, int64_t d,
+                  double* mean_out, double* cov_out);
+
+/* ---- PSIS (psis.py:112-395) ------------------------------------------ */
+/* lw [n, m] C order (m columns of n log weights).  lw_out same layout.
+ * k_out [m].  tail_idx_out (nullable) [m, tail_cap]: the tail indices in
+ * ascending order of the tail values (tailinds[x2si]); n_tail_out (nullable) [m]. */
+int vb_psislw(vb_ctx* ctx, const double* lw, int64_t n, int64_t m, double reff,
+              double* lw_out, double* k_out, int64_t* tail_idx_out,
+              int64_t tail_cap, int64_t* n_tail_out);
+/* Zhang-Stephens GPD fit of x[n] (any order).  ks_out / w_out nullable,
+ * length 30 + floor(sqrt(n)); *n_w_out = number of weights kept. */
+int vb_gpdfit(vb_ctx* ctx, const double* x, int64_t n, double* k, double* sigma,
+              double* ks_out, double* w_out, int64_t* n_w_out);
+int vb_gpinv(vb_ctx* ctx, const double* p, int64_t n, double k, double sigma,
+             double* out);
+int vb_sumlogs(vb_ctx* ctx, const double* x, int64_t n, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VIABEL_AMD_H */

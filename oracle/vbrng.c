@@ -1,0 +1,107 @@
+/*
+ * vbrng.c -- ORACLE / TEST INFRASTRUCTURE ONLY.  Never linked into the product.
+ *
+ * Plain-C restatement of the counter-based noise the HIP kernels draw in
+ * VB_NOISE_PHILOX mode, so tests can regenerate the exact draws on the CPU
+ * and compare kernel results against the numpy restatement of the reference
+ * algorithm (oracle/vb_oracle.py) on identical noise.
+ *
+ *  - Philox4x32-10: Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as
+ *    easy as 1, 2, 3", SC'11 (Random123).  Pinned by the Random123 known-answer
+ *    vectors in tests/test_oracle_rng.py.
+ *  - counter = (pair j, sample n, step, stream | purpose << 24), key = seed.
+ *  - normal pair: Box-Muller on 53-bit uniforms u1 in (0,1), u2 in [0,1).
+ *  - t draw: sqrt(df/2) * gauss / sqrt(gamma(df/2)), the structure of numpy's
+ *    legacy standard_t; gamma by Marsaglia & Tsang (2000), proposals from
+ *    purposes 1..64 with 32-bit uniforms.
+ */
+#include <math.h>
+#include <stdint.h>
+
+typedef struct { uint32_t v[4]; } blk;
+
+static blk philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    uint64_t a = (uint64_t)0xD2511F53u * (uint64_t)c0;
+    uint64_t b = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
+    uint32_t y0 = (uint32_t)(b >> 32) ^ c1 ^ k0;
+    uint32_t y1 = (uint32_t)b;
+    uint32_t y2 = (uint32_t)(a >> 32) ^ c3 ^ k1;
+    uint32_t y3 = (uint32_t)a;
+    c0 = y0; c1 = y1; c2 = y2; c3 = y3;
+  }
+  blk o = {{c0, c1, c2, c3}};
+  return o;
+}
+
+void vbo_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  blk b = philox(ctr[0], ctr[1], ctr[2], ctr[3], key[0], key[1]);
+  for (int i = 0; i < 4; ++i) out[i] = b.v[i];
+}
+
+static blk draw(uint64_t seed, uint32_t stream, uint32_t pair, uint32_t n, uint32_t step,
+                uint32_t purpose) {
+  return philox(pair, n, step, (stream & 0x00FFFFFFu) | (purpose << 24), (uint32_t)seed,
+                (uint32_t)(seed >> 32));
+}
+
+static void gauss2(blk w, double* z0, double* z1) {
+  uint64_t a = ((((uint64_t)w.v[1]) << 32) | w.v[0]) >> 11;
+  uint64_t b = ((((uint64_t)w.v[3]) << 32) | w.v[2]) >> 11;
+  double u1 = ((double)a + 0.5) * 0x1p-53;
+  double u2 = (double)b * 0x1p-53;
+  double r = sqrt(-2.0 * log(u1));
+  double th = 2.0 * M_PI * u2;
+  *z0 = r * cos(th);
+  *z1 = r * sin(th);
+}
+
+static void gamma2(uint64_t seed, uint32_t stream, uint32_t pair, uint32_t n, uint32_t step,
+                   double shape, double* ga, double* gb) {
+  double d = shape - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
+  int okA = 0, okB = 0;
+  *ga = d;
+  *gb = d;
+  for (uint32_t k = 0; k < 64u && !(okA && okB); ++k) {
+    blk w = draw(seed, stream, pair, n, step, 1u + k);
+    double u1 = ((double)w.v[0] + 0.5) * 0x1p-32;
+    double u2 = (double)w.v[1] * 0x1p-32;
+    double r = sqrt(-2.0 * log(u1)), th = 2.0 * M_PI * u2;
+    double z[2] = {r * cos(th), r * sin(th)};
+    double u[2] = {((double)w.v[2] + 0.5) * 0x1p-32, ((double)w.v[3] + 0.5) * 0x1p-32};
+    int* ok[2] = {&okA, &okB};
+    double* g[2] = {ga, gb};
+    for (int e = 0; e < 2; ++e) {
+      if (*ok[e]) continue;
+      double v = 1.0 + c * z[e];
+      if (v <= 0.0) continue;
+      v = v * v * v;
+      if (log(u[e]) < 0.5 * z[e] * z[e] + d - d * v + d * log(v)) {
+        *g[e] = d * v;
+        *ok[e] = 1;
+      }
+    }
+  }
+}
+
+/* standardized draws eps[n][D] for one step: family 0 = N(0,1), 1 = t(df) */
+void vbo_fill(uint64_t seed, uint32_t stream, uint32_t step, int64_t nrows, int64_t D, int family,
+              double df, double* eps) {
+  int64_t npairs = (D + 1) / 2;
+  for (int64_t r = 0; r < nrows; ++r) {
+    for (int64_t j = 0; j < npairs; ++j) {
+      double z0, z1;
+      gauss2(draw(seed, stream, (uint32_t)j, (uint32_t)r, step, 0u), &z0, &z1);
+      if (family == 1) {
+        double ga, gb;
+        gamma2(seed, stream, (uint32_t)j, (uint32_t)r, step, df / 2.0, &ga, &gb);
+        double s = sqrt(df / 2.0);
+        z0 = s * z0 / sqrt(ga);
+        z1 = s * z1 / sqrt(gb);
+      }
+      eps[r * D + 2 * j] = z0;
+      if (2 * j + 1 < D) eps[r * D + 2 * j + 1] = z1;
+    }
+  }
+}

@@ -1,0 +1,27 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (runs the HIP kernels)')
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope='session')
+def golden():
+    import numpy as np
+    d = os.path.join(ROOT, 'tests', 'golden')
+    return {k: np.load(os.path.join(d, k + '_golden.npz')) for k in ('bounds', 'psis', 'rng')}

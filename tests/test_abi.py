@@ -1,0 +1,127 @@
+"""C-ABI checks that need no GPU: the library loads, exports every function
+declared in include/viabel_amd.h, the ctypes descriptors match the header's
+struct layouts, and the product fails loudly (no CPU fallback) without a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT, gpu_available
+
+HEADER = os.path.join(ROOT, 'include', 'viabel_amd.h')
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(vb_[a-z0-9_]+)\s*\(', src)))
+
+
+def test_header_declares_the_hot_path():
+    fns = header_functions()
+    for f in ('vb_objective_value_grad', 'vb_run_create', 'vb_run_advance', 'vb_log_weights',
+              'vb_divergence_bound', 'vb_centered_moments', 'vb_psislw', 'vb_gpdfit'):
+        assert f in fns
+
+
+def test_library_exports_every_header_symbol():
+    from viabel_amd import _native
+    lib = _native.lib()
+    missing = [f for f in header_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+    # and the ctypes binding covers all of them
+    assert set(header_functions()) == set(_native._SIGNATURES)
+    assert lib.vb_abi_version() == 1
+
+
+def test_exported_symbols_are_c_linkage():
+    so = os.path.join(ROOT, 'viabel_amd', 'libviabel_amd.so')
+    out = subprocess.check_output(['nm', '-D', '--defined-only', so]).decode()
+    syms = set(re.findall(r' T (vb_[a-z0-9_]+)$', out, flags=re.M))
+    assert set(header_functions()) <= syms
+
+
+def _struct_sizes_from_c():
+    """Compile a tiny C program against the header to get sizeof/offsetof."""
+    import tempfile
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "viabel_amd.h"
+int main(void){
+  printf("%zu %zu %zu %zu %zu\n", sizeof(vb_family), sizeof(vb_target), sizeof(vb_objective),
+         sizeof(vb_noise), sizeof(vb_adagrad_config));
+  printf("%zu %zu %zu\n", offsetof(vb_noise, eps), offsetof(vb_objective, n_samples),
+         offsetof(vb_adagrad_config, epsilon));
+  return 0; }
+'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, 'p.c')
+        exe = os.path.join(d, 'p')
+        open(c, 'w').write(prog)
+        subprocess.check_call(['gcc', '-I', os.path.join(ROOT, 'include'), c, '-o', exe])
+        lines = subprocess.check_output([exe]).decode().split('\n')
+    return [int(v) for v in lines[0].split()], [int(v) for v in lines[1].split()]
+
+
+def test_ctypes_layouts_match_header():
+    from viabel_amd import _native as n
+    sizes, offs = _struct_sizes_from_c()
+    assert sizes == [ctypes.sizeof(n.Family), ctypes.sizeof(n.Target), ctypes.sizeof(n.Objective),
+                     ctypes.sizeof(n.Noise), ctypes.sizeof(n.AdagradConfig)]
+    assert offs == [n.Noise.eps.offset, n.Objective.n_samples.offset,
+                    n.AdagradConfig.epsilon.offset]
+
+
+@pytest.mark.skipif(gpu_available(), reason='checks the no-GPU failure mode')
+def test_no_gpu_fails_loudly():
+    from viabel_amd import _native, vb, targets
+    _native._ctx.clear()
+    with pytest.raises(RuntimeError):
+        _native.Context(0)
+    fam = vb.mean_field_gaussian_variational_family(3)
+    obj = vb.black_box_klvi(fam, targets.isogauss(3), 10)
+    with pytest.raises(RuntimeError):
+        obj(np.zeros(6))
+
+
+def test_api_argument_errors_without_gpu():
+    """Argument validation that the reference performs before any compute."""
+    from viabel_amd import vb, targets
+    with pytest.raises(ValueError, match='df must be greater than 2'):
+        vb.mean_field_t_variational_family(3, 2)
+    fam = vb.mean_field_gaussian_variational_family(3)
+    with pytest.raises(ValueError, match='only p = 2 or 4 supported'):
+        fam.pth_moment(3, np.zeros(6))
+    with pytest.raises(TypeError, match='viabel_amd.targets'):
+        vb.black_box_klvi(fam, lambda x: -0.5 * np.sum(x ** 2, 1), 10)
+    with pytest.raises(ValueError, match='learning rate must be positive'):
+        vb.adagrad_optimize(10, vb.black_box_klvi(fam, targets.isogauss(3), 5), np.zeros(6),
+                            learning_rate=0)
+    with pytest.raises(ValueError, match='initial learning rate must be greater'):
+        list(vb.learning_rate_schedule(10, 0.01, 0.1))
+    tfam = vb.mean_field_t_variational_family(3, 3.5)
+    with pytest.raises(ValueError, match='df must be greater than p'):
+        tfam.pth_moment(4, np.zeros(6))
+
+
+def test_host_side_closed_forms():
+    """entropy / mean_and_cov / pth_moment follow vb.py:59-79, 153-179."""
+    from viabel_amd import vb
+    from oracle import vb_oracle
+    lam = np.array([0.1, -0.3, 0.2, -0.5, 0.4, 0.05])
+    for kind, df in (('gauss', None), ('t', 7.0)):
+        fam = (vb.mean_field_gaussian_variational_family(3) if kind == 'gauss'
+               else vb.mean_field_t_variational_family(3, df))
+        ofam = vb_oracle.Family(kind, 3, df)
+        assert fam.entropy(lam) == pytest.approx(ofam.entropy(lam), rel=1e-15)
+        for p in (2, 4):
+            assert fam.pth_moment(p, lam) == pytest.approx(ofam.pth_moment(p, lam), rel=1e-14)
+        m, c = fam.mean_and_cov(lam)
+        om, oc = ofam.mean_and_cov(lam)
+        np.testing.assert_array_equal(m, om)
+        np.testing.assert_allclose(c, oc, rtol=1e-15)
+        assert fam.var_param_dim == 6

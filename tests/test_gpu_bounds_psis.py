@@ -1,0 +1,158 @@
+"""GPU parity for viabel_amd.bounds and viabel_amd.psis against the reference's
+golden vectors (tests/golden) and the oracle.  Tolerances: bounds 1e-10
+relative (bar: 1e-5); PSIS k 1e-10 (bar: 1e-5), smoothed log weights 1e-11,
+tail order (tailinds[x2si]) bit-exact."""
+import warnings
+
+import numpy as np
+import pytest
+from scipy.special import factorial2
+
+from tests.conftest import gpu_available
+from tests.golden.make_golden import mixture_inputs
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason='needs an MI355X')]
+
+
+def _close(a, b, rtol=1e-10, atol=1e-12):
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=atol)
+
+
+class TestBounds:
+    def test_normal_mixture_notebook(self, golden):
+        import viabel_amd as va
+        g = golden['bounds']
+        samples, lw, q_var = mixture_inputs()
+        mb = lambda order: factorial2(order - 1) ** (1 / order) * np.sqrt(q_var)
+        cases = {
+            'mix_a': va.all_bounds(lw, samples),
+            'mix_b': va.all_bounds(lw, samples, q_var=q_var, log_norm_bound=0),
+            'mix_c': va.all_bounds(lw, moment_bound_fn=mb, q_var=q_var),
+        }
+        for cname, res in cases.items():
+            assert set(res) == {'W1', 'W2', 'mean_error', 'std_error', 'cov_error', 'd2',
+                                'log_norm_bound'}
+            for k, v in res.items():
+                _close(v, g['%s_%s' % (cname, k)])
+
+    @pytest.mark.parametrize('alpha', [1.5, 2.0, 3.0])
+    @pytest.mark.parametrize('elbo', [None, 0.0])
+    def test_divergence(self, golden, alpha, elbo):
+        import viabel_amd as va
+        g = golden['bounds']
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            d, lnb = va.divergence_bound(g['div_lw'], alpha, elbo, return_log_norm_bound=True)
+        tag = 'div_a%g_%s' % (alpha, 'none' if elbo is None else 'zero')
+        _close([d, lnb], g[tag])
+
+    def test_wasserstein_and_cov(self, golden):
+        import viabel_amd as va
+        g = golden['bounds']
+        for tag, s in (('w1d', g['w_s1']), ('w3d', g['w_s3'])):
+            r = va.wasserstein_bounds(5.0, s)
+            _close([r['W1'], r['W2']], g[tag])
+        r = va.all_bounds(g['ab3_lw'], g['w_s3'])
+        for k, v in r.items():
+            _close(v, g['ab3_' + k])
+
+    def test_warnings_and_errors(self, golden):
+        import viabel_amd as va
+        g = golden['bounds']
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter('always')
+            va.divergence_bound(g['warn_lw'])
+        assert [str(x.message) for x in w] == list(g['warn_msgs'])
+        with pytest.raises(ValueError, match='alpha must be greater than 1'):
+            va.divergence_bound(g['warn_lw'], alpha=1.0)
+        with pytest.raises(ValueError, match='must provides samples'):
+            va.wasserstein_bounds(1.0)
+
+    def test_large_sizes_properties(self):
+        """1e7 draws (reference test_bounds.py MC_SAMPLES): closed-form Renyi
+        divergence of two Gaussians within the reference's MC_TOL, and the
+        oracle within 1e-9."""
+        import viabel_amd as va
+        from oracle import bounds_oracle
+        rs = np.random.RandomState(846)
+        var1, var2 = 4.0, 16.0
+        s = rs.randn(10_000_000) * np.sqrt(var2)
+        lw = (-0.5 * s ** 2 / var1 - 0.5 * np.log(var1)) - (-0.5 * s ** 2 / var2 - 0.5 * np.log(var2))
+        d = va.divergence_bound(lw, 2.0, 0.0)
+        od = bounds_oracle.divergence_bound(lw, 2.0, 0.0)
+        _close(d, od, rtol=1e-9)
+        tmp = 2 * var2 - var1
+        expected = -0.5 * np.log(tmp) + np.log(var2) - 0.5 * np.log(var1)
+        assert abs(d - expected) < 5 / np.sqrt(1e7) * (1 + abs(expected))
+
+
+class TestPsis:
+    @pytest.mark.parametrize('case', ['normal1000', 't3_1000', 'n5', 'n128', 'heavy2e4', 'cols'])
+    def test_psislw_golden(self, golden, case):
+        from viabel_amd import psis
+        from oracle import psis_oracle
+        g = golden['psis']
+        lw = g[case + '_in'].copy()
+        out, k = psis.psislw(lw)
+        _close(out, g[case + '_out'], rtol=1e-11, atol=1e-11)
+        _close(np.atleast_1d(k), g[case + '_k'])
+        if lw.ndim == 1:
+            assert np.isscalar(k) or np.ndim(k) == 0
+        # tail order bit-exact vs the oracle's argsort
+        _, _, tails = psis.psislw_with_tail(lw)
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            _, _, otails = psis_oracle.psislw(lw.copy(), return_tail=True)
+        for t, ot in zip(tails, otails):
+            if len(ot) > 4:
+                np.testing.assert_array_equal(t, ot)
+
+    def test_psislw_output_layout(self, golden):
+        from viabel_amd import psis
+        g = golden['psis']
+        lw = g['cols_in'].copy()
+        out, k = psis.psislw(lw)
+        assert out.flags.f_contiguous and out.shape == lw.shape and k.shape == (3,)
+        lwf = np.asfortranarray(g['cols_in'])
+        res, _ = psis.psislw(lwf, overwrite_lw=True)
+        assert res is lwf
+        _close(lwf, g['cols_out'], rtol=1e-11, atol=1e-11)
+
+    def test_gpdfit_gpinv_sumlogs(self, golden):
+        from viabel_amd import psis
+        g = golden['psis']
+        k, sigma, ks, w = psis.gpdfitnew(g['gpd_x'].copy(), return_quadrature=True)
+        _close([k, sigma], g['gpd_k'])
+        _close(ks, g['gpd_ks'])
+        _close(w, g['gpd_w'])
+        p = g['gpinv_p']
+        for tag, (kk, ss) in {'gpinv_pos': (0.4, 1.3), 'gpinv_neg': (-0.3, 2.0),
+                              'gpinv_zero': (1e-18, 0.7), 'gpinv_badsig': (0.2, -1.0)}.items():
+            _close(psis.gpinv(p, kk, ss), g[tag], rtol=1e-13)
+        _close(psis.sumlogs(g['sumlogs_x']), g['sumlogs'][0], rtol=1e-13)
+
+    def test_errors(self):
+        from viabel_amd import psis
+        with pytest.raises(ValueError, match='More than one log-weight'):
+            psis.psislw(np.zeros(1))
+        with pytest.raises(ValueError, match='Invalid input array'):
+            psis.gpdfitnew(np.zeros(1))
+
+    @pytest.mark.parametrize('n', [1_000_000, 2_500_000])
+    def test_full_size(self, n):
+        """The notebooks' sizes (funnel 1e6, eight schools 2.5e6): k within 1e-9,
+        tail order bit-exact, smoothed weights within 1e-11 of the oracle."""
+        from viabel_amd import psis
+        from oracle import psis_oracle
+        rs = np.random.RandomState(n % 997)
+        lw = rs.standard_t(3, n) * 1.3 - 2.0
+        out, k, tails = psis.psislw_with_tail(lw)
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            oout, ok, otails = psis_oracle.psislw(lw.copy(), return_tail=True)
+        _close(k, ok, rtol=1e-9)
+        np.testing.assert_array_equal(tails[0], otails[0])
+        _close(out[:, 0], oout, rtol=1e-11, atol=1e-11)
+        # size-independent property: smoothed weights are normalised
+        assert abs(np.log(np.sum(np.exp(out))) ) < 1e-10

@@ -1,0 +1,269 @@
+"""GPU parity: the HIP estimators / optimiser against the oracle on identical
+noise.  Tolerances (written per test): single estimator calls 1e-10 relative
+(SURVEY §8c asks <= 1e-12 for identical noise; reduction-order and FMA
+differences stay around 1e-14..1e-12); adagrad trajectories <= 1e-7 relative
+over >= 100 steps (the bar is 1e-5)."""
+import numpy as np
+import pytest
+
+from tests.conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason='needs an MI355X')]
+
+FAMS = [('gauss', None), ('t', 40.0), ('t', 8.0)]
+SMALL_TARGETS = [('isogauss', 6), ('mixture', 5), ('funnel', 10), ('eight_schools_ncp', 10),
+                 ('funnel', 2), ('isogauss', 1)]
+
+
+def _mods():
+    from viabel_amd import vb, targets
+    from oracle import vb_oracle, rng_oracle
+    return vb, targets, vb_oracle, rng_oracle
+
+
+def _family(vb, kind, df, D, rng):
+    if kind == 'gauss':
+        return vb.mean_field_gaussian_variational_family(D, rng=rng)
+    return vb.mean_field_t_variational_family(D, df, rng=rng)
+
+
+def _target(targets, name, D):
+    return {'isogauss': lambda: targets.isogauss(D), 'mixture': lambda: targets.mixture(D),
+            'funnel': lambda: targets.funnel(D),
+            'eight_schools_ncp': targets.eight_schools_ncp}[name]()
+
+
+def _lam(D, seed):
+    rs = np.random.RandomState(seed)
+    return np.concatenate([rs.randn(D) * 0.7, rs.randn(D) * 0.3 - 0.2])
+
+
+def _scale(g):
+    return max(1.0, float(np.max(np.abs(g))))
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize('kind,df', FAMS)
+@pytest.mark.parametrize('target,D', SMALL_TARGETS)
+@pytest.mark.parametrize('N', [1, 100, 128, 700])
+def test_klvi_call_numpy_stream(kind, df, target, D, N):
+    """black_box_klvi(fam, p, N)(lam) consumes fam's RandomState(0) like vb.py:239."""
+    vb, targets, vo, _ = _mods()
+    fam = _family(vb, kind, df, D, 'numpy')
+    ofam = vo.Family(kind, D, df)
+    obj = vb.black_box_klvi(fam, _target(targets, target, D), N)
+    for call in range(3):  # the stream continues across calls
+        lam = _lam(D, call)
+        v, g = obj(lam)
+        ov, og = vo.klvi_value_grad(ofam, target, lam, N)
+        assert abs(v - ov) <= 1e-10 * max(1.0, abs(ov))
+        np.testing.assert_allclose(g, og, rtol=1e-10, atol=1e-10 * _scale(og))
+
+
+@pytest.mark.parametrize('kind,df', FAMS)
+@pytest.mark.parametrize('target,D', SMALL_TARGETS)
+@pytest.mark.parametrize('alpha', [2.0, 1.5])
+def test_chivi_call_numpy_stream(kind, df, target, D, alpha):
+    """black_box_chivi draws seed = npr.randint(2**32) from the GLOBAL RNG (vb.py:258)."""
+    vb, targets, vo, _ = _mods()
+    fam = _family(vb, kind, df, D, 'numpy')
+    ofam = vo.Family(kind, D, df)
+    obj = vb.black_box_chivi(alpha, fam, _target(targets, target, D), 128)
+    for call in range(2):
+        lam = _lam(D, 10 + call)
+        np.random.seed(77 + call)
+        v, g = obj(lam)
+        np.random.seed(77 + call)
+        ov, og = vo.chivi_value_grad(ofam, target, lam, 128, alpha)
+        assert abs(v - ov) <= 1e-10 * max(1.0, abs(ov))
+        np.testing.assert_allclose(g, og, rtol=1e-9, atol=1e-9 * _scale(og))
+
+
+@pytest.mark.parametrize('kind,df', FAMS)
+@pytest.mark.parametrize('target', ['isogauss', 'mixture'])
+@pytest.mark.parametrize('D', [17, 1000, 10001])
+def test_klvi_call_wide_separable(kind, df, target, D):
+    """D > 16 with a separable target goes through the column-pair kernel."""
+    vb, targets, vo, _ = _mods()
+    N = 96
+    fam = _family(vb, kind, df, D, 'numpy')
+    ofam = vo.Family(kind, D, df)
+    obj = vb.black_box_klvi(fam, _target(targets, target, D), N)
+    lam = _lam(D, 5)
+    v, g = obj(lam)
+    ov, og = vo.klvi_value_grad(ofam, target, lam, N)
+    assert abs(v - ov) <= 1e-10 * max(1.0, abs(ov))
+    np.testing.assert_allclose(g, og, rtol=1e-10, atol=1e-10 * _scale(og))
+
+
+@pytest.mark.parametrize('kind,df', FAMS)
+@pytest.mark.parametrize('target,D', [('isogauss', 7), ('funnel', 10), ('mixture', 4000)])
+def test_klvi_call_philox_matches_oracle_noise(kind, df, target, D):
+    """Philox mode: the kernel's in-register draws equal the C oracle's draws, so
+    the estimator matches the oracle fed with rng_oracle noise."""
+    vb, targets, vo, ro = _mods()
+    N = 128
+    fam = _family(vb, kind, df, D, 'philox')
+    obj = vb.black_box_klvi(fam, _target(targets, target, D), N)
+    ofam = vo.Family(kind, D, df)
+    for call in range(2):
+        lam = _lam(D, 20 + call)
+        v, g = obj(lam)
+        eps = ro.noise(fam.seed, fam.stream, call, N, D, kind, df or 0.0)
+        ov, og = vo.klvi_value_grad(ofam, target, lam, N, eps=eps)
+        assert abs(v - ov) <= 1e-10 * max(1.0, abs(ov))
+        np.testing.assert_allclose(g, og, rtol=1e-9, atol=1e-9 * _scale(og))
+
+
+# ---------------------------------------------------------------------------
+def _oracle_run(vo, ofam, objective, target, n_iters, init, N, alpha=2.0, eps_fn=None, **kw):
+    step = [0]
+
+    def f(lam):
+        eps = eps_fn(step[0]) if eps_fn else None
+        step[0] += 1
+        if objective == 'klvi':
+            return vo.klvi_value_grad(ofam, target, lam, N, eps=eps)
+        return vo.chivi_value_grad(ofam, target, lam, N, alpha, eps=eps)
+    return vo.adagrad_optimize(n_iters, f, init, **kw)
+
+
+@pytest.mark.parametrize('kind,df', FAMS)
+@pytest.mark.parametrize('objective', ['klvi', 'chivi'])
+@pytest.mark.parametrize('target,D', [('funnel', 10), ('eight_schools_ncp', 10), ('mixture', 3)])
+def test_adagrad_trajectory_numpy_stream(kind, df, objective, target, D):
+    """Device-resident adagrad == reference loop on the same numpy streams,
+    with the funnel notebook's decaying schedule (lr .01 -> .001)."""
+    vb, targets, vo, _ = _mods()
+    N, n_iters = 100, 120
+    fam = _family(vb, kind, df, D, 'numpy')
+    ofam = vo.Family(kind, D, df)
+    init = np.concatenate([np.zeros(D), np.ones(D)])
+    init[1] = -1.0
+    tgt = _target(targets, target, D)
+    obj = (vb.black_box_klvi(fam, tgt, N) if objective == 'klvi'
+           else vb.black_box_chivi(2.0, fam, tgt, N))
+    np.random.seed(4)
+    res = vb.adagrad_optimize(n_iters, obj, init, learning_rate=.01, learning_rate_end=.001)
+    np.random.seed(4)
+    ores = _oracle_run(vo, ofam, objective, target, n_iters, init, N,
+                       learning_rate=.01, learning_rate_end=.001)
+    assert res[1].shape == ores[1].shape == (n_iters - 3 * n_iters // 4, 2 * D)
+    np.testing.assert_allclose(res[1], ores[1], rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(res[0], ores[0], rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(res[2], ores[2], rtol=1e-7, atol=1e-7)
+    assert np.all(res[3] == 0)
+
+
+@pytest.mark.parametrize('kind,df', [('gauss', None), ('t', 40.0)])
+@pytest.mark.parametrize('D', [33, 2000])
+def test_adagrad_trajectory_wide(kind, df, D):
+    """Column-pair persistent kernel: 130 steps (crosses the chunk and window
+    boundaries), constant lr like config 3."""
+    vb, targets, vo, _ = _mods()
+    N, n_iters = 64, 130
+    fam = _family(vb, kind, df, D, 'numpy')
+    ofam = vo.Family(kind, D, df)
+    init = np.concatenate([np.zeros(D), np.ones(D)])
+    obj = vb.black_box_klvi(fam, targets.isogauss(D), N)
+    res = vb.adagrad_optimize(n_iters, obj, init, learning_rate=0.05)
+    ores = _oracle_run(vo, ofam, 'klvi', 'isogauss', n_iters, init, N, learning_rate=0.05)
+    np.testing.assert_allclose(res[1], ores[1], rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(res[2], ores[2], rtol=1e-7, atol=1e-7)
+
+
+@pytest.mark.parametrize('kind,df', [('gauss', None), ('t', 40.0)])
+@pytest.mark.parametrize('target,D', [('isogauss', 3000), ('funnel', 10)])
+def test_adagrad_trajectory_philox(kind, df, target, D):
+    """Philox mode trajectories equal the oracle loop fed with the C-oracle draws."""
+    vb, targets, vo, ro = _mods()
+    N, n_iters = 64, 110
+    fam = _family(vb, kind, df, D, 'philox')
+    ofam = vo.Family(kind, D, df)
+    init = np.concatenate([np.zeros(D), np.ones(D)])
+    obj = vb.black_box_klvi(fam, _target(targets, target, D), N)
+    seed, stream, step0 = fam.seed, fam.stream, fam.step
+    res = vb.adagrad_optimize(n_iters, obj, init, learning_rate=0.02, learning_rate_end=0.005)
+    eps_fn = lambda i: ro.noise(seed, stream, step0 + i, N, D, kind, df or 0.0)
+    ores = _oracle_run(vo, ofam, 'klvi', target, n_iters, init, N, eps_fn=eps_fn,
+                       learning_rate=0.02, learning_rate_end=0.005)
+    np.testing.assert_allclose(res[1], ores[1], rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(res[2], ores[2], rtol=1e-7, atol=1e-7)
+
+
+def test_many_problems_one_launch():
+    """n_problems restarts in one vb_run (one workgroup each) == independent runs."""
+    vb, targets, vo, ro = _mods()
+    from viabel_amd.vb import DeviceRun
+    D, N, n_iters, R = 10, 100, 60, 5
+    fam = vb.mean_field_t_variational_family(D, 40, rng='philox')
+    obj = vb.black_box_klvi(fam, targets.eight_schools_ncp(), N)
+    inits = np.random.RandomState(0).randn(R, 2 * D) * 0.5
+    run = DeviceRun(obj, n_iters, inits, learning_rate=0.01, learning_rate_end=0.001)
+    run.advance_philox(n_iters, seed=9, stream=100, step=0)
+    lam, hist, vals, smooth = run.result()
+    ofam = vo.Family('t', D, 40.0)
+    for r in range(R):
+        eps_fn = lambda i, r=r: ro.noise(9, 100 + r, i, N, D, 't', 40.0)
+        ores = _oracle_run(vo, ofam, 'klvi', 'eight_schools_ncp', n_iters, inits[r], N,
+                           eps_fn=eps_fn, learning_rate=0.01, learning_rate_end=0.001)
+        np.testing.assert_allclose(hist[r], ores[1], rtol=1e-7, atol=1e-9)
+        np.testing.assert_allclose(vals[r], ores[2], rtol=1e-7, atol=1e-7)
+        np.testing.assert_allclose(smooth[r], ores[0], rtol=1e-7, atol=1e-9)
+
+
+def test_foreign_objective_device_update():
+    """A plain Python objective runs with the device adagrad update kernel."""
+    vb, targets, vo, _ = _mods()
+    D = 4
+    ofam_a = vo.Family('gauss', D)
+    ofam_b = vo.Family('gauss', D)
+    f_a = lambda l: vo.klvi_value_grad(ofam_a, 'isogauss', l, 50)
+    f_b = lambda l: vo.klvi_value_grad(ofam_b, 'isogauss', l, 50)
+    init = np.ones(2 * D)
+    res = vb.adagrad_optimize(40, f_a, init, learning_rate=0.1, learning_rate_end=0.01)
+    ores = vo.adagrad_optimize(40, f_b, init, learning_rate=0.1, learning_rate_end=0.01)
+    np.testing.assert_allclose(res[1], ores[1], rtol=1e-12, atol=1e-14)
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize('kind,df', FAMS)
+@pytest.mark.parametrize('D', [3, 10, 100])
+def test_family_sample_and_logdensity(kind, df, D):
+    vb, targets, vo, _ = _mods()
+    fam = _family(vb, kind, df, D, 'numpy')
+    ofam = vo.Family(kind, D, df)
+    lam = _lam(D, 2)
+    x = fam.sample(lam, 500)
+    ox = ofam.sample(lam, 500)
+    np.testing.assert_allclose(x, ox, rtol=1e-14, atol=1e-14)
+    np.testing.assert_allclose(fam.logdensity(x, lam), ofam.logdensity(x, lam), rtol=1e-12)
+    xs = fam.sample(lam, 7, seed=99)
+    np.testing.assert_allclose(xs, ofam.sample(lam, 7, seed=99), rtol=1e-14, atol=1e-14)
+
+
+@pytest.mark.parametrize('target,D', SMALL_TARGETS + [('mixture', 300), ('isogauss', 5000)])
+def test_target_logdensity_and_grad(target, D):
+    vb, targets, vo, _ = _mods()
+    from oracle import targets_oracle
+    x = np.random.RandomState(1).randn(333, D)
+    lp, g = _target(targets, target, D).logdensity_and_grad(x)
+    olp, og = targets_oracle.TARGETS[target](x)
+    np.testing.assert_allclose(lp, olp, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(g, og, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize('kind,df', FAMS)
+@pytest.mark.parametrize('target,D', [('eight_schools_ncp', 10), ('mixture', 2), ('isogauss', 40)])
+def test_log_weights(kind, df, target, D):
+    """experiments.py:60-63 on the device, continuing the family stream."""
+    from viabel_amd import experiments
+    vb, targets, vo, _ = _mods()
+    fam = _family(vb, kind, df, D, 'numpy')
+    ofam = vo.Family(kind, D, df)
+    lam = _lam(D, 6)
+    x, lw = experiments.get_samples_and_log_weights(_target(targets, target, D), fam, lam, 5000)
+    ox, olw = vo.log_weights(ofam, target, lam, 5000)
+    np.testing.assert_allclose(x, ox, rtol=1e-14, atol=1e-14)
+    np.testing.assert_allclose(lw, olw, rtol=1e-11, atol=1e-11)

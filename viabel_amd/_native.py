@@ -1,0 +1,203 @@
+"""ctypes binding of libviabel_amd.so (include/viabel_amd.h).
+
+The product path has no CPU fallback: if the HIP library is missing, or no
+GPU is visible when a computation is requested, this module raises.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libviabel_amd.so')
+
+VB_OK, VB_EINVAL, VB_EDEVICE, VB_ENOMEM, VB_EUNSUPPORTED = 0, -1, -2, -3, -4
+FAMILY_MF_GAUSSIAN, FAMILY_MF_T = 0, 1
+TARGET_ISOGAUSS, TARGET_MIXTURE, TARGET_FUNNEL, TARGET_EIGHT_SCHOOLS_NCP = 0, 1, 2, 3
+OBJ_KLVI, OBJ_CHIVI = 0, 1
+NOISE_HOST, NOISE_PHILOX = 0, 1
+
+c_double_p = ctypes.POINTER(ctypes.c_double)
+c_int64_p = ctypes.POINTER(ctypes.c_int64)
+
+
+class Family(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int32), ('reserved', ctypes.c_int32),
+                ('dim', ctypes.c_int64), ('df', ctypes.c_double)]
+
+
+class Target(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int32), ('reserved', ctypes.c_int32), ('dim', ctypes.c_int64)]
+
+
+class Objective(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int32), ('reserved', ctypes.c_int32),
+                ('alpha', ctypes.c_double), ('n_samples', ctypes.c_int64)]
+
+
+class Noise(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int32), ('stream', ctypes.c_uint32),
+                ('seed', ctypes.c_uint64), ('step', ctypes.c_uint64), ('eps', c_double_p)]
+
+
+class AdagradConfig(ctypes.Structure):
+    _fields_ = [('n_iters', ctypes.c_int64), ('window', ctypes.c_int32),
+                ('reserved', ctypes.c_int32), ('learning_rate', ctypes.c_double),
+                ('learning_rate_end', ctypes.c_double), ('epsilon', ctypes.c_double)]
+
+
+P = ctypes.POINTER
+_SIGNATURES = {
+    'vb_abi_version': ([], ctypes.c_int),
+    'vb_last_error': ([], ctypes.c_char_p),
+    'vb_ctx_create': ([ctypes.c_int, ctypes.c_void_p, P(ctypes.c_void_p)], ctypes.c_int),
+    'vb_ctx_destroy': ([ctypes.c_void_p], ctypes.c_int),
+    'vb_ctx_synchronize': ([ctypes.c_void_p], ctypes.c_int),
+    'vb_ctx_stream': ([ctypes.c_void_p], ctypes.c_void_p),
+    'vb_family_sample': ([ctypes.c_void_p, P(Family), c_double_p, ctypes.c_int64, P(Noise),
+                          c_double_p], ctypes.c_int),
+    'vb_family_logdensity': ([ctypes.c_void_p, P(Family), c_double_p, c_double_p,
+                              ctypes.c_int64, c_double_p], ctypes.c_int),
+    'vb_target_logdensity': ([ctypes.c_void_p, P(Target), c_double_p, ctypes.c_int64,
+                              c_double_p, c_double_p], ctypes.c_int),
+    'vb_objective_value_grad': ([ctypes.c_void_p, P(Family), P(Target), P(Objective),
+                                 c_double_p, P(Noise), c_double_p, c_double_p], ctypes.c_int),
+    'vb_run_create': ([ctypes.c_void_p, P(Family), P(Target), P(Objective), P(AdagradConfig),
+                       ctypes.c_int64, c_double_p, P(ctypes.c_void_p)], ctypes.c_int),
+    'vb_run_advance': ([ctypes.c_void_p, ctypes.c_int64, P(Noise)], ctypes.c_int),
+    'vb_run_steps_done': ([ctypes.c_void_p, c_int64_p], ctypes.c_int),
+    'vb_run_result': ([ctypes.c_void_p, c_double_p, c_double_p, c_double_p, c_double_p],
+                      ctypes.c_int),
+    'vb_run_destroy': ([ctypes.c_void_p], ctypes.c_int),
+    'vb_adagrad_update': ([ctypes.c_void_p, ctypes.c_int64, c_double_p, c_double_p, c_double_p,
+                           ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_double],
+                          ctypes.c_int),
+    'vb_log_weights': ([ctypes.c_void_p, P(Family), P(Target), c_double_p, ctypes.c_int64,
+                        P(Noise), c_double_p, c_double_p], ctypes.c_int),
+    'vb_divergence_bound': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_double,
+                             ctypes.c_int32, ctypes.c_double, c_double_p], ctypes.c_int),
+    'vb_centered_moments': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,
+                             c_double_p, c_double_p], ctypes.c_int),
+    'vb_covariance': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, c_double_p,
+                       c_double_p], ctypes.c_int),
+    'vb_psislw': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
+                   c_double_p, c_double_p, c_int64_p, ctypes.c_int64, c_int64_p], ctypes.c_int),
+    'vb_gpdfit': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, c_double_p, c_double_p,
+                   c_double_p, c_double_p, c_int64_p], ctypes.c_int),
+    'vb_gpinv': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                  c_double_p], ctypes.c_int),
+    'vb_sumlogs': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, c_double_p], ctypes.c_int),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load libviabel_amd.so (raises ImportError when it was not built)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError(
+                        'viabel_amd: HIP library %s not found; build it with '
+                        '`python -c "import __graft_entry__ as g; g.build()"` or '
+                        '`make -C viabel_amd/csrc`' % LIB_PATH)
+                L = ctypes.CDLL(LIB_PATH)
+                for name, (args, res) in _SIGNATURES.items():
+                    fn = getattr(L, name)
+                    fn.argtypes = args
+                    fn.restype = res
+                _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc == VB_OK:
+        return
+    msg = lib().vb_last_error().decode('utf-8', 'replace')
+    if rc == VB_EINVAL:
+        raise ValueError(msg)
+    if rc == VB_ENOMEM:
+        raise MemoryError(msg)
+    if rc == VB_EUNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(msg)
+
+
+class Context:
+    """One vb_ctx (device + HIP stream)."""
+
+    def __init__(self, device=0, stream=None):
+        h = ctypes.c_void_p()
+        check(lib().vb_ctx_create(int(device), stream, ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def synchronize(self):
+        check(lib().vb_ctx_synchronize(self.handle))
+
+    @property
+    def stream(self):
+        return lib().vb_ctx_stream(self.handle)
+
+    def __del__(self):
+        try:
+            if self.handle and _lib is not None:
+                _lib.vb_ctx_destroy(self.handle)
+        except Exception:
+            pass
+        self.handle = None
+
+
+_ctx = {}
+_default_device = [int(os.environ.get('VIABEL_AMD_DEVICE', '0'))]
+
+
+def set_device(device):
+    _default_device[0] = int(device)
+
+
+def context(device=None):
+    d = _default_device[0] if device is None else int(device)
+    c = _ctx.get(d)
+    if c is None:
+        c = Context(d)
+        _ctx[d] = c
+    return c
+
+
+def dptr(a):
+    """double* of a C-contiguous float64 numpy array, or of a torch tensor's data."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        if a.dtype != np.float64 or not a.flags.c_contiguous:
+            raise TypeError('expected a C-contiguous float64 array')
+        return a.ctypes.data_as(c_double_p)
+    # torch tensor (device or host): pass the raw pointer
+    return ctypes.cast(ctypes.c_void_p(a.data_ptr()), c_double_p)
+
+
+def i64ptr(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(c_int64_p)
+
+
+def as_f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+NAN = float('nan')
+
+
+def use_stream(device, stream_handle):
+    """Make the default context of `device` launch on an existing HIP stream
+    (e.g. torch.cuda.current_stream().cuda_stream) so torch events time it."""
+    c = Context(device, ctypes.c_void_p(stream_handle))
+    _ctx[int(device)] = c
+    _default_device[0] = int(device)
+    return c

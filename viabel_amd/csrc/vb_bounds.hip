@@ -1,0 +1,357 @@
+// vb_bounds.hip — importance-weight reductions behind viabel.bounds.
+//
+//   divergence_bound         viabel/bounds.py:142-180
+//   mean_and_check_mc_error  viabel/bounds.py:183-192   (mean, std/sqrt(n))
+//   wasserstein moments      viabel/bounds.py:127-135   (centred 2p-th moments)
+//   np.cov(samples.T)        viabel/bounds.py:55-56
+//
+// Every reduction is a fixed-order two-level tree (per-block partials, then one
+// block combines them in block order), so results are bitwise reproducible
+// run to run.  Passes follow numpy's two-pass definitions (np.std centres on
+// the mean first) rather than one-pass power sums, which cancel badly.
+#include "vb_device.hpp"
+#include "vb_internal.hpp"
+
+using namespace vbd;
+
+namespace vbk {
+
+namespace {
+
+constexpr int kRedBlocks = 1024;
+
+__device__ __forceinline__ double block_sum1(double v, double* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const double r = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ double block_max1(double v, double* red) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const double r = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  __syncthreads();
+  return r;
+}
+
+int red_grid(long long n) {
+  long long g = (n + 2047) / 2048;
+  if (g < 1) g = 1;
+  if (g > kRedBlocks) g = kRedBlocks;
+  return (int)g;
+}
+
+// pass 1: per-block max and sum of lw
+__global__ __launch_bounds__(256) void lw_max_sum_kernel(const double* lw, long long n,
+                                                         double* part) {
+  __shared__ double red[4];
+  double m = -INFINITY, s = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const double v = lw[i];
+    m = fmax(m, v);
+    s += v;
+  }
+  m = block_max1(m, red);
+  s = block_sum1(s, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = m;
+    part[2 * blockIdx.x + 1] = s;
+  }
+}
+
+// combine pass-1 partials: sc[0] = max, sc[1] = mean
+__global__ __launch_bounds__(256) void lw_max_sum_final(const double* part, int nb, long long n,
+                                                        double* sc) {
+  __shared__ double red[4];
+  double m = -INFINITY, s = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 256) {
+    m = fmax(m, part[2 * b]);
+    s += part[2 * b + 1];
+  }
+  m = block_max1(m, red);
+  s = block_sum1(s, red);
+  if (threadIdx.x == 0) {
+    sc[0] = m;
+    sc[1] = s / (double)n;
+  }
+}
+
+// pass 2: sum of r = exp(lw - max)^alpha and of (lw - mean)^2
+__global__ __launch_bounds__(256) void lw_rescaled_kernel(const double* lw, long long n,
+                                                          double alpha, const double* sc,
+                                                          double* part) {
+  __shared__ double red[4];
+  const double mx = sc[0], mean = sc[1];
+  double s = 0.0, q = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const double v = lw[i];
+    const double e = exp(v - mx);
+    s += (alpha == 2.0) ? e * e : pow(e, alpha);
+    const double dv = v - mean;
+    q += dv * dv;
+  }
+  s = block_sum1(s, red);
+  q = block_sum1(q, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s;
+    part[2 * blockIdx.x + 1] = q;
+  }
+}
+
+__global__ __launch_bounds__(256) void sum2_final(const double* part, int nb, long long n,
+                                                  double* out2) {
+  __shared__ double red[4];
+  double a = 0.0, b = 0.0;
+  for (int k = threadIdx.x; k < nb; k += 256) {
+    a += part[2 * k];
+    b += part[2 * k + 1];
+  }
+  a = block_sum1(a, red);
+  b = block_sum1(b, red);
+  if (threadIdx.x == 0) {
+    out2[0] = a / (double)n;
+    out2[1] = b / (double)n;
+  }
+}
+
+// pass 3: sum of (r - mean_r)^2
+__global__ __launch_bounds__(256) void lw_rdev_kernel(const double* lw, long long n, double alpha,
+                                                      const double* sc, const double* m2,
+                                                      double* part) {
+  __shared__ double red[4];
+  const double mx = sc[0], mr = m2[0];
+  double q = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const double e = exp(lw[i] - mx);
+    const double r = (alpha == 2.0) ? e * e : pow(e, alpha);
+    q += (r - mr) * (r - mr);
+  }
+  q = block_sum1(q, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = q;
+    part[2 * blockIdx.x + 1] = 0.0;
+  }
+}
+
+// out7: d_alpha, elbo, mean_r, se_r, mean_lw, se_lw, log max
+__global__ void divergence_final(const double* part, int nb, long long n, double alpha,
+                                 int has_elbo, double elbo, const double* sc, const double* m2,
+                                 double* out7) {
+  __shared__ double red[4];
+  double q = 0.0;
+  for (int k = threadIdx.x; k < nb; k += 256) q += part[2 * k];
+  q = block_sum1(q, red);
+  if (threadIdx.x == 0) {
+    const double sq = sqrt((double)n);
+    const double mean_r = m2[0];
+    const double se_r = sqrt(q / (double)n) / sq;
+    const double cubo = log(mean_r) / alpha + sc[0];
+    const double mean_lw = sc[1];
+    const double se_lw = has_elbo ? NAN : sqrt(m2[1]) / sq;
+    const double lnb = has_elbo ? elbo : mean_lw;
+    out7[0] = alpha / (alpha - 1.0) * (cubo - lnb);
+    out7[1] = lnb;
+    out7[2] = mean_r;
+    out7[3] = se_r;
+    out7[4] = mean_lw;
+    out7[5] = se_lw;
+    out7[6] = sc[0];
+  }
+}
+
+// ---- column means of x [n][d] ---------------------------------------------
+// grid (row chunks, column tiles of 64); block = 64 columns x 4 row lanes
+__global__ __launch_bounds__(256) void col_sum_kernel(const double* x, long long n, long long d,
+                                                      long long rows_per_chunk, double* part) {
+  __shared__ double red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const long long col = (long long)blockIdx.y * 64 + cl;
+  const long long r0 = (long long)blockIdx.x * rows_per_chunk;
+  const long long r1 = min(n, r0 + rows_per_chunk);
+  double s = 0.0;
+  if (col < d)
+    for (long long r = r0 + rl; r < r1; r += 4) s += x[r * d + col];
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && col < d)
+    part[(long long)blockIdx.x * d + col] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+}
+
+__global__ __launch_bounds__(256) void col_final_kernel(const double* part, int nchunk,
+                                                        long long n, long long d, double* mean) {
+  const long long col = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (col >= d) return;
+  double s = 0.0;
+  for (int k = 0; k < nchunk; ++k) s += part[(long long)k * d + col];
+  mean[col] = s / (double)n;
+}
+
+// 1-D fast path: mean of x[n]
+__global__ __launch_bounds__(256) void flat_sum_kernel(const double* x, long long n,
+                                                       double* part) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256)
+    s += x[i];
+  s = block_sum1(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void flat_final_kernel(const double* part, int nb, long long n,
+                                                         double* mean) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int k = threadIdx.x; k < nb; k += 256) s += part[k];
+  s = block_sum1(s, red);
+  if (threadIdx.x == 0) mean[0] = s / (double)n;
+}
+
+// ---- centred power sums over all elements ---------------------------------
+__global__ __launch_bounds__(256) void cpow_kernel(const double* x, long long n, long long d,
+                                                   const double* mean, double* part) {
+  __shared__ double red[4];
+  const long long tot = n * d;
+  double s2 = 0.0, s4 = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < tot;
+       i += (long long)gridDim.x * 256) {
+    const double v = x[i] - mean[d == 1 ? 0 : i % d];
+    const double v2 = v * v;
+    s2 += v2;
+    s4 += v2 * v2;
+  }
+  s2 = block_sum1(s2, red);
+  s4 = block_sum1(s4, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s2;
+    part[2 * blockIdx.x + 1] = s4;
+  }
+}
+
+// ---- covariance: one block row per (chunk, pair) ----------------------------
+__global__ __launch_bounds__(256) void cov_kernel(const double* x, long long n, long long d,
+                                                  const double* mean, long long rows_per_chunk,
+                                                  double* part) {
+  __shared__ double red[4];
+  const int pair = blockIdx.y;
+  // pair -> (i, j), i <= j, row-major upper triangle
+  int i = 0, rem = pair;
+  while (rem >= d - i) {
+    rem -= (int)(d - i);
+    ++i;
+  }
+  const int j = i + rem;
+  const long long r0 = (long long)blockIdx.x * rows_per_chunk;
+  const long long r1 = min(n, r0 + rows_per_chunk);
+  const double mi = mean[i], mj = mean[j];
+  double s = 0.0;
+  for (long long r = r0 + threadIdx.x; r < r1; r += 256)
+    s += (x[r * d + i] - mi) * (x[r * d + j] - mj);
+  s = block_sum1(s, red);
+  if (threadIdx.x == 0) part[(long long)blockIdx.x * gridDim.y + pair] = s;
+}
+
+__global__ __launch_bounds__(256) void cov_final_kernel(const double* part, int nchunk, int npairs,
+                                                        long long n, long long d, double* cov) {
+  const int pair = blockIdx.x * 256 + threadIdx.x;
+  if (pair >= npairs) return;
+  int i = 0, rem = pair;
+  while (rem >= d - i) {
+    rem -= (int)(d - i);
+    ++i;
+  }
+  const int j = i + rem;
+  double s = 0.0;
+  for (int k = 0; k < nchunk; ++k) s += part[(long long)k * npairs + pair];
+  const double c = s / (double)(n - 1);
+  cov[(long long)i * d + j] = c;
+  cov[(long long)j * d + i] = c;
+}
+
+int col_chunks(long long n, long long* rows_per_chunk) {
+  long long nc = (n + 4095) / 4096;
+  if (nc < 1) nc = 1;
+  if (nc > 512) nc = 512;
+  *rows_per_chunk = (n + nc - 1) / nc;
+  return (int)nc;
+}
+
+hipError_t means(const double* x, long long n, long long d, double* scratch, double* mean,
+                 hipStream_t s) {
+  if (d == 1) {
+    const int g = red_grid(n);
+    hipLaunchKernelGGL(flat_sum_kernel, dim3(g), dim3(256), 0, s, x, n, scratch);
+    hipLaunchKernelGGL(flat_final_kernel, dim3(1), dim3(256), 0, s, scratch, g, n, mean);
+  } else {
+    long long rpc;
+    const int nc = col_chunks(n, &rpc);
+    hipLaunchKernelGGL(col_sum_kernel, dim3(nc, (unsigned)((d + 63) / 64)), dim3(256), 0, s, x, n,
+                       d, rpc, scratch);
+    hipLaunchKernelGGL(col_final_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s,
+                       scratch, nc, n, d, mean);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+size_t bounds_scratch_doubles(long long n, long long d) {
+  long long rpc;
+  const int nc = col_chunks(n, &rpc);
+  const long long npairs = d * (d + 1) / 2;
+  long long need = 4LL * kRedBlocks + 16;
+  need = need > nc * d + 16 ? need : nc * d + 16;
+  if (d <= kCovDMax && need < nc * npairs + 16) need = nc * npairs + 16;
+  return (size_t)need + 2 * (size_t)d + 16;
+}
+
+hipError_t bounds_divergence(const double* lw, long long n, double alpha, int has_elbo,
+                             double elbo, double* scratch, double* out7, hipStream_t s) {
+  const int g = red_grid(n);
+  double* part = scratch;
+  double* sc = scratch + 2 * kRedBlocks;
+  double* m2 = sc + 4;
+  hipLaunchKernelGGL(lw_max_sum_kernel, dim3(g), dim3(256), 0, s, lw, n, part);
+  hipLaunchKernelGGL(lw_max_sum_final, dim3(1), dim3(256), 0, s, part, g, n, sc);
+  hipLaunchKernelGGL(lw_rescaled_kernel, dim3(g), dim3(256), 0, s, lw, n, alpha, sc, part);
+  hipLaunchKernelGGL(sum2_final, dim3(1), dim3(256), 0, s, part, g, n, m2);
+  hipLaunchKernelGGL(lw_rdev_kernel, dim3(g), dim3(256), 0, s, lw, n, alpha, sc, m2, part);
+  hipLaunchKernelGGL(divergence_final, dim3(1), dim3(256), 0, s, part, g, n, alpha, has_elbo, elbo,
+                     sc, m2, out7);
+  return hipGetLastError();
+}
+
+hipError_t bounds_centered_moments(const double* x, long long n, long long d, double* scratch,
+                                   double* out2, hipStream_t s) {
+  // scratch layout: [mean (d)] [partials]
+  double* mean = scratch;
+  double* part = scratch + d + 8;
+  hipError_t e = means(x, n, d, part, mean, s);
+  if (e != hipSuccess) return e;
+  const int g = red_grid(n * d);
+  hipLaunchKernelGGL(cpow_kernel, dim3(g), dim3(256), 0, s, x, n, d, mean, part);
+  hipLaunchKernelGGL(sum2_final, dim3(1), dim3(256), 0, s, part, g, n, out2);
+  return hipGetLastError();
+}
+
+hipError_t bounds_covariance(const double* x, long long n, long long d, double* scratch,
+                             double* mean, double* cov, hipStream_t s) {
+  hipError_t e = means(x, n, d, scratch, mean, s);
+  if (e != hipSuccess) return e;
+  long long rpc;
+  const int nc = col_chunks(n, &rpc);
+  const int npairs = (int)(d * (d + 1) / 2);
+  hipLaunchKernelGGL(cov_kernel, dim3(nc, npairs), dim3(256), 0, s, x, n, d, mean, rpc, scratch);
+  hipLaunchKernelGGL(cov_final_kernel, dim3((npairs + 255) / 256), dim3(256), 0, s, scratch, nc,
+                     npairs, n, d, cov);
+  return hipGetLastError();
+}
+
+}  // namespace vbk

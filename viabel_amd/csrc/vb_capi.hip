@@ -1,0 +1,854 @@
+// vb_capi.hip — the extern "C" boundary declared in include/viabel_amd.h.
+//
+// Host-side responsibilities: argument validation with the reference's error
+// conditions, host/device pointer detection + staging, device-resident
+// optimiser state (vb_run), chunked launches, thread-local error strings.
+#include "../../include/viabel_amd.h"
+#include "vb_internal.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define VB_HIP(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(VB_EDEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                  __FILE__, __LINE__);                                                \
+  } while (0)
+
+#define VB_TRY(expr)             \
+  do {                           \
+    int rc_ = (expr);            \
+    if (rc_ != VB_OK) return rc_; \
+  } while (0)
+
+bool is_device_ptr(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t at;
+  hipError_t e = hipPointerGetAttributes(&at, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged ||
+         at.type == hipMemoryTypeUnified;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int reserve(size_t bytes) {
+    if (bytes <= cap) return VB_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (bytes == 0) return VB_OK;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(VB_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    }
+    cap = bytes;
+    return VB_OK;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  double* d() const { return static_cast<double*>(p); }
+};
+
+}  // namespace
+
+struct vb_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  DevBuf slot[12];
+  std::vector<void*> pending_frees;
+};
+
+namespace {
+
+// An input argument: device pointer used directly, host pointer staged.
+struct In {
+  const double* d = nullptr;
+  int stage(vb_ctx* c, int s, const double* p, size_t count) {
+    if (!p || count == 0) {
+      d = p;
+      return VB_OK;
+    }
+    if (is_device_ptr(p)) {
+      d = p;
+      return VB_OK;
+    }
+    VB_TRY(c->slot[s].reserve(count * sizeof(double)));
+    VB_HIP(hipMemcpyAsync(c->slot[s].p, p, count * sizeof(double), hipMemcpyHostToDevice,
+                          c->stream));
+    d = c->slot[s].d();
+    return VB_OK;
+  }
+};
+
+// An output argument: device pointer written directly, host pointer copied back.
+template <class T>
+struct OutT {
+  T* user = nullptr;
+  T* d = nullptr;
+  size_t count = 0;
+  bool host = false;
+  int stage(vb_ctx* c, int s, T* p, size_t n) {
+    user = p;
+    count = n;
+    if (!p || n == 0) {
+      d = p;
+      return VB_OK;
+    }
+    if (is_device_ptr(p)) {
+      d = p;
+      return VB_OK;
+    }
+    host = true;
+    VB_TRY(c->slot[s].reserve(n * sizeof(T)));
+    d = static_cast<T*>(c->slot[s].p);
+    return VB_OK;
+  }
+  int finish(vb_ctx* c) {
+    if (host && count)
+      VB_HIP(hipMemcpyAsync(user, d, count * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+    return VB_OK;
+  }
+};
+using Out = OutT<double>;
+
+int sync(vb_ctx* c) {
+  VB_HIP(hipStreamSynchronize(c->stream));
+  return VB_OK;
+}
+
+int check_ctx(vb_ctx* c) {
+  if (!c) return fail(VB_EINVAL, "null vb_ctx");
+  VB_HIP(hipSetDevice(c->device));
+  return VB_OK;
+}
+
+struct FamInfo {
+  int kind;
+  int D;
+  double df, t_scale, shape, t_const;
+};
+
+int check_family(const vb_family* f, FamInfo* o) {
+  if (!f) return fail(VB_EINVAL, "null vb_family");
+  if (f->kind != VB_FAMILY_MF_GAUSSIAN && f->kind != VB_FAMILY_MF_T)
+    return fail(VB_EUNSUPPORTED, "family kind %d is not implemented on the device", f->kind);
+  if (f->dim < 1 || f->dim > (1LL << 30)) return fail(VB_EINVAL, "invalid dimension %lld", (long long)f->dim);
+  o->kind = f->kind;
+  o->D = (int)f->dim;
+  o->df = f->df;
+  o->t_scale = o->shape = o->t_const = 0.0;
+  if (f->kind == VB_FAMILY_MF_T) {
+    if (!(f->df > 2)) return fail(VB_EINVAL, "df must be greater than 2");  // vb.py:141-142
+    o->t_scale = std::sqrt(f->df / 2.0);
+    o->shape = f->df / 2.0;
+    // scipy.stats.t._logpdf constant: gammaln((df+1)/2) - gammaln(df/2) - 0.5*log(df*pi)
+    o->t_const = std::lgamma(0.5 * (f->df + 1.0)) - std::lgamma(0.5 * f->df) -
+                 0.5 * std::log(f->df * M_PI);
+  }
+  return VB_OK;
+}
+
+int check_target(const vb_target* t, int D) {
+  if (!t) return fail(VB_EINVAL, "null vb_target");
+  if (t->kind < VB_TARGET_ISOGAUSS || t->kind > VB_TARGET_EIGHT_SCHOOLS_NCP)
+    return fail(VB_EUNSUPPORTED, "target kind %d is not implemented on the device", t->kind);
+  if (t->dim != D)
+    return fail(VB_EINVAL, "target dimension %lld does not match family dimension %d",
+                (long long)t->dim, D);
+  if (t->kind == VB_TARGET_FUNNEL && (D < 2 || D > vbk::kBlockDMax))
+    return fail(VB_EUNSUPPORTED, "funnel target needs 2 <= D <= %d", vbk::kBlockDMax);
+  if (t->kind == VB_TARGET_EIGHT_SCHOOLS_NCP && D != 10)
+    return fail(VB_EINVAL, "eight_schools_ncp target has dimension 10, got %d", D);
+  return VB_OK;
+}
+
+void key_of(uint64_t seed, uint32_t* k0, uint32_t* k1) {
+  *k0 = (uint32_t)(seed & 0xffffffffu);
+  *k1 = (uint32_t)(seed >> 32);
+}
+
+vbk::LrSched make_sched(long long n, double lr, double lr_end) {
+  vbk::LrSched s{};
+  s.lr = lr;
+  s.has_end = !std::isnan(lr_end);
+  s.lr_end = s.has_end ? lr_end : 0.0;
+  if (s.has_end) {
+    // vb.py:332-335, same expression order as the reference
+    s.b = ((double)n * lr_end) / (2.0 * (lr - lr_end));
+    s.a = lr * s.b;
+    s.start = n / 4;
+    s.end = (3 * n) / 4;
+  }
+  return s;
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+int vb_abi_version(void) { return VB_ABI_VERSION; }
+
+const char* vb_last_error(void) { return g_err.c_str(); }
+
+int vb_ctx_create(int device, void* hip_stream, vb_ctx** out) {
+  if (!out) return fail(VB_EINVAL, "null output pointer");
+  *out = nullptr;
+  int n = 0;
+  VB_HIP(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(VB_EINVAL, "device %d out of range (%d devices)", device, n);
+  VB_HIP(hipSetDevice(device));
+  vb_ctx* c = new (std::nothrow) vb_ctx();
+  if (!c) return fail(VB_ENOMEM, "out of host memory");
+  c->device = device;
+  if (hip_stream) {
+    c->stream = static_cast<hipStream_t>(hip_stream);
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete c;
+      return fail(VB_EDEVICE, "hipStreamCreate failed: %s", hipGetErrorString(e));
+    }
+    c->own_stream = true;
+  }
+  *out = c;
+  return VB_OK;
+}
+
+int vb_ctx_destroy(vb_ctx* c) {
+  if (!c) return VB_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (c->own_stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return VB_OK;
+}
+
+int vb_ctx_synchronize(vb_ctx* c) {
+  VB_TRY(check_ctx(c));
+  return sync(c);
+}
+
+void* vb_ctx_stream(vb_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+// ---------------------------------------------------------------------------
+int vb_family_sample(vb_ctx* c, const vb_family* fam, const double* lam, int64_t n,
+                     const vb_noise* noise, double* x_out) {
+  VB_TRY(check_ctx(c));
+  FamInfo fi;
+  VB_TRY(check_family(fam, &fi));
+  if (!lam || !x_out || !noise || n < 0) return fail(VB_EINVAL, "null argument");
+  const size_t nd = (size_t)n * fi.D;
+  In dl, dn;
+  Out dx;
+  VB_TRY(dl.stage(c, 0, lam, 2 * (size_t)fi.D));
+  if (noise->kind == VB_NOISE_HOST) {
+    if (!noise->eps) return fail(VB_EINVAL, "host noise requires eps");
+    VB_TRY(dn.stage(c, 1, noise->eps, nd));
+  }
+  VB_TRY(dx.stage(c, 2, x_out, nd));
+  uint32_t k0, k1;
+  key_of(noise->seed, &k0, &k1);
+  VB_HIP(vbk::launch_sample(fi.kind, fi.D, n, dl.d, fi.t_scale, fi.shape,
+                            noise->kind == VB_NOISE_HOST ? dn.d : nullptr, k0, k1, noise->stream,
+                            (uint32_t)noise->step, dx.d, c->stream));
+  VB_TRY(dx.finish(c));
+  return sync(c);
+}
+
+int vb_family_logdensity(vb_ctx* c, const vb_family* fam, const double* lam, const double* x,
+                         int64_t n, double* out) {
+  VB_TRY(check_ctx(c));
+  FamInfo fi;
+  VB_TRY(check_family(fam, &fi));
+  if (!lam || !x || !out || n < 0) return fail(VB_EINVAL, "null argument");
+  In dl, dxx;
+  Out dout;
+  VB_TRY(dl.stage(c, 0, lam, 2 * (size_t)fi.D));
+  VB_TRY(dxx.stage(c, 1, x, (size_t)n * fi.D));
+  VB_TRY(dout.stage(c, 2, out, (size_t)n));
+  VB_HIP(vbk::launch_family_logdensity(fi.kind, fi.D, n, dl.d, fi.df, fi.t_const, dxx.d, dout.d,
+                                       c->stream));
+  VB_TRY(dout.finish(c));
+  return sync(c);
+}
+
+int vb_target_logdensity(vb_ctx* c, const vb_target* tgt, const double* x, int64_t n,
+                         double* out, double* grad_out) {
+  VB_TRY(check_ctx(c));
+  if (!tgt) return fail(VB_EINVAL, "null target");
+  VB_TRY(check_target(tgt, (int)tgt->dim));
+  if (!x || !out || n < 0) return fail(VB_EINVAL, "null argument");
+  const int D = (int)tgt->dim;
+  In dxx;
+  Out dout, dg;
+  VB_TRY(dxx.stage(c, 0, x, (size_t)n * D));
+  VB_TRY(dout.stage(c, 1, out, (size_t)n));
+  VB_TRY(dg.stage(c, 2, grad_out, grad_out ? (size_t)n * D : 0));
+  VB_HIP(vbk::launch_target_logdensity(tgt->kind, D, n, dxx.d, dout.d, dg.d, c->stream));
+  VB_TRY(dout.finish(c));
+  VB_TRY(dg.finish(c));
+  return sync(c);
+}
+
+// ---------------------------------------------------------------------------
+int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tgt,
+                            const vb_objective* obj, const double* lam, const vb_noise* noise,
+                            double* value, double* grad) {
+  VB_TRY(check_ctx(c));
+  FamInfo fi;
+  VB_TRY(check_family(fam, &fi));
+  VB_TRY(check_target(tgt, fi.D));
+  if (!obj || !lam || !noise || !value || !grad) return fail(VB_EINVAL, "null argument");
+  if (obj->n_samples < 1 || obj->n_samples > (1LL << 31))
+    return fail(VB_EINVAL, "n_samples must be positive");
+  if (obj->kind == VB_OBJ_CHIVI && !(obj->alpha > 0))
+    return fail(VB_EINVAL, "alpha must be positive");
+  const int D = fi.D, N = (int)obj->n_samples;
+  const size_t P = 2 * (size_t)D;
+  const bool host = noise->kind == VB_NOISE_HOST;
+  if (host && !noise->eps) return fail(VB_EINVAL, "host noise requires eps");
+  uint32_t k0, k1;
+  key_of(noise->seed, &k0, &k1);
+  In dl, dn;
+  Out dg;
+  VB_TRY(dl.stage(c, 0, lam, P));
+  if (host) VB_TRY(dn.stage(c, 1, noise->eps, (size_t)N * D));
+  VB_TRY(dg.stage(c, 2, grad, P));
+  // device copy of lam that the kernels may read (they do not write in emit mode)
+  VB_TRY(c->slot[3].reserve(P * sizeof(double)));
+  VB_HIP(hipMemcpyAsync(c->slot[3].p, dl.d, P * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  double* dval;
+  VB_TRY(c->slot[4].reserve(sizeof(double) * 2));
+  dval = c->slot[4].d();
+
+  const bool sep = vbk::target_separable(tgt->kind) && obj->kind == VB_OBJ_KLVI;
+  if (sep && D > vbk::kBlockDMax) {
+    vbk::SepArgs a{};
+    a.D = D;
+    a.N = N;
+    a.W = 1;
+    a.n_pairs = (D + 1) / 2;
+    a.n_steps = 1;
+    a.emit_grad = 1;
+    a.step0 = 0;
+    a.hist_start = 1LL << 62;
+    a.rng_step0 = (long long)noise->step;
+    a.n_waves = a.n_pairs;
+    a.t_scale = fi.t_scale;
+    a.shape = fi.shape;
+    a.lam = c->slot[3].d();
+    VB_TRY(c->slot[5].reserve(sizeof(double) * a.n_waves));
+    a.vpart = c->slot[5].d();
+    a.grad = dg.d;
+    a.noise = host ? dn.d : nullptr;
+    a.k0 = k0;
+    a.k1 = k1;
+    a.stream = noise->stream;
+    VB_HIP(vbk::launch_sep(fi.kind, tgt->kind, host, a, c->stream));
+    const double c0 = fi.kind == VB_FAMILY_MF_T ? 0.0 : 0.5 * D * (1.0 + std::log(2 * M_PI));
+    VB_HIP(vbk::launch_sep_values(a.vpart, 1, a.n_waves, c0, dval, c->stream));
+  } else if (D <= vbk::kBlockDMax) {
+    vbk::BlockArgs a{};
+    a.D = D;
+    a.N = N;
+    a.W = 1;
+    a.P = (int)P;
+    a.n_steps = 1;
+    a.emit_grad = 1;
+    a.chivi = obj->kind == VB_OBJ_CHIVI;
+    a.step0 = 0;
+    a.hist_start = 1LL << 62;
+    a.n_iters = 1;
+    a.n_hist = 0;
+    a.rng_step0 = (long long)noise->step;
+    a.alpha = obj->alpha;
+    a.t_scale = fi.t_scale;
+    a.shape = fi.shape;
+    a.t_const = fi.t_const;
+    a.df = fi.df;
+    a.lam = c->slot[3].d();
+    a.ring = nullptr;
+    a.values = dval;
+    a.grad = dg.d;
+    a.noise = host ? dn.d : nullptr;
+    a.k0 = k0;
+    a.k1 = k1;
+    a.stream = noise->stream;
+    VB_HIP(vbk::launch_block(fi.kind, tgt->kind, host, a, 1, c->stream));
+  } else {
+    return fail(VB_EUNSUPPORTED,
+                "objective %d with target %d at D=%d is not implemented on the device "
+                "(non-separable targets and CHIVI need D <= %d)",
+                obj->kind, tgt->kind, D, vbk::kBlockDMax);
+  }
+  VB_HIP(hipMemcpyAsync(value, dval, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  VB_TRY(dg.finish(c));
+  return sync(c);
+}
+
+// ---------------------------------------------------------------------------
+}  // extern "C"
+
+struct vb_run {
+  vb_ctx* ctx = nullptr;
+  FamInfo fi{};
+  int tgt = 0, obj = 0;
+  double alpha = 2.0;
+  int N = 0, W = 10;
+  long long nprob = 1, n_iters = 0, hist_start = 0, n_hist = 0, done = 0;
+  double eps = 0.1;
+  vbk::LrSched sched{};
+  bool sep = false;
+  int n_waves = 0;
+  int max_chunk = 256;
+  DevBuf lam, ring, hist, values, vpart, noise, smooth;
+};
+
+extern "C" {
+
+int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const vb_objective* obj,
+                  const vb_adagrad_config* cfg, int64_t n_problems, const double* init,
+                  vb_run** out) {
+  VB_TRY(check_ctx(c));
+  if (!out) return fail(VB_EINVAL, "null output pointer");
+  *out = nullptr;
+  FamInfo fi;
+  VB_TRY(check_family(fam, &fi));
+  VB_TRY(check_target(tgt, fi.D));
+  if (!obj || !cfg || !init) return fail(VB_EINVAL, "null argument");
+  if (!(cfg->learning_rate > 0)) return fail(VB_EINVAL, "learning rate must be positive");
+  if (!std::isnan(cfg->learning_rate_end) && cfg->learning_rate <= cfg->learning_rate_end)
+    return fail(VB_EINVAL, "initial learning rate must be greater than final learning rate");
+  if (cfg->window < 1 || cfg->window > 64) return fail(VB_EINVAL, "window must be in [1, 64]");
+  if (cfg->n_iters < 0) return fail(VB_EINVAL, "n_iters must be non-negative");
+  if (n_problems < 1) return fail(VB_EINVAL, "n_problems must be positive");
+  if (obj->n_samples < 1 || obj->n_samples > (1LL << 31))
+    return fail(VB_EINVAL, "n_samples must be positive");
+  const int D = fi.D;
+  const bool sep = vbk::target_separable(tgt->kind) && obj->kind == VB_OBJ_KLVI &&
+                   (D > vbk::kBlockDMax);
+  if (!sep && D > vbk::kBlockDMax)
+    return fail(VB_EUNSUPPORTED,
+                "device adagrad for objective %d / target %d needs D <= %d (got %d)", obj->kind,
+                tgt->kind, vbk::kBlockDMax, D);
+  if (sep && n_problems != 1)
+    return fail(VB_EUNSUPPORTED, "wide (D > %d) runs hold one problem per vb_run", vbk::kBlockDMax);
+
+  vb_run* r = new (std::nothrow) vb_run();
+  if (!r) return fail(VB_ENOMEM, "out of host memory");
+  r->ctx = c;
+  r->fi = fi;
+  r->tgt = tgt->kind;
+  r->obj = obj->kind;
+  r->alpha = obj->alpha;
+  r->N = (int)obj->n_samples;
+  r->W = cfg->window;
+  r->nprob = n_problems;
+  r->n_iters = cfg->n_iters;
+  r->hist_start = (3 * cfg->n_iters) / 4;
+  r->n_hist = cfg->n_iters - r->hist_start;
+  r->eps = cfg->epsilon;
+  r->sched = make_sched(cfg->n_iters, cfg->learning_rate, cfg->learning_rate_end);
+  r->sep = sep;
+  r->n_waves = (D + 1) / 2;
+  const size_t P = 2 * (size_t)D;
+  auto bail = [&](int rc) {
+    delete r;
+    return rc;
+  };
+  int rc;
+  if ((rc = r->lam.reserve(sizeof(double) * P * n_problems)) != VB_OK) return bail(rc);
+  if ((rc = r->ring.reserve(sizeof(double) * P * r->W * n_problems)) != VB_OK) return bail(rc);
+  if ((rc = r->hist.reserve(sizeof(double) * P * std::max<long long>(r->n_hist, 1) * n_problems)) != VB_OK)
+    return bail(rc);
+  if ((rc = r->values.reserve(sizeof(double) * std::max<long long>(r->n_iters, 1) * n_problems)) != VB_OK)
+    return bail(rc);
+  if ((rc = r->smooth.reserve(sizeof(double) * P * n_problems)) != VB_OK) return bail(rc);
+  if (sep && (rc = r->vpart.reserve(sizeof(double) * r->n_waves * r->max_chunk)) != VB_OK)
+    return bail(rc);
+  In di;
+  if ((rc = di.stage(c, 0, init, P * n_problems)) != VB_OK) return bail(rc);
+  hipError_t e = hipMemcpyAsync(r->lam.p, di.d, sizeof(double) * P * n_problems,
+                                hipMemcpyDeviceToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(r->ring.p, 0, sizeof(double) * P * r->W * n_problems, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return bail(fail(VB_EDEVICE, "run init failed: %s", hipGetErrorString(e)));
+  *out = r;
+  return VB_OK;
+}
+
+int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
+  if (!r) return fail(VB_EINVAL, "null vb_run");
+  vb_ctx* c = r->ctx;
+  VB_TRY(check_ctx(c));
+  if (!noise) return fail(VB_EINVAL, "null noise");
+  if (n_steps < 0 || r->done + n_steps > r->n_iters)
+    return fail(VB_EINVAL, "advance(%lld) past n_iters=%lld (done %lld)", (long long)n_steps,
+                (long long)r->n_iters, (long long)r->done);
+  if (n_steps == 0) return VB_OK;
+  const bool host = noise->kind == VB_NOISE_HOST;
+  const int D = r->fi.D, N = r->N;
+  const size_t P = 2 * (size_t)D;
+  const size_t per_step = (size_t)N * D;
+  if (host) {
+    if (!noise->eps) return fail(VB_EINVAL, "host noise requires eps");
+    const size_t tot = per_step * n_steps * r->nprob;
+    if (is_device_ptr(noise->eps)) {
+      // used in place
+    } else {
+      VB_TRY(r->noise.reserve(tot * sizeof(double)));
+      VB_HIP(hipMemcpyAsync(r->noise.p, noise->eps, tot * sizeof(double), hipMemcpyHostToDevice,
+                            c->stream));
+    }
+  }
+  const double* noise_base =
+      host ? (is_device_ptr(noise->eps) ? noise->eps : r->noise.d()) : nullptr;
+  uint32_t k0, k1;
+  key_of(noise->seed, &k0, &k1);
+
+  if (r->sep) {
+    long long off = 0;
+    while (off < n_steps) {
+      const int cs = (int)std::min<long long>(r->max_chunk, n_steps - off);
+      vbk::SepArgs a{};
+      a.D = D;
+      a.N = N;
+      a.W = r->W;
+      a.n_pairs = r->n_waves;
+      a.n_steps = cs;
+      a.emit_grad = 0;
+      a.step0 = r->done + off;
+      a.hist_start = r->hist_start;
+      a.rng_step0 = (long long)noise->step + off;
+      a.n_waves = r->n_waves;
+      a.t_scale = r->fi.t_scale;
+      a.shape = r->fi.shape;
+      a.eps = r->eps;
+      a.lr = r->sched;
+      a.lam = r->lam.d();
+      a.ring = r->ring.d();
+      a.hist = r->hist.d();
+      a.vpart = r->vpart.d();
+      a.grad = nullptr;
+      a.noise = host ? noise_base + (size_t)off * per_step : nullptr;
+      a.k0 = k0;
+      a.k1 = k1;
+      a.stream = noise->stream;
+      VB_HIP(vbk::launch_sep(r->fi.kind, r->tgt, host, a, c->stream));
+      const double c0 = r->fi.kind == VB_FAMILY_MF_T ? 0.0 : 0.5 * D * (1.0 + std::log(2 * M_PI));
+      VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, c0, r->values.d() + a.step0, c->stream));
+      off += cs;
+    }
+  } else {
+    vbk::BlockArgs a{};
+    a.D = D;
+    a.N = N;
+    a.W = r->W;
+    a.P = (int)P;
+    a.n_steps = (int)n_steps;
+    a.emit_grad = 0;
+    a.chivi = r->obj == VB_OBJ_CHIVI;
+    a.step0 = r->done;
+    a.hist_start = r->hist_start;
+    a.n_iters = r->n_iters;
+    a.n_hist = r->n_hist;
+    a.rng_step0 = (long long)noise->step;
+    a.alpha = r->alpha;
+    a.t_scale = r->fi.t_scale;
+    a.shape = r->fi.shape;
+    a.t_const = r->fi.t_const;
+    a.df = r->fi.df;
+    a.eps = r->eps;
+    a.lr = r->sched;
+    a.lam = r->lam.d();
+    a.ring = r->ring.d();
+    a.hist = r->hist.d();
+    a.values = r->values.d();
+    a.grad = nullptr;
+    a.noise = noise_base;
+    a.k0 = k0;
+    a.k1 = k1;
+    a.stream = noise->stream;
+    VB_HIP(vbk::launch_block(r->fi.kind, r->tgt, host, a, (int)r->nprob, c->stream));
+  }
+  r->done += n_steps;
+  // host noise staging buffer is reused by the next call: finish before returning
+  if (host) return sync(c);
+  return VB_OK;
+}
+
+int vb_run_steps_done(vb_run* r, int64_t* out) {
+  if (!r || !out) return fail(VB_EINVAL, "null argument");
+  *out = r->done;
+  return VB_OK;
+}
+
+int vb_run_result(vb_run* r, double* lam_out, double* hist_out, double* values_out,
+                  double* smoothed_out) {
+  if (!r) return fail(VB_EINVAL, "null vb_run");
+  vb_ctx* c = r->ctx;
+  VB_TRY(check_ctx(c));
+  const size_t P = 2 * (size_t)r->fi.D;
+  auto copy_out = [&](double* dst, const void* src, size_t n) -> int {
+    if (!dst || n == 0) return VB_OK;
+    VB_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDefault, c->stream));
+    return VB_OK;
+  };
+  VB_TRY(copy_out(lam_out, r->lam.p, P * r->nprob));
+  VB_TRY(copy_out(hist_out, r->hist.p, P * r->n_hist * r->nprob));
+  VB_TRY(copy_out(values_out, r->values.p, (size_t)r->n_iters * r->nprob));
+  if (smoothed_out) {
+    if (r->n_hist > 0) {
+      VB_HIP(vbk::launch_row_mean(r->hist.d(), r->n_hist, (long long)P, r->nprob, r->smooth.d(),
+                                  c->stream));
+      VB_TRY(copy_out(smoothed_out, r->smooth.p, P * r->nprob));
+    } else {
+      // np.mean of an empty history is NaN (with a RuntimeWarning) in the reference
+      std::vector<double> nanv(P * r->nprob, std::nan(""));
+      VB_HIP(hipMemcpyAsync(smoothed_out, nanv.data(), nanv.size() * sizeof(double),
+                            hipMemcpyDefault, c->stream));
+      return sync(c);
+    }
+  }
+  return sync(c);
+}
+
+int vb_run_destroy(vb_run* r) {
+  if (!r) return VB_OK;
+  if (r->ctx) {
+    (void)hipSetDevice(r->ctx->device);
+    (void)hipStreamSynchronize(r->ctx->stream);
+  }
+  delete r;
+  return VB_OK;
+}
+
+int vb_adagrad_update(vb_ctx* c, int64_t P, double* lam, const double* grad, double* ring,
+                      int32_t window, int64_t step, double lr, double epsilon) {
+  VB_TRY(check_ctx(c));
+  if (!lam || !grad || !ring || P < 1 || window < 1 || step < 0)
+    return fail(VB_EINVAL, "invalid argument");
+  if (!is_device_ptr(lam) || !is_device_ptr(ring))
+    return fail(VB_EINVAL, "vb_adagrad_update keeps lam and ring on the device: pass device pointers");
+  In dg;
+  VB_TRY(dg.stage(c, 0, grad, (size_t)P));
+  VB_HIP(vbk::launch_adagrad_update(P, lam, dg.d, ring, window, step, lr, epsilon, c->stream));
+  return sync(c);
+}
+
+// ---------------------------------------------------------------------------
+int vb_log_weights(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const double* lam,
+                   int64_t m, const vb_noise* noise, double* lw_out, double* samples_out) {
+  VB_TRY(check_ctx(c));
+  FamInfo fi;
+  VB_TRY(check_family(fam, &fi));
+  VB_TRY(check_target(tgt, fi.D));
+  if (!lam || !noise || !lw_out || m < 0) return fail(VB_EINVAL, "null argument");
+  if (!vbk::target_separable(tgt->kind) && fi.D > vbk::kBlockDMax)
+    return fail(VB_EUNSUPPORTED, "log weights for target %d need D <= %d", tgt->kind, vbk::kBlockDMax);
+  const bool host = noise->kind == VB_NOISE_HOST;
+  if (host && !noise->eps) return fail(VB_EINVAL, "host noise requires eps");
+  In dl, dn;
+  Out dlw, dxs;
+  VB_TRY(dl.stage(c, 0, lam, 2 * (size_t)fi.D));
+  if (host) VB_TRY(dn.stage(c, 1, noise->eps, (size_t)m * fi.D));
+  VB_TRY(dlw.stage(c, 2, lw_out, (size_t)m));
+  VB_TRY(dxs.stage(c, 3, samples_out, samples_out ? (size_t)m * fi.D : 0));
+  uint32_t k0, k1;
+  key_of(noise->seed, &k0, &k1);
+  VB_HIP(vbk::launch_log_weights(fi.kind, tgt->kind, fi.D, m, dl.d, fi.t_scale, fi.shape, fi.df,
+                                 fi.t_const, host ? dn.d : nullptr, k0, k1, noise->stream,
+                                 (uint32_t)noise->step, dlw.d, dxs.d, c->stream));
+  VB_TRY(dlw.finish(c));
+  VB_TRY(dxs.finish(c));
+  return sync(c);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int vb_divergence_bound(vb_ctx* c, const double* lw, int64_t n, double alpha, int32_t has_elbo,
+                        double elbo, double* out7) {
+  VB_TRY(check_ctx(c));
+  if (!lw || !out7) return fail(VB_EINVAL, "null argument");
+  if (!(alpha > 1)) return fail(VB_EINVAL, "alpha must be greater than 1");  // bounds.py:166-167
+  if (n < 1) return fail(VB_EINVAL, "log_weights must be non-empty");
+  In dlw;
+  VB_TRY(dlw.stage(c, 0, lw, (size_t)n));
+  VB_TRY(c->slot[1].reserve(sizeof(double) * vbk::bounds_scratch_doubles(n, 1)));
+  Out o;
+  VB_TRY(o.stage(c, 2, out7, 7));
+  VB_HIP(vbk::bounds_divergence(dlw.d, n, alpha, has_elbo, elbo, c->slot[1].d(), o.d, c->stream));
+  VB_TRY(o.finish(c));
+  return sync(c);
+}
+
+int vb_centered_moments(vb_ctx* c, const double* x, int64_t n, int64_t d, double* c2,
+                        double* c4) {
+  VB_TRY(check_ctx(c));
+  if (!x || !c2 || !c4 || n < 1 || d < 1) return fail(VB_EINVAL, "invalid argument");
+  In dx;
+  VB_TRY(dx.stage(c, 0, x, (size_t)n * d));
+  VB_TRY(c->slot[1].reserve(sizeof(double) * vbk::bounds_scratch_doubles(n, d)));
+  VB_TRY(c->slot[2].reserve(sizeof(double) * 2));
+  VB_HIP(vbk::bounds_centered_moments(dx.d, n, d, c->slot[1].d(), c->slot[2].d(), c->stream));
+  double h[2];
+  VB_HIP(hipMemcpyAsync(h, c->slot[2].p, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  VB_TRY(sync(c));
+  *c2 = h[0];
+  *c4 = h[1];
+  return VB_OK;
+}
+
+int vb_covariance(vb_ctx* c, const double* x, int64_t n, int64_t d, double* mean_out,
+                  double* cov_out) {
+  VB_TRY(check_ctx(c));
+  if (!x || !cov_out || n < 2 || d < 1) return fail(VB_EINVAL, "invalid argument");
+  if (d > vbk::kCovDMax)
+    return fail(VB_EUNSUPPORTED, "device covariance supports d <= %d (got %lld)", vbk::kCovDMax,
+                (long long)d);
+  In dx;
+  VB_TRY(dx.stage(c, 0, x, (size_t)n * d));
+  VB_TRY(c->slot[1].reserve(sizeof(double) * vbk::bounds_scratch_doubles(n, d)));
+  Out dm, dc;
+  VB_TRY(c->slot[4].reserve(sizeof(double) * d));
+  double* mdev = c->slot[4].d();
+  VB_TRY(dm.stage(c, 5, mean_out, mean_out ? (size_t)d : 0));
+  VB_TRY(dc.stage(c, 2, cov_out, (size_t)d * d));
+  VB_HIP(vbk::bounds_covariance(dx.d, n, d, c->slot[1].d(), mdev, dc.d, c->stream));
+  if (mean_out) VB_HIP(hipMemcpyAsync(dm.d, mdev, sizeof(double) * d, hipMemcpyDeviceToDevice, c->stream));
+  VB_TRY(dm.finish(c));
+  VB_TRY(dc.finish(c));
+  return sync(c);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int vb_psislw(vb_ctx* c, const double* lw, int64_t n, int64_t m, double reff, double* lw_out,
+              double* k_out, int64_t* tail_idx_out, int64_t tail_cap, int64_t* n_tail_out) {
+  VB_TRY(check_ctx(c));
+  if (!lw || !lw_out || !k_out || m < 1) return fail(VB_EINVAL, "invalid argument");
+  if (n <= 1) return fail(VB_EINVAL, "More than one log-weight needed.");  // psis.py:143-144
+  // cutoff_ind = -ceil(min(0.2 n, 3 sqrt(n / Reff))) - 1   (psis.py:157)
+  const double mt_f = std::ceil(std::fmin(0.2 * (double)n, 3.0 * std::sqrt((double)n / reff)));
+  const long long Mt = (long long)mt_f;
+  if (Mt > vbk::psis_tail_max())
+    return fail(VB_EUNSUPPORTED, "PSIS tail of %lld draws exceeds the device sort capacity %lld",
+                Mt, vbk::psis_tail_max());
+  if (tail_idx_out && tail_cap < Mt) return fail(VB_EINVAL, "tail_cap must be >= %lld", Mt);
+  In dlw;
+  VB_TRY(dlw.stage(c, 0, lw, (size_t)n * m));
+  Out dout, dk;
+  VB_TRY(dout.stage(c, 1, lw_out, (size_t)n * m));
+  VB_TRY(dk.stage(c, 2, k_out, (size_t)m));
+  VB_TRY(c->slot[3].reserve(vbk::psis_scratch_bytes()));
+  OutT<long long> dti, dnt;
+  VB_TRY(dti.stage(c, 4, reinterpret_cast<long long*>(tail_idx_out),
+                   tail_idx_out ? (size_t)tail_cap * m : 0));
+  VB_TRY(dnt.stage(c, 5, reinterpret_cast<long long*>(n_tail_out), n_tail_out ? (size_t)m : 0));
+  for (int64_t col = 0; col < m; ++col) {
+    VB_HIP(vbk::psis_column(dlw.d + col, dout.d + col, n, m, Mt, c->slot[3].p, dk.d + col,
+                            dti.d ? dti.d + (size_t)col * tail_cap : nullptr,
+                            dnt.d ? dnt.d + col : nullptr, c->stream));
+  }
+  VB_TRY(dout.finish(c));
+  VB_TRY(dk.finish(c));
+  VB_TRY(dti.finish(c));
+  VB_TRY(dnt.finish(c));
+  return sync(c);
+}
+
+int vb_gpdfit(vb_ctx* c, const double* x, int64_t n, double* k, double* sigma, double* ks_out,
+              double* w_out, int64_t* n_w_out) {
+  VB_TRY(check_ctx(c));
+  if (!x || !k || !sigma) return fail(VB_EINVAL, "null argument");
+  if (n <= 1) return fail(VB_EINVAL, "Invalid input array.");  // psis.py:250-251
+  if (n > vbk::psis_tail_max())
+    return fail(VB_EUNSUPPORTED, "gpdfit of %lld values exceeds the device sort capacity %lld",
+                (long long)n, vbk::psis_tail_max());
+  const int m = 30 + (int)std::sqrt((double)n);
+  In dx;
+  VB_TRY(dx.stage(c, 0, x, (size_t)n));
+  VB_TRY(c->slot[3].reserve(vbk::psis_scratch_bytes()));
+  Out dks, dw;
+  VB_TRY(dks.stage(c, 1, ks_out, ks_out ? (size_t)m : 0));
+  VB_TRY(dw.stage(c, 2, w_out, w_out ? (size_t)m : 0));
+  VB_TRY(c->slot[4].reserve(sizeof(double) * 4));
+  VB_HIP(vbk::psis_gpdfit(dx.d, n, c->slot[3].p, c->slot[4].d(), dks.d, dw.d, c->stream));
+  double h[4];
+  VB_HIP(hipMemcpyAsync(h, c->slot[4].p, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  VB_TRY(dks.finish(c));
+  VB_TRY(dw.finish(c));
+  VB_TRY(sync(c));
+  *k = h[0];
+  *sigma = h[1];
+  if (n_w_out) {
+    long long nk;
+    std::memcpy(&nk, &h[3], sizeof nk);
+    *n_w_out = nk;
+  }
+  return VB_OK;
+}
+
+int vb_gpinv(vb_ctx* c, const double* p, int64_t n, double k, double sigma, double* out) {
+  VB_TRY(check_ctx(c));
+  if (!p || !out || n < 0) return fail(VB_EINVAL, "invalid argument");
+  In dp;
+  Out dout;
+  VB_TRY(dp.stage(c, 0, p, (size_t)n));
+  VB_TRY(dout.stage(c, 1, out, (size_t)n));
+  VB_HIP(vbk::psis_gpinv(dp.d, n, k, sigma, dout.d, c->stream));
+  VB_TRY(dout.finish(c));
+  return sync(c);
+}
+
+int vb_sumlogs(vb_ctx* c, const double* x, int64_t n, double* out) {
+  VB_TRY(check_ctx(c));
+  if (!x || !out || n < 1) return fail(VB_EINVAL, "invalid argument");
+  In dx;
+  VB_TRY(dx.stage(c, 0, x, (size_t)n));
+  VB_TRY(c->slot[3].reserve(vbk::psis_scratch_bytes()));
+  VB_TRY(c->slot[4].reserve(sizeof(double)));
+  VB_HIP(vbk::psis_sumlogs(dx.d, n, c->slot[3].p, c->slot[4].d(), c->stream));
+  VB_HIP(hipMemcpyAsync(out, c->slot[4].p, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  return sync(c);
+}
+
+}  // extern "C"

@@ -1,0 +1,237 @@
+// vb_device.hpp — device building blocks shared by the gfx950 kernels.
+//
+//  * Philox4x32-10 counter RNG (Salmon et al., SC'11), counter layout
+//      c0 = column pair j, c1 = sample n, c2 = step, c3 = stream | purpose<<24
+//    key = (seed lo, seed hi).  Purpose 0 = standard-normal pairs, purpose
+//    1+k = k-th Marsaglia-Tsang gamma proposal.  The layout makes every draw
+//    addressable, so kernels regenerate noise instead of storing it, and any
+//    tiling of (n, d) produces the same draws.
+//  * normal pair: Box-Muller on two 53-bit uniforms (u1 in (0,1), u2 in [0,1)).
+//  * t draws follow numpy's legacy standard_t structure
+//    sqrt(df/2) * gauss / sqrt(gamma(df/2)) (numpy legacy distributions.c),
+//    with gamma by Marsaglia-Tsang (shape >= 1, which df > 2 guarantees).
+//  * target log densities with gradients.
+//
+// Everything is fp64; the build never uses fast-math (PSIS needs IEEE inf).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vbd {
+
+constexpr double kLog2Pi = 1.8378770664093454835606594728112;  // log(2*pi)
+constexpr double kLn2 = 0.69314718055994530941723212145818;
+
+struct u4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                     uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+  }
+  return u4{c0, c1, c2, c3};
+}
+
+struct Rng {
+  uint32_t k0, k1;      // key
+  uint32_t stream;      // 24-bit stream id (restart / family instance)
+  __device__ __forceinline__ u4 draw(uint32_t pair, uint32_t sample, uint32_t step,
+                                     uint32_t purpose) const {
+    return philox(pair, sample, step, (stream & 0x00FFFFFFu) | (purpose << 24), k0, k1);
+  }
+};
+
+// Two standard normals from one Philox block.
+__device__ __forceinline__ void normal_pair(u4 w, double& z0, double& z1) {
+  const uint64_t a = ((((uint64_t)w.y) << 32) | w.x) >> 11;
+  const uint64_t b = ((((uint64_t)w.w) << 32) | w.z) >> 11;
+  const double u1 = ((double)a + 0.5) * 0x1p-53;
+  const double u2 = (double)b * 0x1p-53;
+  const double r = sqrt(-2.0 * log(u1));
+  double s, c;
+  sincospi(2.0 * u2, &s, &c);
+  z0 = r * c;
+  z1 = r * s;
+}
+
+// Gamma(shape) draws for the two elements of a column pair (Marsaglia-Tsang,
+// ACM TOMS 26(3) 2000).  Proposal k uses Philox purpose 1+k; each proposal
+// block gives two 32-bit-uniform Box-Muller normals and two uniforms.
+__device__ __forceinline__ void gamma_pair(const Rng& rng, uint32_t pair, uint32_t sample,
+                                           uint32_t step, double shape, double& ga,
+                                           double& gb) {
+  const double d = shape - 1.0 / 3.0;
+  const double c = 1.0 / sqrt(9.0 * d);
+  bool da = false, db = false;
+  ga = d;
+  gb = d;
+  for (uint32_t k = 0; k < 64u && !(da && db); ++k) {
+    const u4 w = rng.draw(pair, sample, step, 1u + k);
+    const double u1 = ((double)w.x + 0.5) * 0x1p-32;
+    const double u2 = (double)w.y * 0x1p-32;
+    const double r = sqrt(-2.0 * log(u1));
+    double s, cs;
+    sincospi(2.0 * u2, &s, &cs);
+    const double za = r * cs, zb = r * s;
+    const double ua = ((double)w.z + 0.5) * 0x1p-32;
+    const double ub = ((double)w.w + 0.5) * 0x1p-32;
+    if (!da) {
+      double v = 1.0 + c * za;
+      if (v > 0.0) {
+        v = v * v * v;
+        if (log(ua) < 0.5 * za * za + d - d * v + d * log(v)) {
+          ga = d * v;
+          da = true;
+        }
+      }
+    }
+    if (!db) {
+      double v = 1.0 + c * zb;
+      if (v > 0.0) {
+        v = v * v * v;
+        if (log(ub) < 0.5 * zb * zb + d - d * v + d * log(v)) {
+          gb = d * v;
+          db = true;
+        }
+      }
+    }
+  }
+}
+
+// ---- wave-level helpers (wave64) -------------------------------------------
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const uint64_t b = __double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)b, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// numpy's logaddexp (npy_logaddexp): equal args -> x + log 2.
+__device__ __forceinline__ double logaddexp(double x, double y) {
+  if (x == y) return x + kLn2;
+  const double t = x - y;
+  if (t > 0) return x + log1p(exp(-t));
+  if (t <= 0) return y + log1p(exp(t));
+  return t;  // NaN
+}
+
+// ---- targets -----------------------------------------------------------------
+// Separable targets expose a per-coordinate log density + derivative (lp1);
+// every target exposes a row evaluation (row) for D <= kRowMax.
+
+struct IsoGauss {  // N(0, I): log p = sum_d -x_d^2/2 - log(2 pi)/2
+  static constexpr bool kSeparable = true;
+  __device__ __forceinline__ static double lp1(double x, double& g) {
+    g = -x;
+    return -0.5 * x * x - 0.5 * kLog2Pi;
+  }
+};
+
+// normal-mixture.ipynb cell 2: logaddexp(N(x;-2,1), N(x;2,1)) - log 2, per coordinate.
+struct Mixture {
+  static constexpr bool kSeparable = true;
+  __device__ __forceinline__ static double lp1(double x, double& g) {
+    const double a = -0.5 * (x + 2.0) * (x + 2.0) - 0.5 * kLog2Pi;
+    const double b = -0.5 * (x - 2.0) * (x - 2.0) - 0.5 * kLog2Pi;
+    // posterior weight of the +2 component: 1 / (1 + exp(a - b)), a - b = -4x
+    const double wb = 1.0 / (1.0 + exp(a - b));
+    g = -(x + 2.0) + 4.0 * wb;
+    return logaddexp(a, b) - kLn2;
+  }
+};
+
+// funnel-distribution.ipynb cell 2, generalised to D: x[1] = log sigma ~ N(0, 1.35^2),
+// every other coordinate ~ N(0, exp(log sigma)^2).
+struct Funnel {
+  static constexpr bool kSeparable = false;
+  template <int DMAX>
+  __device__ __forceinline__ static double row(const double* x, double* g, int D) {
+    constexpr double s0 = 1.35;
+    const double v = x[1];
+    const double zv = v / s0;
+    double lp = -0.5 * zv * zv - log(s0) - 0.5 * kLog2Pi;
+    double gv = -zv / s0;
+    const double scale = exp(v);
+    const double inv_s2 = exp(-2.0 * v);
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      if (d < D && d != 1) {
+        const double z = x[d] / scale;
+        lp += -0.5 * z * z - v - 0.5 * kLog2Pi;
+        g[d] = -x[d] * inv_s2;
+        gv += z * z - 1.0;
+      }
+    }
+    g[1] = gv;
+    return lp;
+  }
+};
+
+// eight_schools_ncp.stan:1-23 log_prob (constants of the ~ statements dropped,
+// log-Jacobian of tau = exp(u) added), unconstrained order [mu, log tau, theta_tilde(8)].
+struct EightSchools {
+  static constexpr bool kSeparable = false;
+  template <int DMAX>
+  __device__ __forceinline__ static double row(const double* x, double* g, int /*D*/) {
+    const double y[8] = {28., 8., -3., 7., -1., 1., 18., 12.};
+    const double sg[8] = {15., 10., 16., 11., 9., 11., 10., 18.};
+    const double mu = x[0], u = x[1], tau = exp(u);
+    const double t5 = tau / 5.0;
+    double lp = -0.5 * (mu / 5.0) * (mu / 5.0) - log1p(t5 * t5) + u;
+    double gmu = -mu / 25.0;
+    double gu = -2.0 * t5 * t5 / (1.0 + t5 * t5) + 1.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double th = x[2 + j];
+      const double r = (y[j] - mu - tau * th) / sg[j];
+      lp += -0.5 * th * th - 0.5 * r * r;
+      gmu += r / sg[j];
+      gu += r * tau * th / sg[j];
+      g[2 + j] = -th + r * tau / sg[j];
+    }
+    g[0] = gmu;
+    g[1] = gu;
+    return lp;
+  }
+};
+
+// Row evaluation for separable targets.
+template <class T>
+struct SepRow {
+  template <int DMAX>
+  __device__ __forceinline__ static double row(const double* x, double* g, int D) {
+    double lp = 0.0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d)
+      if (d < D) lp += T::lp1(x[d], g[d]);
+    return lp;
+  }
+};
+
+}  // namespace vbd

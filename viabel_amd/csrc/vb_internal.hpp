@@ -1,0 +1,110 @@
+// vb_internal.hpp — host-side launch interface between the C ABI layer
+// (vb_capi.hip) and the kernel translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vbk {
+
+constexpr int kBlockDMax = 16;  // largest D handled by the block-per-problem kernel
+
+// learning_rate_schedule (vb.py:324-342) evaluated on the device for local step i.
+// a, b, start, end are computed on the host with the reference's own float
+// expression order; device fp64 division is IEEE, so lr(i) matches bit for bit.
+struct LrSched {
+  double lr, lr_end, a, b;
+  long long start, end;
+  int has_end;
+  __host__ __device__ double at(long long i) const {
+    if (!has_end || i < start) return lr;
+    if (i < end) return a / (((b + (double)i) - (double)start) + 1.0);
+    return lr_end;
+  }
+};
+
+// Arguments of the column-pair persistent KLVI kernel (separable targets).
+struct SepArgs {
+  int D, N, W, n_pairs, n_steps, emit_grad;
+  long long step0, hist_start;  // local step index of the first step; 3*n_iters//4
+  long long rng_step0;          // Philox step counter of the first step
+  int n_waves;
+  double t_scale, shape;  // t family: sqrt(df/2), df/2
+  double eps;             // adagrad epsilon
+  LrSched lr;
+  double* lam;            // [P]
+  double* ring;           // [W][P]
+  double* hist;           // [n_hist][P]
+  double* vpart;          // [n_steps][n_waves]
+  double* grad;           // [P] (emit_grad)
+  const double* noise;    // host noise [n_steps][N][D] or null
+  uint32_t k0, k1, stream;
+};
+
+// Arguments of the block-per-problem kernel (any target, D <= kBlockDMax).
+struct BlockArgs {
+  int D, N, W, P, n_steps, emit_grad, chivi;
+  long long step0, hist_start, n_iters, n_hist, rng_step0;
+  double alpha;
+  double t_scale, shape, t_const, df;  // t family constants
+  double eps;
+  LrSched lr;
+  double* lam;          // [n_problems][P]
+  double* ring;         // [n_problems][W][P]
+  double* hist;         // [n_problems][n_hist][P]
+  double* values;       // [n_problems][n_iters] (indexed by global step)
+  double* grad;         // [n_problems][P] (emit_grad)
+  const double* noise;  // host noise [n_problems][n_steps][N][D] or null
+  uint32_t k0, k1, stream;
+};
+
+// family kind 0 = mf gaussian, 1 = mf t; target kind per vb_target_kind.
+hipError_t launch_sep(int fam, int tgt, bool host_noise, const SepArgs& a, hipStream_t s);
+hipError_t launch_block(int fam, int tgt, bool host_noise, const BlockArgs& a, int n_problems,
+                        hipStream_t s);
+bool target_separable(int tgt);
+
+// values[i] = -(c0 + sum_w vpart[s][w]) for i = step0 + s
+hipError_t launch_sep_values(const double* vpart, int n_steps, int n_waves, double c0,
+                             double* values_at_step0, hipStream_t s);
+// out[p] = mean over rows of hist [rows][P]   (per problem block of rows)
+hipError_t launch_row_mean(const double* hist, long long rows, long long P, long long n_problems,
+                           double* out, hipStream_t s);
+
+// elementwise family helpers
+hipError_t launch_sample(int fam, int D, long long n, const double* lam, double t_scale,
+                         double shape, const double* noise, uint32_t k0, uint32_t k1,
+                         uint32_t stream, uint32_t step, double* x, hipStream_t s);
+hipError_t launch_family_logdensity(int fam, int D, long long n, const double* lam, double df,
+                                    double t_const, const double* x, double* out, hipStream_t s);
+hipError_t launch_target_logdensity(int tgt, int D, long long n, const double* x, double* out,
+                                    double* grad, hipStream_t s);
+hipError_t launch_log_weights(int fam, int tgt, int D, long long m, const double* lam,
+                              double t_scale, double shape, double df, double t_const,
+                              const double* noise, uint32_t k0, uint32_t k1, uint32_t stream,
+                              uint32_t step, double* lw, double* xs, hipStream_t s);
+hipError_t launch_adagrad_update(long long P, double* lam, const double* g, double* ring, int W,
+                                 long long step, double lr, double eps, hipStream_t s);
+
+// bounds
+hipError_t bounds_divergence(const double* lw, long long n, double alpha, int has_elbo,
+                             double elbo, double* dev_scratch, double* out7_dev, hipStream_t s);
+hipError_t bounds_centered_moments(const double* x, long long n, long long d,
+                                   double* dev_scratch, double* out2_dev, hipStream_t s);
+hipError_t bounds_covariance(const double* x, long long n, long long d, double* dev_scratch,
+                             double* mean_dev, double* cov_dev, hipStream_t s);
+size_t bounds_scratch_doubles(long long n, long long d);
+constexpr int kCovDMax = 64;
+
+// PSIS (vb_psis.hip)
+size_t psis_scratch_bytes();
+long long psis_tail_max();
+hipError_t psis_column(const double* lw, double* out, long long n, long long st, long long Mt,
+                       void* scratch, double* k_dev, long long* tail_idx_dev,
+                       long long* n_tail_dev, hipStream_t s);
+hipError_t psis_gpdfit(const double* x, long long n, void* scratch, double* out4,
+                       double* ks_out, double* w_out, hipStream_t s);
+hipError_t psis_gpinv(const double* p, long long n, double k, double sigma, double* out,
+                      hipStream_t s);
+hipError_t psis_sumlogs(const double* x, long long n, void* scratch, double* out, hipStream_t s);
+
+}  // namespace vbk

@@ -1,0 +1,113 @@
+"""Pareto-smoothed importance sampling on the GPU (API of notebooks/psis.py).
+
+  psislw(lw, Reff=1.0, overwrite_lw=False) -> (lw_out, kss)    psis.py:112-208
+  gpdfitnew(x, sort=True, sort_in_place=False, return_quadrature=False)
+                                                               psis.py:211-331
+  gpinv(p, k, sigma)                                           psis.py:334-376
+  sumlogs(x, axis=None, out=None)                              psis.py:379-395
+
+All arithmetic runs in libviabel_amd.so (vb_psislw, vb_gpdfit, vb_gpinv,
+vb_sumlogs).  ``psislw_with_tail`` additionally returns the tail order
+tailinds[x2si] the device used, for bit-exact checks.
+"""
+import numpy as np
+
+from . import _native as nat
+
+__all__ = ['psislw', 'psislw_with_tail', 'gpdfitnew', 'gpinv', 'sumlogs']
+
+
+def _tail_cap(n, Reff):
+    return int(np.ceil(min(0.2 * n, 3 * np.sqrt(n / Reff))))
+
+
+def psislw_with_tail(lw, Reff=1.0):
+    lw = np.asarray(lw, dtype=float)
+    if lw.ndim == 2:
+        n, m = lw.shape
+    elif lw.ndim == 1:
+        n, m = len(lw), 1
+    else:
+        raise ValueError("Argument `lw` must be 1 or 2 dimensional.")
+    if n <= 1:
+        raise ValueError("More than one log-weight needed.")
+    src = nat.as_f64(lw.reshape(n, m))
+    out = np.empty((n, m))
+    k = np.empty(m)
+    cap = _tail_cap(n, Reff)
+    tail = np.empty((m, max(cap, 1)), dtype=np.int64)
+    ntail = np.empty(m, dtype=np.int64)
+    nat.check(nat.lib().vb_psislw(nat.context().handle, nat.dptr(src), n, m, float(Reff),
+                                  nat.dptr(out), nat.dptr(k), nat.i64ptr(tail), max(cap, 1),
+                                  nat.i64ptr(ntail)))
+    tails = [tail[c, :ntail[c]].copy() for c in range(m)]
+    return out, k, tails
+
+
+def psislw(lw, Reff=1.0, overwrite_lw=False):
+    """Pareto smoothed importance sampling (PSIS).  Returns (lw_out, kss);
+    kss is a scalar for 1-D input (psis.py:204-206)."""
+    out, k, _ = psislw_with_tail(lw, Reff)
+    lw_arr = np.asarray(lw)
+    if lw_arr.ndim == 1:
+        res = out[:, 0]
+        if overwrite_lw and isinstance(lw, np.ndarray) and lw.flags.f_contiguous:
+            lw[...] = res
+            res = lw
+        return res, k[0]
+    if overwrite_lw and isinstance(lw, np.ndarray) and lw.flags.f_contiguous:
+        lw[...] = out
+        return lw, k
+    return np.asfortranarray(out), k
+
+
+def gpdfitnew(x, sort=True, sort_in_place=False, return_quadrature=False):
+    """Zhang-Stephens empirical-Bayes GPD fit; returns (k, sigma[, ks, w])."""
+    x = np.asarray(x)
+    if x.ndim != 1 or len(x) <= 1:
+        raise ValueError("Invalid input array.")
+    if sort is True and sort_in_place:
+        x.sort()                      # the reference's documented side effect
+    xx = nat.as_f64(x)
+    n = xx.size
+    m = 30 + int(np.sqrt(n))
+    k, sigma = np.empty(1), np.empty(1)
+    ks, w = np.empty(m), np.empty(m)
+    nw = np.empty(1, dtype=np.int64)
+    nat.check(nat.lib().vb_gpdfit(nat.context().handle, nat.dptr(xx), n, nat.dptr(k),
+                                  nat.dptr(sigma), nat.dptr(ks), nat.dptr(w), nat.i64ptr(nw)))
+    if return_quadrature:
+        return k[0], sigma[0], ks[:nw[0]].copy(), w[:nw[0]].copy()
+    return k[0], sigma[0]
+
+
+def gpinv(p, k, sigma):
+    """Inverse generalised Pareto distribution function."""
+    p = np.asarray(p, dtype=float)
+    pp = nat.as_f64(p.ravel())
+    out = np.empty(pp.size)
+    nat.check(nat.lib().vb_gpinv(nat.context().handle, nat.dptr(pp), pp.size, float(k),
+                                 float(sigma), nat.dptr(out)))
+    return out.reshape(p.shape)
+
+
+def _sumlogs_1d(v):
+    v = nat.as_f64(v)
+    r = np.empty(1)
+    nat.check(nat.lib().vb_sumlogs(nat.context().handle, nat.dptr(v), v.size, nat.dptr(r)))
+    return r[0]
+
+
+def sumlogs(x, axis=None, out=None):
+    """log(sum(exp(x), axis)) computed stably."""
+    x = np.asarray(x, dtype=float)
+    if axis is None:
+        res = _sumlogs_1d(x.ravel())
+    else:
+        moved = np.moveaxis(x, axis, -1)
+        flat = moved.reshape(-1, moved.shape[-1])
+        res = np.array([_sumlogs_1d(row) for row in flat]).reshape(moved.shape[:-1])
+    if out is not None:
+        out[...] = res
+        return out
+    return res

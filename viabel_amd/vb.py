@@ -1,0 +1,385 @@
+"""Monte Carlo VI on the GPU behind the viabel.vb API.
+
+Mirrors the reference module viabel/vb.py (names, signatures, return shapes,
+error messages) for the hot path:
+
+  mean_field_gaussian_variational_family  vb.py:48-82
+  mean_field_t_variational_family         vb.py:140-182
+  black_box_klvi                          vb.py:236-245
+  black_box_chivi                         vb.py:248-266
+  learning_rate_schedule                  vb.py:324-342
+  adagrad_optimize                        vb.py:345-389
+
+Computation runs in libviabel_amd.so (HIP, gfx950).  Two noise sources:
+
+* ``rng='numpy'`` (default): the family owns ``RandomState(0)`` exactly like the
+  reference (vb.py:49, 143) and CHIVI draws its per-call seed from the global
+  numpy RNG (vb.py:258); the standardized draws are generated on the host with
+  the same calls in the same order and streamed to the kernels, so results
+  match the reference on identical seeds.
+* ``rng='philox'``: draws come from an in-kernel Philox4x32-10 counter RNG
+  (counter = column pair, sample, step, stream); nothing is transferred per
+  step.  Statistically equivalent, not stream-identical, to the reference.
+  This is the throughput path (bench.py).
+
+The module-wide default is taken from $VIABEL_AMD_RNG or set_default_rng().
+"""
+import itertools
+import math
+import os
+from collections import namedtuple
+
+import numpy as np
+
+from . import _native as nat
+from .targets import Target
+
+__all__ = [
+    'mean_field_gaussian_variational_family',
+    'mean_field_t_variational_family',
+    'black_box_klvi',
+    'black_box_chivi',
+    'learning_rate_schedule',
+    'adagrad_optimize',
+    'set_default_rng',
+]
+
+VariationalFamily = namedtuple('VariationalFamily',
+                               ['sample', 'entropy',
+                                'logdensity', 'mean_and_cov',
+                                'pth_moment', 'var_param_dim'])
+
+_DEFAULT_RNG = [os.environ.get('VIABEL_AMD_RNG', 'numpy')]
+_STREAMS = itertools.count(1)
+LOG2PI = math.log(2 * math.pi)
+
+
+def set_default_rng(kind):
+    if kind not in ('numpy', 'philox'):
+        raise ValueError("rng must be 'numpy' or 'philox'")
+    _DEFAULT_RNG[0] = kind
+
+
+class NativeVariationalFamily(VariationalFamily):
+    """VariationalFamily namedtuple carrying the device descriptor and RNG state."""
+
+    def _struct(self):
+        return nat.Family(self.kind, 0, self.dim, float(self.df or 0.0))
+
+    # standardized draws exactly as the reference draws them
+    def _draw(self, n, seed=None):
+        rs = self.rs if seed is None else np.random.RandomState(seed)
+        if self.kind == nat.FAMILY_MF_GAUSSIAN:
+            return rs.randn(n, self.dim)
+        return rs.standard_t(self.df, size=(n, self.dim))
+
+    def _philox_noise(self, seed=None, steps=1):
+        """Noise descriptor for the next `steps` Philox steps of this family."""
+        if seed is None:
+            nz = nat.Noise(nat.NOISE_PHILOX, self.stream, self.seed, self.step, None)
+            self.step += steps
+        else:
+            nz = nat.Noise(nat.NOISE_PHILOX, 0, int(seed) & 0xFFFFFFFFFFFFFFFF, 0, None)
+        return nz
+
+
+def _make_family(kind, dim, df, rng):
+    rng = _DEFAULT_RNG[0] if rng is None else rng
+    if rng not in ('numpy', 'philox'):
+        raise ValueError("rng must be 'numpy' or 'philox'")
+
+    def unpack(var_param):
+        var_param = np.asarray(var_param, dtype=float)
+        return var_param[:dim], var_param[dim:]
+
+    def sample(var_param, n_samples, seed=None):
+        lam = nat.as_f64(var_param)
+        out = np.empty((int(n_samples), dim))
+        if fam.rng == 'numpy':
+            eps = nat.as_f64(fam._draw(int(n_samples), seed))
+            nz = nat.Noise(nat.NOISE_HOST, 0, 0, 0, nat.dptr(eps))
+        else:
+            nz = fam._philox_noise(seed)
+        nat.check(nat.lib().vb_family_sample(nat.context().handle, fam._struct(), nat.dptr(lam),
+                                             int(n_samples), nz, nat.dptr(out)))
+        return out
+
+    def logdensity(x, var_param):
+        lam = nat.as_f64(var_param)
+        xx = np.asarray(x, dtype=float)
+        one_d = xx.ndim == 1
+        xx = nat.as_f64(np.atleast_2d(xx))
+        out = np.empty(xx.shape[0])
+        nat.check(nat.lib().vb_family_logdensity(nat.context().handle, fam._struct(),
+                                                 nat.dptr(lam), nat.dptr(xx), xx.shape[0],
+                                                 nat.dptr(out)))
+        if one_d and kind == nat.FAMILY_MF_GAUSSIAN:
+            return out[0]            # mvn.logpdf of one point is a scalar
+        return out
+
+    if kind == nat.FAMILY_MF_GAUSSIAN:
+        def entropy(var_param):
+            _, log_std = unpack(var_param)
+            return 0.5 * dim * (1.0 + np.log(2 * np.pi)) + np.sum(log_std)   # vb.py:61
+
+        def mean_and_cov(var_param):
+            mean, log_std = unpack(var_param)
+            return mean, np.diag(np.exp(2 * log_std))                       # vb.py:69
+
+        def pth_moment(p, var_param):
+            if p not in [2, 4]:
+                raise ValueError('only p = 2 or 4 supported')
+            _, log_std = unpack(var_param)
+            v = np.exp(2 * log_std)
+            if p == 2:
+                return np.sum(v)
+            return 2 * np.sum(v ** 2) + np.sum(v) ** 2
+    else:
+        def entropy(var_param):
+            _, log_scale = unpack(var_param)
+            return np.sum(log_scale)                                          # vb.py:156
+
+        def mean_and_cov(var_param):
+            mean, log_scale = unpack(var_param)
+            return mean, df / (df - 2) * np.diag(np.exp(2 * log_scale))       # vb.py:166
+
+        def pth_moment(p, var_param):
+            if p not in [2, 4]:
+                raise ValueError('only p = 2 or 4 supported')
+            if df <= p:
+                raise ValueError('df must be greater than p')
+            _, log_scale = unpack(var_param)
+            s = np.exp(log_scale)
+            c = df / (df - 2)
+            if p == 2:
+                return c * np.sum(s ** 2)
+            return c ** 2 * (2 * (df - 1) / (df - 4) * np.sum(s ** 4) + np.sum(s ** 2) ** 2)
+
+    fam = NativeVariationalFamily(sample, entropy, logdensity, mean_and_cov, pth_moment, 2 * dim)
+    fam.kind, fam.dim, fam.df, fam.rng = kind, int(dim), df, rng
+    fam.rs = np.random.RandomState(0)      # vb.py:49 / vb.py:143
+    fam.seed, fam.stream, fam.step = 0, next(_STREAMS) & 0xFFFFFF, 0
+    return fam
+
+
+def mean_field_gaussian_variational_family(dim, rng=None):
+    """vb.py:48-82.  var_param = [mean (dim), log_std (dim)]."""
+    return _make_family(nat.FAMILY_MF_GAUSSIAN, dim, None, rng)
+
+
+def mean_field_t_variational_family(dim, df, rng=None):
+    """vb.py:140-182.  var_param = [mean (dim), log_scale (dim)]."""
+    if df <= 2:
+        raise ValueError('df must be greater than 2')
+    return _make_family(nat.FAMILY_MF_T, dim, float(df), rng)
+
+
+class NativeObjective:
+    """objective_and_grad(var_param) -> (value, grad) evaluated on the GPU."""
+
+    def __init__(self, kind, var_family, logdensity, n_samples, alpha=None):
+        if not isinstance(var_family, NativeVariationalFamily):
+            raise TypeError('var_family must come from viabel_amd.vb')
+        if not isinstance(logdensity, Target):
+            raise TypeError(
+                'the device estimator needs a viabel_amd.targets target as logdensity '
+                '(arbitrary Python callables cannot run in a HIP kernel); got %r' % (logdensity,))
+        if logdensity.dim != var_family.dim:
+            raise ValueError('target dimension %d != family dimension %d'
+                             % (logdensity.dim, var_family.dim))
+        self.kind, self.family, self.target = kind, var_family, logdensity
+        self.n_samples = int(n_samples)
+        self.alpha = float(alpha) if alpha is not None else 2.0
+
+    def _structs(self):
+        return (self.family._struct(), self.target._struct(),
+                nat.Objective(self.kind, 0, self.alpha, self.n_samples))
+
+    def _eps_one_call(self):
+        """Host draws for one call, in the reference's order (numpy mode)."""
+        fam = self.family
+        if self.kind == nat.OBJ_KLVI:
+            return fam._draw(self.n_samples)                        # vb.py:239
+        seed = np.random.randint(2 ** 32)                           # vb.py:258
+        return fam._draw(self.n_samples, seed)                      # vb.py:251
+
+    def __call__(self, var_param):
+        lam = nat.as_f64(var_param)
+        if lam.shape != (2 * self.family.dim,):
+            raise ValueError('var_param must have shape (%d,)' % (2 * self.family.dim))
+        fam = self.family
+        if fam.rng == 'numpy':
+            eps = nat.as_f64(self._eps_one_call())
+            nz = nat.Noise(nat.NOISE_HOST, 0, 0, 0, nat.dptr(eps))
+        elif self.kind == nat.OBJ_CHIVI:
+            nz = fam._philox_noise(np.random.randint(2 ** 32))
+            nz.stream = fam.stream
+        else:
+            nz = fam._philox_noise()
+        f, t, o = self._structs()
+        val = np.empty(1)
+        grad = np.empty(lam.size)
+        nat.check(nat.lib().vb_objective_value_grad(nat.context().handle, f, t, o, nat.dptr(lam),
+                                                    nz, nat.dptr(val), nat.dptr(grad)))
+        return val[0], grad
+
+
+def black_box_klvi(var_family, logdensity, n_samples):
+    """vb.py:236-245: returns objective_and_grad(var_param) -> (-ELBO, grad)."""
+    return NativeObjective(nat.OBJ_KLVI, var_family, logdensity, n_samples)
+
+
+def black_box_chivi(alpha, var_family, logdensity, n_samples):
+    """vb.py:248-266: returns objective_and_grad(var_param) -> (CUBO, grad)."""
+    return NativeObjective(nat.OBJ_CHIVI, var_family, logdensity, n_samples, alpha)
+
+
+def learning_rate_schedule(n_iters, learning_rate, learning_rate_end):
+    """vb.py:324-342 (generator); the device evaluates the same expression."""
+    if learning_rate <= 0:
+        raise ValueError('learning rate must be positive')
+    if learning_rate_end is not None:
+        if learning_rate <= learning_rate_end:
+            raise ValueError('initial learning rate must be greater than final learning rate')
+        b = n_iters * learning_rate_end / (2 * (learning_rate - learning_rate_end))
+        a = learning_rate * b
+        start_decrease_at = n_iters // 4
+        end_decrease_at = 3 * n_iters // 4
+    for i in range(n_iters):
+        if learning_rate_end is None or i < start_decrease_at:
+            yield learning_rate
+        elif i < end_decrease_at:
+            yield a / (b + i - start_decrease_at + 1)
+        else:
+            yield learning_rate_end
+
+
+# host draws per device chunk in numpy mode (bounded host memory)
+_HOST_CHUNK_ELEMS = 1 << 24
+
+
+class DeviceRun:
+    """Device-resident adagrad state for one or more problems (vb_run)."""
+
+    def __init__(self, objective, n_iters, init_params, window=10, learning_rate=.01,
+                 epsilon=.1, learning_rate_end=None):
+        init = nat.as_f64(np.atleast_2d(init_params))
+        self.obj = objective
+        self.n_iters = int(n_iters)
+        self.n_problems = init.shape[0]
+        self.P = init.shape[1]
+        f, t, o = objective._structs()
+        cfg = nat.AdagradConfig(self.n_iters, int(window), 0, float(learning_rate),
+                                nat.NAN if learning_rate_end is None else float(learning_rate_end),
+                                float(epsilon))
+        import ctypes
+        h = ctypes.c_void_p()
+        nat.check(nat.lib().vb_run_create(nat.context().handle, f, t, o, cfg, self.n_problems,
+                                          nat.dptr(init), ctypes.byref(h)))
+        self.handle = h
+        self.done = 0
+
+    def advance_philox(self, n_steps, seed, stream, step):
+        nz = nat.Noise(nat.NOISE_PHILOX, stream & 0xFFFFFF, seed, step, None)
+        nat.check(nat.lib().vb_run_advance(self.handle, int(n_steps), nz))
+        self.done += int(n_steps)
+
+    def advance_host(self, eps):
+        """eps: [n_problems][n_steps][N][D] standardized draws."""
+        eps = nat.as_f64(eps)
+        n_steps = eps.shape[1]
+        nz = nat.Noise(nat.NOISE_HOST, 0, 0, 0, nat.dptr(eps))
+        nat.check(nat.lib().vb_run_advance(self.handle, n_steps, nz))
+        self.done += n_steps
+
+    def result(self):
+        n_hist = self.n_iters - 3 * self.n_iters // 4
+        lam = np.empty((self.n_problems, self.P))
+        hist = np.empty((self.n_problems, n_hist, self.P))
+        vals = np.empty((self.n_problems, self.n_iters))
+        smooth = np.empty((self.n_problems, self.P))
+        nat.check(nat.lib().vb_run_result(self.handle, nat.dptr(lam), nat.dptr(hist),
+                                          nat.dptr(vals), nat.dptr(smooth)))
+        return lam, hist, vals, smooth
+
+    def synchronize(self):
+        nat.context().synchronize()
+
+    def __del__(self):
+        try:
+            if getattr(self, 'handle', None) and nat._lib is not None:
+                nat._lib.vb_run_destroy(self.handle)
+        except Exception:
+            pass
+
+
+def _native_adagrad(n_iters, obj, init_param, window, learning_rate, epsilon,
+                    learning_rate_end):
+    fam = obj.family
+    run = DeviceRun(obj, n_iters, init_param[None, :], window, learning_rate, epsilon,
+                    learning_rate_end)
+    if fam.rng == 'philox':
+        run.advance_philox(n_iters, fam.seed, fam.stream, fam.step)
+        fam.step += n_iters
+    else:
+        per_step = obj.n_samples * fam.dim
+        chunk = max(1, min(n_iters, _HOST_CHUNK_ELEMS // max(per_step, 1)))
+        done = 0
+        while done < n_iters:
+            cs = min(chunk, n_iters - done)
+            eps = np.stack([obj._eps_one_call() for _ in range(cs)])
+            run.advance_host(eps[None])
+            done += cs
+    _, hist, vals, smooth = run.result()
+    return smooth[0], hist[0], vals[0], np.zeros(n_iters)
+
+
+def _foreign_adagrad(n_iters, objective_and_grad, init_param, has_log_norm, window,
+                     learning_rate, epsilon, learning_rate_end):
+    """Adagrad for a caller-supplied objective: the objective is the caller's
+    Python; the update (vb.py:364-374) runs in the device kernel vb_adagrad_update
+    on device-resident state."""
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError('viabel_amd.adagrad_optimize needs a GPU')
+    if has_log_norm:
+        raise NotImplementedError('has_log_norm=True is not supported by the device optimiser')
+    dev = torch.device('cuda', nat.context().device)
+    lam = torch.tensor(np.asarray(init_param, dtype=float), dtype=torch.float64, device=dev)
+    ring = torch.zeros((window, lam.numel()), dtype=torch.float64, device=dev)
+    values, hist = [], []
+    sched = learning_rate_schedule(n_iters, learning_rate, learning_rate_end)
+    for i, lr in zip(range(n_iters), sched):
+        torch.cuda.synchronize(dev)
+        val, g = objective_and_grad(lam.cpu().numpy())
+        values.append(val)
+        g = nat.as_f64(g)
+        nat.check(nat.lib().vb_adagrad_update(nat.context().handle, lam.numel(), nat.dptr(lam),
+                                              nat.dptr(g), nat.dptr(ring), window, i, lr,
+                                              epsilon))
+        if i >= 3 * n_iters // 4:
+            hist.append(lam.cpu().numpy().copy())
+    hist = np.array(hist)
+    smooth = np.mean(hist, axis=0) if len(hist) else np.full(lam.numel(), np.nan)
+    return smooth, hist, np.array(values), np.zeros(n_iters)
+
+
+def adagrad_optimize(n_iters, objective_and_grad, init_param,
+                     has_log_norm=False, window=10, learning_rate=.01,
+                     epsilon=.1, learning_rate_end=None):
+    """vb.py:345-389.  Returns (smoothed_opt_param, variational_param_history,
+    value_history, log_norm_history).  Native objectives run the whole loop on
+    the device (one kernel chain, no per-step host work in philox mode)."""
+    # validate like the reference's schedule generator
+    if learning_rate <= 0:
+        raise ValueError('learning rate must be positive')
+    if learning_rate_end is not None and learning_rate <= learning_rate_end:
+        raise ValueError('initial learning rate must be greater than final learning rate')
+    init_param = np.asarray(init_param, dtype=float)
+    if isinstance(objective_and_grad, NativeObjective):
+        if has_log_norm:
+            raise ValueError('not enough values to unpack (expected 3, got 2)')
+        return _native_adagrad(int(n_iters), objective_and_grad, init_param, int(window),
+                               learning_rate, epsilon, learning_rate_end)
+    return _foreign_adagrad(int(n_iters), objective_and_grad, init_param, has_log_norm,
+                            int(window), learning_rate, epsilon, learning_rate_end)
