@@ -92,7 +92,9 @@ def main():
 
     from viabel_amd import _native as nat, targets
     from viabel_amd import vb
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-NULL) stream: the kernels and the timing events share it
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     nat.use_stream(local, stream.cuda_stream)
 
     fam = vb.mean_field_gaussian_variational_family(D, rng='philox')

@@ -95,14 +95,17 @@ typedef struct vb_objective {
 /* Noise source.  HOST: `eps` holds standardized draws laid out
  * [problem][step][sample][dim] (C order): N(0,1) for the Gaussian family,
  * standard_t(df) for the t family.  PHILOX: `seed` keys the generator;
- * `stream` (24 bits) + problem index selects the stream; `step` is the
- * global step index of the first step of the call. */
+ * problem q of a call draws from stream `stream + q * stream_stride`
+ * (24 bits; stride 0 means 1); `step` is the global step index of the first
+ * step of the call. */
 typedef struct vb_noise {
   int32_t kind;      /* vb_noise_kind */
   uint32_t stream;
   uint64_t seed;
   uint64_t step;
   const double* eps; /* HOST only */
+  uint32_t stream_stride;
+  uint32_t reserved;
 } vb_noise;
 
 /* Adagrad settings, vb.py:345-347 defaults: window 10, lr .01, eps .1. */

@@ -10,6 +10,17 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line('markers', 'gpu: needs an MI355X (runs the HIP kernels)')
+    _build_missing()
+
+
+def _build_missing():
+    """Build the oracle's C library and the HIP library if a fresh checkout
+    lacks them (hipcc cross-compiles without a GPU)."""
+    import subprocess
+    if not os.path.exists(os.path.join(ROOT, 'oracle', 'liboracle_rng.so')):
+        subprocess.call(['make', '-s', '-C', os.path.join(ROOT, 'oracle')])
+    if not os.path.exists(os.path.join(ROOT, 'viabel_amd', 'libviabel_amd.so')):
+        subprocess.call(['make', '-s', '-j8', '-C', os.path.join(ROOT, 'viabel_amd', 'csrc')])
 
 
 def gpu_available():

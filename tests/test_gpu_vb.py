@@ -267,3 +267,42 @@ def test_log_weights(kind, df, target, D):
     ox, olw = vo.log_weights(ofam, target, lam, 5000)
     np.testing.assert_allclose(x, ox, rtol=1e-14, atol=1e-14)
     np.testing.assert_allclose(lw, olw, rtol=1e-11, atol=1e-11)
+
+
+@pytest.mark.parametrize('kind,df', [('gauss', None), ('t', 40.0), ('t', 3.5)])
+@pytest.mark.parametrize('D', [1, 2, 9, 64])
+def test_device_philox_noise_equals_c_oracle(kind, df, D):
+    """The in-kernel draws (lambda = 0: x = eps) equal oracle/vbrng.c's draws to
+    ~1 ulp (the device uses short fp64 log/sqrt/sincospi, the oracle libm)."""
+    vb, targets, vo, ro = _mods()
+    fam = _family(vb, kind, df, D, 'philox')
+    lam = np.zeros(2 * D)
+    for call in range(2):
+        x = fam.sample(lam, 3000)
+        eps = ro.noise(fam.seed, fam.stream, call, 3000, D, kind, df or 0.0)
+        np.testing.assert_allclose(x, eps, rtol=2e-14, atol=1e-13)
+    # a seeded call uses key = seed, stream 0, step 0
+    x = fam.sample(lam, 100, seed=1234)
+    np.testing.assert_allclose(x, ro.noise(1234, 0, 0, 100, D, kind, df or 0.0),
+                               rtol=2e-14, atol=1e-13)
+
+
+@pytest.mark.parametrize('mode', ['1', '2', 'mix'])
+@pytest.mark.parametrize('kind,df,D', [('gauss', None, 9001), ('t', 40.0, 8200), ('gauss', None, 17)])
+def test_sep_layouts_agree(mode, kind, df, D, monkeypatch):
+    """The column-pair kernel's layouts (1 or 2 pairs per wavefront, or the
+    mixed grid) give the oracle's trajectory (Philox noise)."""
+    vb, targets, vo, ro = _mods()
+    monkeypatch.setenv('VB_SEP_MODE', mode)
+    N, n_iters = 100, 24
+    fam = _family(vb, kind, df, D, 'philox')
+    ofam = vo.Family(kind, D, df)
+    init = np.concatenate([np.linspace(-1, 1, D), np.full(D, 0.3)])
+    obj = vb.black_box_klvi(fam, targets.mixture(D), N)
+    seed, stream, step0 = fam.seed, fam.stream, fam.step
+    res = vb.adagrad_optimize(n_iters, obj, init, learning_rate=0.03, window=7)
+    eps_fn = lambda i: ro.noise(seed, stream, step0 + i, N, D, kind, df or 0.0)
+    ores = _oracle_run(vo, ofam, 'klvi', 'mixture', n_iters, init, N, eps_fn=eps_fn,
+                       learning_rate=0.03, window=7)
+    np.testing.assert_allclose(res[1], ores[1], rtol=1e-9, atol=1e-11)
+    np.testing.assert_allclose(res[2], ores[2], rtol=1e-9, atol=1e-9)

@@ -38,7 +38,8 @@ class Objective(ctypes.Structure):
 
 class Noise(ctypes.Structure):
     _fields_ = [('kind', ctypes.c_int32), ('stream', ctypes.c_uint32),
-                ('seed', ctypes.c_uint64), ('step', ctypes.c_uint64), ('eps', c_double_p)]
+                ('seed', ctypes.c_uint64), ('step', ctypes.c_uint64), ('eps', c_double_p),
+                ('stream_stride', ctypes.c_uint32), ('reserved', ctypes.c_uint32)]
 
 
 class AdagradConfig(ctypes.Structure):

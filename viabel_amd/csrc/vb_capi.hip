@@ -406,6 +406,7 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
     a.k0 = k0;
     a.k1 = k1;
     a.stream = noise->stream;
+    a.stream_stride = 1;
     VB_HIP(vbk::launch_block(fi.kind, tgt->kind, host, a, 1, c->stream));
   } else {
     return fail(VB_EUNSUPPORTED,
@@ -601,6 +602,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
     a.k0 = k0;
     a.k1 = k1;
     a.stream = noise->stream;
+    a.stream_stride = noise->stream_stride ? noise->stream_stride : 1;
     VB_HIP(vbk::launch_block(r->fi.kind, r->tgt, host, a, (int)r->nprob, c->stream));
   }
   r->done += n_steps;

@@ -55,15 +55,99 @@ struct Rng {
   }
 };
 
+// ---- fp64 transcendentals for noise generation --------------------------------
+// Box-Muller needs log, sqrt and sin/cos of uniforms only.  These short forms
+// (about 1 ulp) replace the general ocml routines (which carry extra-precision
+// arithmetic and special-case handling the noise path never needs): the
+// transform is ~40% cheaper.  The C oracle uses libm; tests compare at 1e-14.
+
+// log(u) for u in (0, 1]: u = m 2^e with m in [sqrt(1/2), sqrt(2)),
+// log m = 2 atanh(f) = 2 f sum_k f^2k / (2k+1), f = (m-1)/(m+1), |f| <= 0.1716.
+__device__ __forceinline__ double log_unit(double u) {
+  int e;
+  double m = frexp(u, &e);
+  const bool lo = m < 0.70710678118654752440;
+  m = lo ? m + m : m;
+  e = lo ? e - 1 : e;
+  const double num = m - 1.0, den = m + 1.0;
+  double r = __builtin_amdgcn_rcp(den);
+  r = fma(r, fma(-den, r, 1.0), r);
+  r = fma(r, fma(-den, r, 1.0), r);
+  double f = num * r;
+  f = fma(r, fma(-den, f, num), f);
+  const double f2 = f * f;
+  double p = 0.04347826086956522;            // 1/23
+  p = fma(p, f2, 0.047619047619047616);      // 1/21
+  p = fma(p, f2, 0.05263157894736842);
+  p = fma(p, f2, 0.058823529411764705);
+  p = fma(p, f2, 0.06666666666666667);
+  p = fma(p, f2, 0.07692307692307693);
+  p = fma(p, f2, 0.09090909090909091);
+  p = fma(p, f2, 0.1111111111111111);
+  p = fma(p, f2, 0.14285714285714285);
+  p = fma(p, f2, 0.2);
+  p = fma(p, f2, 0.3333333333333333);
+  const double de = (double)e;
+  // ln2 = LN2_HI + LN2_LO, LN2_HI with trailing zero bits so de * LN2_HI is exact
+  const double t = fma(2.0 * f * f2, p, 2.0 * f);
+  return fma(de, 0.6931471805598903, fma(de, 5.497923018708371e-14, t));
+}
+
+// sqrt(y) for y > 0 normal: rsq seed + Goldschmidt refinement.
+__device__ __forceinline__ double sqrt_pos(double y) {
+  const double r = __builtin_amdgcn_rsq(y);
+  double h = 0.5 * r;
+  double s = y * r;
+  const double e = fma(-s, h, 0.5);
+  s = fma(s, e, s);
+  h = fma(h, e, h);
+  const double d = fma(-s, s, y);
+  return fma(d, h, s);
+}
+
+// sin(pi x), cos(pi x) for x in [0, 2]: octant reduction + Taylor on [-pi/4, pi/4].
+__device__ __forceinline__ void sincospi_unit(double x, double& sn, double& cs) {
+  const double q = rint(x + x);            // 0..4
+  const double r = fma(-0.5, q, x);        // exact, |r| <= 1/4
+  const double th = fma(r, 3.141592653589793, r * 1.2246467991473532e-16);
+  const double t2 = th * th;
+  double ps = -8.22063524662433e-18;
+  ps = fma(ps, t2, 2.8114572543455206e-15);
+  ps = fma(ps, t2, -7.647163731819816e-13);
+  ps = fma(ps, t2, 1.6059043836821613e-10);
+  ps = fma(ps, t2, -2.505210838544172e-08);
+  ps = fma(ps, t2, 2.7557319223985893e-06);
+  ps = fma(ps, t2, -0.0001984126984126984);
+  ps = fma(ps, t2, 0.008333333333333333);
+  ps = fma(ps, t2, -0.16666666666666666);
+  const double s0 = fma(th * t2, ps, th);
+  double pc = 4.110317623312165e-19;
+  pc = fma(pc, t2, -1.5619206968586225e-16);
+  pc = fma(pc, t2, 4.779477332387385e-14);
+  pc = fma(pc, t2, -1.1470745597729725e-11);
+  pc = fma(pc, t2, 2.08767569878681e-09);
+  pc = fma(pc, t2, -2.755731922398589e-07);
+  pc = fma(pc, t2, 2.48015873015873e-05);
+  pc = fma(pc, t2, -0.001388888888888889);
+  pc = fma(pc, t2, 0.041666666666666664);
+  pc = fma(pc, t2, -0.5);
+  const double c0 = fma(t2, pc, 1.0);
+  const int k = ((int)q) & 3;
+  const double a = (k & 1) ? c0 : s0;     // |sin| or |cos| swapped on odd octant pairs
+  const double b = (k & 1) ? s0 : c0;
+  sn = (k & 2) ? -a : a;
+  cs = (k == 1 || k == 2) ? -b : b;
+}
+
 // Two standard normals from one Philox block.
 __device__ __forceinline__ void normal_pair(u4 w, double& z0, double& z1) {
   const uint64_t a = ((((uint64_t)w.y) << 32) | w.x) >> 11;
   const uint64_t b = ((((uint64_t)w.w) << 32) | w.z) >> 11;
   const double u1 = ((double)a + 0.5) * 0x1p-53;
   const double u2 = (double)b * 0x1p-53;
-  const double r = sqrt(-2.0 * log(u1));
+  const double r = sqrt_pos(-2.0 * log_unit(u1));
   double s, c;
-  sincospi(2.0 * u2, &s, &c);
+  sincospi_unit(2.0 * u2, s, c);
   z0 = r * c;
   z1 = r * s;
 }
@@ -83,9 +167,9 @@ __device__ __forceinline__ void gamma_pair(const Rng& rng, uint32_t pair, uint32
     const u4 w = rng.draw(pair, sample, step, 1u + k);
     const double u1 = ((double)w.x + 0.5) * 0x1p-32;
     const double u2 = (double)w.y * 0x1p-32;
-    const double r = sqrt(-2.0 * log(u1));
+    const double r = sqrt_pos(-2.0 * log_unit(u1));
     double s, cs;
-    sincospi(2.0 * u2, &s, &cs);
+    sincospi_unit(2.0 * u2, s, cs);
     const double za = r * cs, zb = r * s;
     const double ua = ((double)w.z + 0.5) * 0x1p-32;
     const double ub = ((double)w.w + 0.5) * 0x1p-32;
@@ -124,6 +208,38 @@ __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
+}
+
+// Wave-wide sum of a double with DPP row ops + gfx950 permlane swaps (no LDS
+// traffic, short latency).  Every lane ends with the bitwise-identical total.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double swap_sum16(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+}
+
+__device__ __forceinline__ double swap_sum32(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+}
+
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  v = swap_sum16(v);       // rows 0+1, 2+3
+  return swap_sum32(v);    // halves
 }
 
 __device__ __forceinline__ double wave_max(double v) {

@@ -38,6 +38,7 @@ struct SepArgs {
   double* grad;           // [P] (emit_grad)
   const double* noise;    // host noise [n_steps][N][D] or null
   uint32_t k0, k1, stream;
+  int pairs2, blocks2, blocks1;  // filled by the launcher (2-pair / 1-pair split)
 };
 
 // Arguments of the block-per-problem kernel (any target, D <= kBlockDMax).
@@ -54,7 +55,7 @@ struct BlockArgs {
   double* values;       // [n_problems][n_iters] (indexed by global step)
   double* grad;         // [n_problems][P] (emit_grad)
   const double* noise;  // host noise [n_problems][n_steps][N][D] or null
-  uint32_t k0, k1, stream;
+  uint32_t k0, k1, stream, stream_stride;
 };
 
 // family kind 0 = mf gaussian, 1 = mf t; target kind per vb_target_kind.

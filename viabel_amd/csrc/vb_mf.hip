@@ -21,6 +21,7 @@
 #include "vb_device.hpp"
 #include "vb_internal.hpp"
 
+#include <cstdlib>
 #include <type_traits>
 
 using namespace vbd;
@@ -30,137 +31,177 @@ namespace vbk {
 // -------------------------------------------------------------------------
 // column-pair persistent KLVI kernel
 // -------------------------------------------------------------------------
-template <class TGT, bool TFAM, bool HOST>
-__global__ __launch_bounds__(256) void sep_kernel(SepArgs a) {
+// Reduce-scatter of the four per-lane partial sums (gA, gB, hA, hB) over the
+// lanes of one column pair (64 lanes for PPW = 1, 32 for PPW = 2): lane l ends
+// with the group total of quantity (l & 3).  Two DPP exchange steps hand each
+// lane one quantity, two row rotations and one or two permlane swaps finish the
+// sum: about a third of the instructions of four all-reduces.
+template <int PPW>
+__device__ __forceinline__ double reduce_scatter4(int lane, double gA, double gB, double hA,
+                                                  double hB) {
+  const bool b0 = lane & 1, b1 = lane & 2;
+  double kg = b0 ? gB : gA, kh = b0 ? hB : hA;
+  kg += dpp_f64<0xB1>(b0 ? gA : gB);  // quad_perm [1,0,3,2]: partner keeps the other column
+  kh += dpp_f64<0xB1>(b0 ? hA : hB);
+  double k = b1 ? kh : kg;
+  k += dpp_f64<0x4E>(b1 ? kg : kh);   // quad_perm [2,3,0,1]
+  k += dpp_f64<0x124>(k);             // row_ror:4  (same lane & 3)
+  k += dpp_f64<0x128>(k);             // row_ror:8
+  k = swap_sum16(k);                  // rows 0+1 and 2+3
+  if constexpr (PPW == 1) k = swap_sum32(k);
+  return k;
+}
+
+// Sum over the lanes of one column-pair group (all lanes get their group's total).
+template <int PPW>
+__device__ __forceinline__ double group_sum(double v) {
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
+  v += dpp_f64<0x140>(v);
+  v = swap_sum16(v);
+  if constexpr (PPW == 1) v = swap_sum32(v);
+  return v;
+}
+
+// Value of lane (group base + k) for every lane of the group.
+template <int PPW>
+__device__ __forceinline__ double group_bcast(double v, int k, bool upper) {
+  if constexpr (PPW == 1) return readlane_f64(v, k);
+  const double lo = readlane_f64(v, k), hi = readlane_f64(v, 32 + k);
+  return upper ? hi : lo;
+}
+
+// PPW column pairs per wavefront (PPW in {1, 2}); pair index = wave * PPW + (lane >> 5 for PPW 2).
+template <class TGT, bool TFAM, bool HOST, int PPW>
+__device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, int wave) {
+  constexpr int LPP = 64 / PPW;  // lanes per column pair
   const int lane = threadIdx.x & 63;
-  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (w >= a.n_pairs) return;  // wave-uniform exit: no block barriers below
+  const int grp = PPW == 1 ? 0 : (lane >> 5);
+  const bool upper = grp == 1;
+  const int gl = lane & (LPP - 1);           // lane within the pair's group
+  const int w = wave * PPW + grp;            // column pair of this lane
+  const bool live = w < a.n_pairs;           // the upper group of the last wave may be empty
   const int D = a.D, N = a.N, W = a.W;
   const long long P = 2LL * D;
   const int dA = 2 * w, dB = 2 * w + 1;
-  const bool hasB = dB < D;
+  const bool hasB = live && dB < D;
+  double* ring = ring_base + grp * 4;        // [slot][PPW * 4]
 
-  double muA = a.lam[dA], lsA = a.lam[D + dA];
-  double muB = hasB ? a.lam[dB] : 0.0, lsB = hasB ? a.lam[D + dB] : 0.0;
+  const int own = lane & 3;                  // 0 muA, 1 muB, 2 lsA, 3 lsB
+  const long long own_idx = (own & 2 ? D : 0) + (own & 1 ? dB : dA);
+  const bool own_ok = live && (hasB || !(own & 1));
+  const bool updater = gl < 4 && own_ok;
+  double lam_own = own_ok ? a.lam[own_idx] : 0.0;
+  double s_own = exp(lam_own);
+  double muA = group_bcast<PPW>(lam_own, 0, upper), muB = group_bcast<PPW>(lam_own, 1, upper);
+  double sA = group_bcast<PPW>(s_own, 2, upper), sB = group_bcast<PPW>(s_own, 3, upper);
 
-  // adagrad window: lane k < W holds ring slot k for the pair's 4 parameters
-  double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0;
-  if (!a.emit_grad && lane < W) {
-    const double* rs = a.ring + (long long)lane * P;
-    r0 = rs[dA];
-    r2 = rs[D + dA];
-    if (hasB) {
-      r1 = rs[dB];
-      r3 = rs[D + dB];
-    }
+  int slot = 0, cnt = 0;
+  if (!a.emit_grad) {
+    if (gl < 4)
+      for (int k = 0; k < W; ++k)
+        ring[k * 4 * PPW + gl] = own_ok ? a.ring[(long long)k * P + own_idx] : 0.0;
+    slot = (int)(a.step0 % W);
+    cnt = a.step0 < W ? (int)a.step0 : W;
   }
   const Rng rng{a.k0, a.k1, a.stream};
-  const double dN = (double)N;
+  const double invN = 1.0 / (double)N;
 
   for (int s = 0; s < a.n_steps; ++s) {
     const long long i = a.step0 + s;
-    const long long ri = a.rng_step0 + s;
-    const double sA = exp(lsA), sB = exp(lsB);
+    const uint32_t ri = (uint32_t)(a.rng_step0 + s);
     double gA = 0.0, gB = 0.0, hA = 0.0, hB = 0.0, v = 0.0;
-    for (int n = lane; n < N; n += 64) {
+#pragma unroll 1
+    for (int n = gl; n < N; n += LPP) {
       double eA, eB;
       if constexpr (HOST) {
         const double* row = a.noise + ((long long)s * N + n) * D;
-        eA = row[dA];
+        eA = live ? row[dA] : 0.0;
         eB = hasB ? row[dB] : 0.0;
       } else {
-        normal_pair(rng.draw((uint32_t)w, (uint32_t)n, (uint32_t)ri, 0u), eA, eB);
+        normal_pair(rng.draw((uint32_t)w, (uint32_t)n, ri, 0u), eA, eB);
         if constexpr (TFAM) {
           double GA, GB;
-          gamma_pair(rng, (uint32_t)w, (uint32_t)n, (uint32_t)ri, a.shape, GA, GB);
+          gamma_pair(rng, (uint32_t)w, (uint32_t)n, ri, a.shape, GA, GB);
           eA = a.t_scale * eA / sqrt(GA);
           eB = a.t_scale * eB / sqrt(GB);
         }
       }
       double dg;
       const double xA = eA * sA + muA;
-      v += TGT::lp1(xA, dg);
+      const double lpA = TGT::lp1(xA, dg);
       gA += dg;
       hA += dg * eA;
-      if (hasB) {
-        const double xB = eB * sB + muB;
-        v += TGT::lp1(xB, dg);
-        gB += dg;
-        hB += dg * eB;
-      }
+      const double xB = eB * sB + muB;
+      const double lpB = TGT::lp1(xB, dg);
+      v += hasB ? lpA + lpB : lpA;
+      gB += dg;
+      hB += dg * eB;
     }
-    gA = wave_sum(gA);
-    gB = wave_sum(gB);
-    hA = wave_sum(hA);
-    hB = wave_sum(hB);
-    v = wave_sum(v);
-
+    const double S = reduce_scatter4<PPW>(lane, gA, gB, hA, hB);
+    v = group_sum<PPW>(v);
     // d/dmu = -mean g ; d/dlog sigma = -(1 + sigma * mean(g * eps))
-    const double gmA = -(gA / dN), gmB = -(gB / dN);
-    const double gsA = -(1.0 + sA * (hA / dN)), gsB = hasB ? -(1.0 + sB * (hB / dN)) : 0.0;
-    if (lane == 0) a.vpart[(long long)s * a.n_waves + w] = (hasB ? lsA + lsB : lsA) + v / dN;
+    const double m = S * invN;
+    const double g_own = own < 2 ? -m : -(1.0 + s_own * m);
+    // cross-lane reads with every lane active (a readlane of a lane outside the
+    // exec mask may see a register the compiler did not keep for that lane)
+    const double lsA_b = group_bcast<PPW>(lam_own, 2, upper);
+    const double lsB_b = group_bcast<PPW>(lam_own, 3, upper);
+    const double vpart = (hasB ? lsA_b + lsB_b : lsA_b) + v * invN;
+    if (gl == 0 && live) a.vpart[(long long)s * a.n_waves + w] = vpart;
 
     if (a.emit_grad) {
-      if (lane == 0) a.grad[dA] = gmA;
-      if (lane == 1 && hasB) a.grad[dB] = gmB;
-      if (lane == 2) a.grad[D + dA] = gsA;
-      if (lane == 3 && hasB) a.grad[D + dB] = gsB;
+      if (updater) a.grad[own_idx] = g_own;
       continue;
     }
 
-    // window push (vb.py:365-370): the slot of step i is i % W
-    const int slot = (int)(i % W);
-    if (lane == slot) {
-      r0 = gmA;
-      r1 = gmB;
-      r2 = gsA;
-      r3 = gsB;
-    }
-    const int cnt = (i + 1 < W) ? (int)(i + 1) : W;
-    const int oldest = (cnt < W) ? 0 : (int)((i + 1) % W);
-    // accum = sum over the window of g^2, oldest first (vb.py:371-373)
-    double q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
+    // window push (vb.py:365-370); accum = sum of g^2 over the window, oldest
+    // first (vb.py:371-373), read from this wave's LDS ring.
+    if (gl < 4) ring[slot * 4 * PPW + gl] = g_own;
+    cnt = cnt < W ? cnt + 1 : W;
+    int L = (cnt < W) ? 0 : (slot + 1 == W ? 0 : slot + 1);
+    double q = 0.0;
     for (int k = 0; k < cnt; ++k) {
-      int L = oldest + k;
-      if (L >= W) L -= W;
-      const double t0 = readlane_f64(r0, L), t1 = readlane_f64(r1, L);
-      const double t2 = readlane_f64(r2, L), t3 = readlane_f64(r3, L);
-      q0 = __dadd_rn(q0, __dmul_rn(t0, t0));
-      q1 = __dadd_rn(q1, __dmul_rn(t1, t1));
-      q2 = __dadd_rn(q2, __dmul_rn(t2, t2));
-      q3 = __dadd_rn(q3, __dmul_rn(t3, t3));
+      const double t = ring[L * 4 * PPW + (gl & 3)];
+      q = __dadd_rn(q, __dmul_rn(t, t));
+      L = (L + 1 == W) ? 0 : L + 1;
     }
-    const double lr = a.lr.at(i);
     // lam - lr * g / sqrt(eps + accum)   (vb.py:374)
-    muA = __dsub_rn(muA, __dmul_rn(lr, gmA) / sqrt(__dadd_rn(a.eps, q0)));
-    lsA = __dsub_rn(lsA, __dmul_rn(lr, gsA) / sqrt(__dadd_rn(a.eps, q2)));
-    if (hasB) {
-      muB = __dsub_rn(muB, __dmul_rn(lr, gmB) / sqrt(__dadd_rn(a.eps, q1)));
-      lsB = __dsub_rn(lsB, __dmul_rn(lr, gsB) / sqrt(__dadd_rn(a.eps, q3)));
-    }
-    if (i >= a.hist_start) {
-      double* h = a.hist + (i - a.hist_start) * P;
-      if (lane == 0) h[dA] = muA;
-      if (lane == 1 && hasB) h[dB] = muB;
-      if (lane == 2) h[D + dA] = lsA;
-      if (lane == 3 && hasB) h[D + dB] = lsB;
-    }
+    lam_own = __dsub_rn(lam_own, __dmul_rn(a.lr.at(i), g_own) / sqrt(__dadd_rn(a.eps, q)));
+    s_own = exp(lam_own);
+    muA = group_bcast<PPW>(lam_own, 0, upper);
+    muB = group_bcast<PPW>(lam_own, 1, upper);
+    sA = group_bcast<PPW>(s_own, 2, upper);
+    sB = group_bcast<PPW>(s_own, 3, upper);
+    if (i >= a.hist_start && updater) a.hist[(i - a.hist_start) * P + own_idx] = lam_own;
+    slot = (slot + 1 == W) ? 0 : slot + 1;
   }
 
-  if (!a.emit_grad) {
-    if (lane == 0) a.lam[dA] = muA;
-    if (lane == 1 && hasB) a.lam[dB] = muB;
-    if (lane == 2) a.lam[D + dA] = lsA;
-    if (lane == 3 && hasB) a.lam[D + dB] = lsB;
-    if (lane < W) {
-      double* rs = a.ring + (long long)lane * P;
-      rs[dA] = r0;
-      rs[D + dA] = r2;
-      if (hasB) {
-        rs[dB] = r1;
-        rs[D + dB] = r3;
-      }
-    }
+  if (!a.emit_grad && updater) {
+    a.lam[own_idx] = lam_own;
+    for (int k = 0; k < W; ++k) a.ring[(long long)k * P + own_idx] = ring[k * 4 * PPW + gl];
+  }
+}
+
+// Grid: blocks [0, a.blocks2) run two column pairs per wave (32 lanes each),
+// the remaining blocks one pair per wave.  The split balances the work per
+// SIMD with every wave resident; it only affects speed.
+template <class TGT, bool TFAM, bool HOST>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(3)))
+void sep_kernel(SepArgs a) {
+  __shared__ double s_ring[4][64 * 8];  // per wave: [slot < 64][PPW * 4 params]
+  const int wid = threadIdx.x >> 6;
+  if ((int)blockIdx.x < a.blocks2) {
+    const int wave = blockIdx.x * 4 + wid;           // 2 pairs per wave
+    if (wave * 2 >= a.pairs2) return;
+    sep_body<TGT, TFAM, HOST, 2>(a, s_ring[wid], wave);
+  } else {
+    const int wave = (blockIdx.x - a.blocks2) * 4 + wid;  // 1 pair per wave
+    const int pair = a.pairs2 + wave;
+    if (pair >= a.n_pairs) return;
+    // sep_body<.., 1> indexes pairs as wave * 1 + 0
+    sep_body<TGT, TFAM, HOST, 1>(a, s_ring[wid], pair);
   }
 }
 
@@ -235,7 +276,7 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
     for (int q = tid; q < W * P; q += 256) s_ring[q] = ring_g[q];
   __syncthreads();
 
-  const Rng rng{a.k0, a.k1, (uint32_t)(a.stream + (uint32_t)prob)};
+  const Rng rng{a.k0, a.k1, (uint32_t)(a.stream + (uint32_t)prob * a.stream_stride)};
   const double c0 = TFAM ? 0.0 : 0.5 * D * (1.0 + kLog2Pi);
 
   for (int s = 0; s < a.n_steps; ++s) {
@@ -586,9 +627,35 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
 // -------------------------------------------------------------------------
 bool target_separable(int tgt) { return tgt == 0 || tgt == 1; }
 
+// Split of the column pairs between 2-pair and 1-pair waves.  VB_SEP_MODE:
+// "1" all single, "2" all double, default "mix": per SIMD (1024 of them) two
+// double waves + single waves for the remainder, so the per-SIMD work is even
+// when blocks are dealt round-robin over the CUs.
+static void sep_split(SepArgs& a) {
+  const char* e = getenv("VB_SEP_MODE");
+  const int np = a.n_pairs;
+  int pairs2;
+  if (e && e[0] == '1') {
+    pairs2 = 0;
+  } else if (e && e[0] == '2') {
+    pairs2 = np & ~1;
+  } else {
+    // 1024 SIMDs: give each SIMD up to two double waves (4 pairs) first
+    const int cap2 = 1024 * 2 * 2;
+    pairs2 = np >= cap2 + 1024 ? cap2 : (np > 4096 ? (np - 1024) & ~1 : np & ~1);
+    if (np <= 4096) pairs2 = 0;  // small problems: one pair per wave fits resident
+  }
+  pairs2 &= ~7;                   // whole blocks of 4 double waves
+  a.pairs2 = pairs2;
+  a.blocks2 = pairs2 / 8;
+  const int rest = np - pairs2;
+  a.blocks1 = (rest + 3) / 4;
+}
+
 template <class TGT>
-static hipError_t sep_dispatch(int fam, bool host, const SepArgs& a, hipStream_t s) {
-  const dim3 grid((a.n_pairs + 3) / 4), block(256);
+static hipError_t sep_dispatch(int fam, bool host, SepArgs a, hipStream_t s) {
+  sep_split(a);
+  const dim3 grid(a.blocks2 + a.blocks1), block(256);
   if (host) {
     // host noise holds standardized draws for either family
     hipLaunchKernelGGL((sep_kernel<TGT, false, true>), grid, block, 0, s, a);

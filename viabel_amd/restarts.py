@@ -1,0 +1,117 @@
+"""Independent optimisation restarts sharded over GPUs.
+
+The reference's restart loop (rmsprop_IA_optimize_with_rhat, viabel/vb.py:
+417-421) runs restarts one after another on one CPU.  Here restart r lives on
+rank r % world; each rank runs all of its restarts in ONE device-resident
+adagrad launch chain (vb_run with n_problems = local restarts, one workgroup
+per restart), then, per restart, draws M log weights on the device and reduces
+them to the divergence / Wasserstein bounds (viabel/bounds.py) and the PSIS
+k-hat (notebooks/psis.py).  The only collective is one all_gather of a
+fixed-size summary record per restart at the end (RCCL over xGMI on the GPU
+pool; gloo in the CPU tests).  There is no data-path collective.
+
+Summary record (float64), per restart:
+  [restart id, ELBO estimate (mean log weight), CUBO-based d2, W1, W2,
+   mean_error, std_error, cov_error, k_hat, final objective value, lambda*(P)]
+"""
+import numpy as np
+
+from . import _native as nat
+
+__all__ = ['shard', 'run_restarts', 'gather_records', 'RECORD_HEAD']
+
+RECORD_HEAD = ['restart', 'elbo', 'd2', 'W1', 'W2', 'mean_error', 'std_error', 'cov_error',
+               'khat', 'final_value']
+
+
+def shard(n_restarts, rank, world):
+    """Restart ids owned by `rank`: r = rank, rank + world, ..."""
+    return list(range(rank, n_restarts, world))
+
+
+def default_inits(n_restarts, P, scale=0.5, base=None):
+    """init_r = base + RandomState(r).randn(P) * scale (SURVEY §8d config 5,
+    the fixed-scale variant of vb.py:420-421)."""
+    base = np.zeros(P) if base is None else np.asarray(base, dtype=float)
+    return np.stack([base + np.random.RandomState(r).randn(P) * scale for r in range(n_restarts)])
+
+
+def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bounds,
+                    learning_rate, learning_rate_end, window, seed, stream_base, stride):
+    """Fit this rank's restarts in ONE device run (one workgroup per restart;
+    restart r draws from Philox stream 1 + r whatever the sharding) and
+    summarise each with device log weights, bounds and PSIS."""
+    from . import vb, bounds, psis, experiments
+    fam = family_factory()
+    obj = vb.black_box_klvi(fam, target, n_samples)
+    run = vb.DeviceRun(obj, n_iters, inits, window=window, learning_rate=learning_rate,
+                       learning_rate_end=learning_rate_end)
+    run.advance_philox(n_iters, seed, stream_base, 0, stream_stride=stride)
+    _, _, vals, smooth = run.result()
+    recs = []
+    for j, r in enumerate(ids):
+        opt = smooth[j]
+        bfam = family_factory()
+        bfam.stream = (1 << 20) + r          # bound draws: a Philox stream of their own
+        _, lw = experiments.log_weights(target, bfam, opt, n_bounds, return_samples=False)
+        elbo = float(np.mean(lw))
+        res = bounds.all_bounds(lw, q_var=bfam.mean_and_cov(opt)[1],
+                                moment_bound_fn=lambda p: bfam.pth_moment(p, opt))
+        _, khat = psis.psislw(lw)
+        recs.append(np.concatenate([[r, elbo, res['d2'], res['W1'], res['W2'],
+                                     res['mean_error'], res['std_error'], res['cov_error'],
+                                     khat, vals[j, -1]], opt]))
+    return np.array(recs)
+
+
+def gather_records(local, n_restarts, width, group=None):
+    """all_gather of the fixed-size per-restart records; returns the full
+    [n_restarts, width] table ordered by restart id on every rank."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    per_rank = -(-n_restarts // world)
+    backend = dist.get_backend(group)
+    dev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' else torch.device('cpu')
+    buf = torch.full((per_rank, width), float('nan'), dtype=torch.float64, device=dev)
+    if len(local):
+        buf[:len(local)] = torch.as_tensor(np.asarray(local), dtype=torch.float64, device=dev)
+    out = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(out, buf, group=group)
+    table = torch.cat(out).cpu().numpy()
+    table = table[~np.isnan(table[:, 0])]
+    return table[np.argsort(table[:, 0])]
+
+
+def run_restarts(family_factory, target, n_restarts, n_iters, n_samples=100, n_bounds=1_000_000,
+                 learning_rate=.01, learning_rate_end=.001, window=10, inits=None, seed=0,
+                 group=None, compute=None):
+    """Fit n_restarts KLVI restarts sharded over the ranks of `group` (or this
+    process alone when torch.distributed is not initialised) and return the
+    gathered summary table (RECORD_HEAD + lambda*) on every rank.
+
+    `compute(ids, inits) -> records` replaces the device computation (tests use
+    it to run the sharding and the collective without a GPU)."""
+    try:
+        import torch.distributed as dist
+        dist_on = dist.is_available() and dist.is_initialized()
+    except ImportError:
+        dist_on = False
+    rank, world = (dist.get_rank(group), dist.get_world_size(group)) if dist_on else (0, 1)
+    fam0 = family_factory()
+    P = fam0.var_param_dim
+    if inits is None:
+        inits = default_inits(n_restarts, P)
+    ids = shard(n_restarts, rank, world)
+    local_inits = np.asarray(inits)[ids] if ids else np.zeros((0, P))
+    if compute is None:
+        local = (_native_compute(ids, local_inits, family_factory, target, n_iters, n_samples,
+                                 n_bounds, learning_rate, learning_rate_end, window, seed,
+                                 1 + rank, world)
+                 if ids else np.zeros((0, len(RECORD_HEAD) + P)))
+    else:
+        local = compute(ids, local_inits)
+    width = len(RECORD_HEAD) + P
+    if not dist_on:
+        return np.asarray(local)[np.argsort(np.asarray(local)[:, 0])]
+    return gather_records(local, n_restarts, width, group)

@@ -279,8 +279,9 @@ class DeviceRun:
         self.handle = h
         self.done = 0
 
-    def advance_philox(self, n_steps, seed, stream, step):
-        nz = nat.Noise(nat.NOISE_PHILOX, stream & 0xFFFFFF, seed, step, None)
+    def advance_philox(self, n_steps, seed, stream, step, stream_stride=1):
+        """Problem q draws from Philox stream `stream + q * stream_stride`."""
+        nz = nat.Noise(nat.NOISE_PHILOX, stream & 0xFFFFFF, seed, step, None, stream_stride)
         nat.check(nat.lib().vb_run_advance(self.handle, int(n_steps), nz))
         self.done += int(n_steps)
 
