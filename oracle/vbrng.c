@@ -10,13 +10,15 @@
  *    easy as 1, 2, 3", SC'11 (Random123).  Pinned by the Random123 known-answer
  *    vectors in tests/test_oracle_rng.py.
  *  - counter = (pair j, sample n, step, stream | purpose << 24), key = seed.
- *  - normal pair: Box-Muller on 53-bit uniforms u1 in (0,1), u2 in [0,1).
+ *  - normal pair: Box-Muller on 52-bit mantissa-fill uniforms u1 = (2m+1)2^-53,
+ *    u2 = m 2^-52 (m the top 52 bits of a 64-bit half of the block).
  *  - t draw: sqrt(df/2) * gauss / sqrt(gamma(df/2)), the structure of numpy's
  *    legacy standard_t; gamma by Marsaglia & Tsang (2000), proposals from
  *    purposes 1..64 with 32-bit uniforms.
  */
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 typedef struct { uint32_t v[4]; } blk;
 
@@ -46,11 +48,17 @@ static blk draw(uint64_t seed, uint32_t stream, uint32_t pair, uint32_t n, uint3
                 (uint32_t)(seed >> 32));
 }
 
+/* 52 random bits into the mantissa of a double in [1, 2) */
+static double unit_mantissa(uint32_t lo, uint32_t hi) {
+  uint64_t bits = 0x3FF0000000000000ull | (((((uint64_t)hi) << 32) | lo) >> 12);
+  double d;
+  memcpy(&d, &bits, sizeof d);
+  return d;
+}
+
 static void gauss2(blk w, double* z0, double* z1) {
-  uint64_t a = ((((uint64_t)w.v[1]) << 32) | w.v[0]) >> 11;
-  uint64_t b = ((((uint64_t)w.v[3]) << 32) | w.v[2]) >> 11;
-  double u1 = ((double)a + 0.5) * 0x1p-53;
-  double u2 = (double)b * 0x1p-53;
+  double u1 = unit_mantissa(w.v[0], w.v[1]) - 0x1.fffffffffffffp-1; /* (2m+1) 2^-53 */
+  double u2 = unit_mantissa(w.v[2], w.v[3]) - 1.0;                  /* m 2^-52 */
   double r = sqrt(-2.0 * log(u1));
   double th = 2.0 * M_PI * u2;
   *z0 = r * cos(th);

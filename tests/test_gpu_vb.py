@@ -287,7 +287,7 @@ def test_device_philox_noise_equals_c_oracle(kind, df, D):
                                rtol=2e-14, atol=1e-13)
 
 
-@pytest.mark.parametrize('mode', ['1', '2', 'mix'])
+@pytest.mark.parametrize('mode', ['1', '2', '4', 'mix', 'q'])
 @pytest.mark.parametrize('kind,df,D', [('gauss', None, 9001), ('t', 40.0, 8200), ('gauss', None, 17)])
 def test_sep_layouts_agree(mode, kind, df, D, monkeypatch):
     """The column-pair kernel's layouts (1 or 2 pairs per wavefront, or the

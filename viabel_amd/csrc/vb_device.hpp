@@ -6,7 +6,7 @@
 //    1+k = k-th Marsaglia-Tsang gamma proposal.  The layout makes every draw
 //    addressable, so kernels regenerate noise instead of storing it, and any
 //    tiling of (n, d) produces the same draws.
-//  * normal pair: Box-Muller on two 53-bit uniforms (u1 in (0,1), u2 in [0,1)).
+//  * normal pair: Box-Muller on two 52-bit uniforms (u1 in (0,1), u2 in [0,1)).
 //  * t draws follow numpy's legacy standard_t structure
 //    sqrt(df/2) * gauss / sqrt(gamma(df/2)) (numpy legacy distributions.c),
 //    with gamma by Marsaglia-Tsang (shape >= 1, which df > 2 guarantees).
@@ -139,12 +139,19 @@ __device__ __forceinline__ void sincospi_unit(double x, double& sn, double& cs) 
   cs = (k == 1 || k == 2) ? -b : b;
 }
 
-// Two standard normals from one Philox block.
+// Uniforms from 52 random bits by filling the mantissa of a double in [1, 2):
+//   u1 = 1.m - (1 - 2^-53) = (2m + 1) 2^-53  in (0, 1)   (never 0: log is finite)
+//   u2 = 1.m - 1            = m 2^-52         in [0, 1)
+__device__ __forceinline__ double unit_mantissa(uint32_t lo, uint32_t hi) {
+  const uint32_t mlo = __builtin_amdgcn_alignbit(hi, lo, 12);
+  const uint32_t mhi = (hi >> 12) | 0x3FF00000u;
+  return __hiloint2double((int)mhi, (int)mlo);
+}
+
+// Two standard normals from one Philox block (Box-Muller).
 __device__ __forceinline__ void normal_pair(u4 w, double& z0, double& z1) {
-  const uint64_t a = ((((uint64_t)w.y) << 32) | w.x) >> 11;
-  const uint64_t b = ((((uint64_t)w.w) << 32) | w.z) >> 11;
-  const double u1 = ((double)a + 0.5) * 0x1p-53;
-  const double u2 = (double)b * 0x1p-53;
+  const double u1 = unit_mantissa(w.x, w.y) - 0x1.fffffffffffffp-1;
+  const double u2 = unit_mantissa(w.z, w.w) - 1.0;
   const double r = sqrt_pos(-2.0 * log_unit(u1));
   double s, c;
   sincospi_unit(2.0 * u2, s, c);
@@ -240,6 +247,17 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
   v += dpp_f64<0x140>(v);  // row_mirror
   v = swap_sum16(v);       // rows 0+1, 2+3
   return swap_sum32(v);    // halves
+}
+
+// Sum over lanes l = c (mod 4) of a group of 64/PPW lanes (all lanes of the
+// group receive their residue class's total).
+template <int PPW>
+__device__ __forceinline__ double stride4_sum(double k) {
+  k += dpp_f64<0x124>(k);  // row_ror:4
+  k += dpp_f64<0x128>(k);  // row_ror:8
+  if constexpr (PPW <= 2) k = swap_sum16(k);  // rows 0+1, 2+3
+  if constexpr (PPW == 1) k = swap_sum32(k);  // halves
+  return k;
 }
 
 __device__ __forceinline__ double wave_max(double v) {

@@ -32,10 +32,10 @@ namespace vbk {
 // column-pair persistent KLVI kernel
 // -------------------------------------------------------------------------
 // Reduce-scatter of the four per-lane partial sums (gA, gB, hA, hB) over the
-// lanes of one column pair (64 lanes for PPW = 1, 32 for PPW = 2): lane l ends
-// with the group total of quantity (l & 3).  Two DPP exchange steps hand each
-// lane one quantity, two row rotations and one or two permlane swaps finish the
-// sum: about a third of the instructions of four all-reduces.
+// LPP = 64 / PPW lanes of one column pair: lane l ends with the group total of
+// quantity (l & 3).  Two DPP exchange steps hand each lane one quantity; two
+// row rotations (16 lanes) and, for groups wider than a row, permlane swaps
+// finish the sum: about a third of the instructions of four all-reduces.
 template <int PPW>
 __device__ __forceinline__ double reduce_scatter4(int lane, double gA, double gB, double hA,
                                                   double hB) {
@@ -45,11 +45,7 @@ __device__ __forceinline__ double reduce_scatter4(int lane, double gA, double gB
   kh += dpp_f64<0xB1>(b0 ? hA : hB);
   double k = b1 ? kh : kg;
   k += dpp_f64<0x4E>(b1 ? kg : kh);   // quad_perm [2,3,0,1]
-  k += dpp_f64<0x124>(k);             // row_ror:4  (same lane & 3)
-  k += dpp_f64<0x128>(k);             // row_ror:8
-  k = swap_sum16(k);                  // rows 0+1 and 2+3
-  if constexpr (PPW == 1) k = swap_sum32(k);
-  return k;
+  return stride4_sum<PPW>(k);
 }
 
 // Sum over the lanes of one column-pair group (all lanes get their group's total).
@@ -57,51 +53,77 @@ template <int PPW>
 __device__ __forceinline__ double group_sum(double v) {
   v += dpp_f64<0xB1>(v);
   v += dpp_f64<0x4E>(v);
-  v += dpp_f64<0x141>(v);
-  v += dpp_f64<0x140>(v);
-  v = swap_sum16(v);
-  if constexpr (PPW == 1) v = swap_sum32(v);
-  return v;
+  return stride4_sum<PPW>(v);
 }
 
 // Value of lane (group base + k) for every lane of the group.
 template <int PPW>
-__device__ __forceinline__ double group_bcast(double v, int k, bool upper) {
-  if constexpr (PPW == 1) return readlane_f64(v, k);
-  const double lo = readlane_f64(v, k), hi = readlane_f64(v, 32 + k);
-  return upper ? hi : lo;
+__device__ __forceinline__ double group_bcast(double v, int k, int grp) {
+  constexpr int LPP = 64 / PPW;
+  if constexpr (PPW == 1) {
+    return readlane_f64(v, k);
+  } else if constexpr (PPW == 2) {
+    const double lo = readlane_f64(v, k), hi = readlane_f64(v, LPP + k);
+    return grp ? hi : lo;
+  } else {
+    const double g0 = readlane_f64(v, k), g1 = readlane_f64(v, LPP + k);
+    const double g2 = readlane_f64(v, 2 * LPP + k), g3 = readlane_f64(v, 3 * LPP + k);
+    return grp == 0 ? g0 : grp == 1 ? g1 : grp == 2 ? g2 : g3;
+  }
 }
 
-// PPW column pairs per wavefront (PPW in {1, 2}); pair index = wave * PPW + (lane >> 5 for PPW 2).
-template <class TGT, bool TFAM, bool HOST, int PPW>
+// 1 / sqrt(y), y > 0: v_rsq_f64 seed + two Newton steps (~1 ulp).
+__device__ __forceinline__ double rsqrt_pos(double y) {
+  double r = __builtin_amdgcn_rsq(y);
+  const double hy = 0.5 * y;
+  r = r * fma(-hy * r, r, 1.5);
+  r = r * fma(-hy * r, r, 1.5);
+  return r;
+}
+
+// PPW column pairs per wavefront (PPW in {1, 2, 4}); pair = wave * PPW + lane / LPP.
+// REGRING: the adagrad window (W <= 16) lives in registers, one entry per
+// (lane, j): slot j * (LPP / 4) + gl / 4 of parameter gl & 3; otherwise in LDS.
+template <class TGT, bool TFAM, bool HOST, int PPW, bool REGRING>
 __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, int wave) {
-  constexpr int LPP = 64 / PPW;  // lanes per column pair
+  constexpr int LPP = 64 / PPW;       // lanes per column pair
+  constexpr int SL = LPP / 4;         // slot lanes per parameter
   const int lane = threadIdx.x & 63;
-  const int grp = PPW == 1 ? 0 : (lane >> 5);
-  const bool upper = grp == 1;
-  const int gl = lane & (LPP - 1);           // lane within the pair's group
-  const int w = wave * PPW + grp;            // column pair of this lane
-  const bool live = w < a.n_pairs;           // the upper group of the last wave may be empty
+  const int grp = lane / LPP;
+  const int gl = lane & (LPP - 1);    // lane within the pair's group
+  const int w = wave * PPW + grp;     // column pair of this lane
+  const bool live = w < a.n_pairs;    // trailing groups of the last wave may be empty
   const int D = a.D, N = a.N, W = a.W;
   const long long P = 2LL * D;
   const int dA = 2 * w, dB = 2 * w + 1;
   const bool hasB = live && dB < D;
-  double* ring = ring_base + grp * 4;        // [slot][PPW * 4]
+  double* ring = ring_base + grp * 4;  // LDS ring [slot][PPW * 4]
 
-  const int own = lane & 3;                  // 0 muA, 1 muB, 2 lsA, 3 lsB
+  const int own = lane & 3;            // 0 muA, 1 muB, 2 lsA, 3 lsB
   const long long own_idx = (own & 2 ? D : 0) + (own & 1 ? dB : dA);
   const bool own_ok = live && (hasB || !(own & 1));
   const bool updater = gl < 4 && own_ok;
   double lam_own = own_ok ? a.lam[own_idx] : 0.0;
   double s_own = exp(lam_own);
-  double muA = group_bcast<PPW>(lam_own, 0, upper), muB = group_bcast<PPW>(lam_own, 1, upper);
-  double sA = group_bcast<PPW>(s_own, 2, upper), sB = group_bcast<PPW>(s_own, 3, upper);
+  double muA = group_bcast<PPW>(lam_own, 0, grp), muB = group_bcast<PPW>(lam_own, 1, grp);
+  double sA = group_bcast<PPW>(s_own, 2, grp), sB = group_bcast<PPW>(s_own, 3, grp);
 
   int slot = 0, cnt = 0;
+  double rg[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) rg[j] = 0.0;
   if (!a.emit_grad) {
-    if (gl < 4)
-      for (int k = 0; k < W; ++k)
-        ring[k * 4 * PPW + gl] = own_ok ? a.ring[(long long)k * P + own_idx] : 0.0;
+    if constexpr (REGRING) {
+#pragma unroll
+      for (int j = 0; j < PPW; ++j) {
+        const int sl = j * SL + (gl >> 2);
+        if (sl < W && own_ok) rg[j] = a.ring[(long long)sl * P + own_idx];
+      }
+    } else {
+      if (gl < 4)
+        for (int k = 0; k < W; ++k)
+          ring[k * 4 * PPW + gl] = own_ok ? a.ring[(long long)k * P + own_idx] : 0.0;
+    }
     slot = (int)(a.step0 % W);
     cnt = a.step0 < W ? (int)a.step0 : W;
   }
@@ -146,8 +168,8 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
     const double g_own = own < 2 ? -m : -(1.0 + s_own * m);
     // cross-lane reads with every lane active (a readlane of a lane outside the
     // exec mask may see a register the compiler did not keep for that lane)
-    const double lsA_b = group_bcast<PPW>(lam_own, 2, upper);
-    const double lsB_b = group_bcast<PPW>(lam_own, 3, upper);
+    const double lsA_b = group_bcast<PPW>(lam_own, 2, grp);
+    const double lsB_b = group_bcast<PPW>(lam_own, 3, grp);
     const double vpart = (hasB ? lsA_b + lsB_b : lsA_b) + v * invN;
     if (gl == 0 && live) a.vpart[(long long)s * a.n_waves + w] = vpart;
 
@@ -156,52 +178,74 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
       continue;
     }
 
-    // window push (vb.py:365-370); accum = sum of g^2 over the window, oldest
-    // first (vb.py:371-373), read from this wave's LDS ring.
-    if (gl < 4) ring[slot * 4 * PPW + gl] = g_own;
+    // window push (vb.py:365-370) and accum = sum of g^2 over the window
+    // (vb.py:371-373).  Slots outside the window hold 0 or stale values that
+    // the count mask removes.
     cnt = cnt < W ? cnt + 1 : W;
-    int L = (cnt < W) ? 0 : (slot + 1 == W ? 0 : slot + 1);
-    double q = 0.0;
-    for (int k = 0; k < cnt; ++k) {
-      const double t = ring[L * 4 * PPW + (gl & 3)];
-      q = __dadd_rn(q, __dmul_rn(t, t));
-      L = (L + 1 == W) ? 0 : L + 1;
+    double q;
+    if constexpr (REGRING) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < PPW; ++j) {
+        const int sl = j * SL + (gl >> 2);
+        if (sl == slot) rg[j] = g_own;
+        const double t = rg[j];
+        acc += (sl < W) ? t * t : 0.0;
+      }
+      q = stride4_sum<PPW>(acc);
+    } else {
+      if (gl < 4) ring[slot * 4 * PPW + gl] = g_own;
+      int L = (cnt < W) ? 0 : (slot + 1 == W ? 0 : slot + 1);
+      q = 0.0;
+      for (int k = 0; k < cnt; ++k) {
+        const double t = ring[L * 4 * PPW + (gl & 3)];
+        q += t * t;
+        L = (L + 1 == W) ? 0 : L + 1;
+      }
     }
     // lam - lr * g / sqrt(eps + accum)   (vb.py:374)
-    lam_own = __dsub_rn(lam_own, __dmul_rn(a.lr.at(i), g_own) / sqrt(__dadd_rn(a.eps, q)));
+    lam_own = lam_own - (a.lr.at(i) * g_own) * rsqrt_pos(a.eps + q);
     s_own = exp(lam_own);
-    muA = group_bcast<PPW>(lam_own, 0, upper);
-    muB = group_bcast<PPW>(lam_own, 1, upper);
-    sA = group_bcast<PPW>(s_own, 2, upper);
-    sB = group_bcast<PPW>(s_own, 3, upper);
+    muA = group_bcast<PPW>(lam_own, 0, grp);
+    muB = group_bcast<PPW>(lam_own, 1, grp);
+    sA = group_bcast<PPW>(s_own, 2, grp);
+    sB = group_bcast<PPW>(s_own, 3, grp);
     if (i >= a.hist_start && updater) a.hist[(i - a.hist_start) * P + own_idx] = lam_own;
     slot = (slot + 1 == W) ? 0 : slot + 1;
   }
 
-  if (!a.emit_grad && updater) {
-    a.lam[own_idx] = lam_own;
-    for (int k = 0; k < W; ++k) a.ring[(long long)k * P + own_idx] = ring[k * 4 * PPW + gl];
+  if (!a.emit_grad && own_ok) {
+    if (gl < 4) a.lam[own_idx] = lam_own;
+    if constexpr (REGRING) {
+#pragma unroll
+      for (int j = 0; j < PPW; ++j) {
+        const int sl = j * SL + (gl >> 2);
+        if (sl < W) a.ring[(long long)sl * P + own_idx] = rg[j];
+      }
+    } else {
+      if (gl < 4)
+        for (int k = 0; k < W; ++k) a.ring[(long long)k * P + own_idx] = ring[k * 4 * PPW + gl];
+    }
   }
 }
 
-// Grid: blocks [0, a.blocks2) run two column pairs per wave (32 lanes each),
-// the remaining blocks one pair per wave.  The split balances the work per
-// SIMD with every wave resident; it only affects speed.
-template <class TGT, bool TFAM, bool HOST>
+// Grid: blocks [0, a.blocks2) run PPW_BIG column pairs per wave, the remaining
+// blocks one pair per wave.  The split balances the work per SIMD with every
+// wave resident; it affects speed only.
+template <class TGT, bool TFAM, bool HOST, int PPW_BIG, bool REGRING>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(3)))
 void sep_kernel(SepArgs a) {
-  __shared__ double s_ring[4][64 * 8];  // per wave: [slot < 64][PPW * 4 params]
+  __shared__ double s_ring[REGRING ? 1 : 4][REGRING ? 1 : 64 * 4 * PPW_BIG];
   const int wid = threadIdx.x >> 6;
+  double* ring = REGRING ? nullptr : &s_ring[REGRING ? 0 : wid][0];
   if ((int)blockIdx.x < a.blocks2) {
-    const int wave = blockIdx.x * 4 + wid;           // 2 pairs per wave
-    if (wave * 2 >= a.pairs2) return;
-    sep_body<TGT, TFAM, HOST, 2>(a, s_ring[wid], wave);
+    const int wave = blockIdx.x * 4 + wid;
+    if (wave * PPW_BIG >= a.pairs2) return;
+    sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave);
   } else {
-    const int wave = (blockIdx.x - a.blocks2) * 4 + wid;  // 1 pair per wave
-    const int pair = a.pairs2 + wave;
+    const int pair = a.pairs2 + (blockIdx.x - a.blocks2) * 4 + wid;
     if (pair >= a.n_pairs) return;
-    // sep_body<.., 1> indexes pairs as wave * 1 + 0
-    sep_body<TGT, TFAM, HOST, 1>(a, s_ring[wid], pair);
+    sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair);
   }
 }
 
@@ -627,42 +671,63 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
 // -------------------------------------------------------------------------
 bool target_separable(int tgt) { return tgt == 0 || tgt == 1; }
 
-// Split of the column pairs between 2-pair and 1-pair waves.  VB_SEP_MODE:
-// "1" all single, "2" all double, default "mix": per SIMD (1024 of them) two
-// double waves + single waves for the remainder, so the per-SIMD work is even
-// when blocks are dealt round-robin over the CUs.
-static void sep_split(SepArgs& a) {
+// Split of the column pairs between multi-pair (PPW_BIG) and 1-pair waves.
+// VB_SEP_MODE: "1" all single; "2" / "4" all 2- / 4-pair; "mix": per SIMD
+// (1024 of them) two 2-pair waves, then 1-pair waves for the rest; "q"
+// (default, measured fastest: profiles/r01/ab_layouts_q.json): one 4-pair wave
+// per SIMD, then 1-pair waves.  Blocks of big waves come first so round-robin
+// dispatch deals the same mix to every CU.
+static int sep_split(SepArgs& a, int& big) {
   const char* e = getenv("VB_SEP_MODE");
   const int np = a.n_pairs;
   int pairs2;
+  big = 2;
   if (e && e[0] == '1') {
     pairs2 = 0;
   } else if (e && e[0] == '2') {
-    pairs2 = np & ~1;
-  } else {
-    // 1024 SIMDs: give each SIMD up to two double waves (4 pairs) first
+    pairs2 = np;
+  } else if (e && e[0] == '4') {
+    big = 4;
+    pairs2 = np;
+  } else if (e && e[0] == 'm') {  // "mix": two 2-pair waves + 1-pair waves per SIMD
     const int cap2 = 1024 * 2 * 2;
-    pairs2 = np >= cap2 + 1024 ? cap2 : (np > 4096 ? (np - 1024) & ~1 : np & ~1);
-    if (np <= 4096) pairs2 = 0;  // small problems: one pair per wave fits resident
+    pairs2 = np >= cap2 + 1024 ? cap2 : (np > 4096 ? np - 1024 : 0);
+  } else {                         // default "q": one 4-pair wave + 1-pair waves per SIMD
+    big = 4;
+    pairs2 = np > 4096 + 1024 ? 4096 : (np > 1024 ? np - 1024 : 0);
   }
-  pairs2 &= ~7;                   // whole blocks of 4 double waves
+  pairs2 -= pairs2 % (4 * big);   // whole blocks of 4 big waves
   a.pairs2 = pairs2;
-  a.blocks2 = pairs2 / 8;
+  a.blocks2 = pairs2 / (4 * big);
   const int rest = np - pairs2;
   a.blocks1 = (rest + 3) / 4;
+  return big;
+}
+
+template <class TGT, bool TFAM, bool HOST, bool REG>
+static void sep_launch_ppw(int big, const SepArgs& a, hipStream_t s) {
+  const dim3 grid(a.blocks2 + a.blocks1), block(256);
+  if (big == 4)
+    hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 4, REG>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 2, REG>), grid, block, 0, s, a);
 }
 
 template <class TGT>
 static hipError_t sep_dispatch(int fam, bool host, SepArgs a, hipStream_t s) {
-  sep_split(a);
-  const dim3 grid(a.blocks2 + a.blocks1), block(256);
+  int big;
+  sep_split(a, big);
+  const bool reg = a.W <= 16 || a.emit_grad;
   if (host) {
     // host noise holds standardized draws for either family
-    hipLaunchKernelGGL((sep_kernel<TGT, false, true>), grid, block, 0, s, a);
+    if (reg) sep_launch_ppw<TGT, false, true, true>(big, a, s);
+    else sep_launch_ppw<TGT, false, true, false>(big, a, s);
   } else if (fam == 1) {
-    hipLaunchKernelGGL((sep_kernel<TGT, true, false>), grid, block, 0, s, a);
+    if (reg) sep_launch_ppw<TGT, true, false, true>(big, a, s);
+    else sep_launch_ppw<TGT, true, false, false>(big, a, s);
   } else {
-    hipLaunchKernelGGL((sep_kernel<TGT, false, false>), grid, block, 0, s, a);
+    if (reg) sep_launch_ppw<TGT, false, false, true>(big, a, s);
+    else sep_launch_ppw<TGT, false, false, false>(big, a, s);
   }
   return hipGetLastError();
 }
