@@ -76,3 +76,21 @@ TARGETS = {
     'funnel': funnel,
     'eight_schools_ncp': eight_schools_ncp,
 }
+
+
+class CorrGauss:
+    """corr_gauss target: N(0, Sigma*) with
+    Sigma* = A A^T / D + I, A = RandomState(seed).randn(D, D)."""
+
+    def __init__(self, dim, seed=512):
+        a = np.random.RandomState(seed).randn(dim, dim)
+        self.sigma = a @ a.T / dim + np.eye(dim)
+        self.prec = np.linalg.inv(self.sigma)
+        self.prec = 0.5 * (self.prec + self.prec.T)
+        sign, logdet = np.linalg.slogdet(self.sigma)
+        self.const = -0.5 * logdet - 0.5 * dim * LOG2PI
+
+    def __call__(self, x):
+        x = np.atleast_2d(x)
+        px = x @ self.prec
+        return -0.5 * np.sum(x * px, axis=1) + self.const, -px
