@@ -15,7 +15,11 @@
  *
  * Reference interfaces replaced (paths relative to the reference repo):
  *   vb_family_*            viabel/vb.py:42-82 (mean_field_gaussian_variational_family),
- *                          viabel/vb.py:140-182 (mean_field_t_variational_family)
+ *                          viabel/vb.py:140-182 (mean_field_t_variational_family),
+ *                          viabel/vb.py:192-233 (t_variational_family, full rank) with
+ *                          viabel/_distributions.py:8-38 (multivariate_t_logpdf)
+ *   vb_family_moments      viabel/vb.py:215-229 (full-rank mean_and_cov / pth_moment
+ *                          eigvalsh / entropy det)
  *   vb_objective_value_grad viabel/vb.py:236-245 (black_box_klvi),
  *                          viabel/vb.py:248-266 (black_box_chivi)
  *   vb_run_*               viabel/vb.py:324-389 (learning_rate_schedule, adagrad_optimize)
@@ -52,14 +56,18 @@ enum {
 /* ---- descriptors ----------------------------------------------------- */
 enum vb_family_kind {
   VB_FAMILY_MF_GAUSSIAN = 0, /* lambda = [mean(D), log_std(D)]       vb.py:48-82   */
-  VB_FAMILY_MF_T = 1         /* lambda = [mean(D), log_scale(D)], df  vb.py:140-182 */
+  VB_FAMILY_MF_T = 1,        /* lambda = [mean(D), log_scale(D)], df  vb.py:140-182 */
+  VB_FAMILY_FR_T = 2         /* lambda = [mu(D), tril(M) row-major (D(D+1)/2)], df;
+                                L = M with exp'd diagonal, Sigma = L L^T  vb.py:192-233 */
 };
 
 enum vb_target_kind {
   VB_TARGET_ISOGAUSS = 0,       /* N(0, I_D)                                  (separable) */
   VB_TARGET_MIXTURE = 1,        /* prod_d 0.5 N(-2,1) + 0.5 N(2,1)            (separable) */
   VB_TARGET_FUNNEL = 2,         /* Neal's funnel, x[1] = log sigma ~ N(0,1.35^2)           */
-  VB_TARGET_EIGHT_SCHOOLS_NCP = 3 /* eight_schools_ncp.stan log_prob, D = 10               */
+  VB_TARGET_EIGHT_SCHOOLS_NCP = 3, /* eight_schools_ncp.stan log_prob, D = 10              */
+  VB_TARGET_CORR_GAUSS = 4    /* N(0, Sigma*): params = [inv(Sigma*) (D x D row-major),
+                                 log normaliser]; full-rank family only (SURVEY §8d cfg 4) */
 };
 
 enum vb_objective_kind {
@@ -83,6 +91,8 @@ typedef struct vb_target {
   int32_t kind;   /* vb_target_kind */
   int32_t reserved;
   int64_t dim;    /* D (must equal the family's) */
+  const double* params; /* target parameters (host or device), NULL if none */
+  int64_t n_params;
 } vb_target;
 
 typedef struct vb_objective {
@@ -97,7 +107,9 @@ typedef struct vb_objective {
  * standard_t(df) for the t family.  PHILOX: `seed` keys the generator;
  * problem q of a call draws from stream `stream + q * stream_stride`
  * (24 bits; stride 0 means 1); `step` is the global step index of the first
- * step of the call. */
+ * step of the call.  Full-rank t family (VB_FAMILY_FR_T): each step's block of
+ * `eps` is [s (N), z (N x D)] with s = sqrt(chisquare(df)/df) and z ~ N(0, I),
+ * drawn in that order (vb.py:204-206). */
 typedef struct vb_noise {
   int32_t kind;      /* vb_noise_kind */
   uint32_t stream;
@@ -138,12 +150,18 @@ int vb_family_sample(vb_ctx* ctx, const vb_family* fam, const double* lam,
 /* out[n] = log q(x[n, :]; lambda) with all normalising constants. */
 int vb_family_logdensity(vb_ctx* ctx, const vb_family* fam, const double* lam,
                          const double* x, int64_t n, double* out);
+/* Full-rank family only: sigma_out [D][D] = Sigma = L L^T and eig_out [D] =
+ * its eigenvalues in ascending order (both nullable).  mean_and_cov is
+ * (mu, df/(df-2) Sigma), entropy .5 sum log eig, pth_moment from eig. */
+int vb_family_moments(vb_ctx* ctx, const vb_family* fam, const double* lam,
+                      double* sigma_out, double* eig_out);
 /* out[n] = log p(x[n, :]); grad_out (nullable) = d log p / dx, [n, D]. */
 int vb_target_logdensity(vb_ctx* ctx, const vb_target* tgt, const double* x,
                          int64_t n, double* out, double* grad_out);
 
 /* ---- estimators (vb.py:236-266) -------------------------------------- */
-/* One stochastic objective value and gradient at lambda (P = 2D values). */
+/* One stochastic objective value and gradient at lambda (P = 2D values for
+ * the mean-field families, D + D(D+1)/2 for the full-rank t family). */
 int vb_objective_value_grad(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,
                             const vb_objective* obj, const double* lam,
                             const vb_noise* noise, double* value, double* grad);

@@ -24,6 +24,9 @@ def _lib():
         lib.vbo_fill.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                  ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_double,
                                  ctypes.POINTER(ctypes.c_double)]
+        lib.vbo_fr_scale.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.c_int64, ctypes.c_double,
+                                     ctypes.POINTER(ctypes.c_double)]
         _LIB = lib
     return _LIB
 
@@ -43,3 +46,11 @@ def noise(seed, stream, step, n, dim, family='gauss', df=0.0):
                     1 if family == 't' else 0, float(df),
                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
     return out
+
+
+def fr_noise(seed, stream, step, n, dim, df):
+    """Full-rank t draws of one step: (s [n], z [n, dim]) (vb_fr.hip fr_noise_kernel)."""
+    s = np.empty(n)
+    _lib().vbo_fr_scale(seed, stream & 0xFFFFFF, step & 0xFFFFFFFF, n, float(df),
+                        s.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return s, noise(seed, stream, step, n, dim, 'gauss')

@@ -113,3 +113,14 @@ void vbo_fill(uint64_t seed, uint32_t stream, uint32_t step, int64_t nrows, int6
     }
   }
 }
+
+/* full-rank t scale draws s[n] = sqrt(chisquare(df)/df) = sqrt(2 Gamma(df/2)/df)
+ * from the reserved column pair 0xFFFFFFFF (vb_fr.hip fr_noise_kernel) */
+void vbo_fr_scale(uint64_t seed, uint32_t stream, uint32_t step, int64_t nrows, double df,
+                  double* s) {
+  for (int64_t r = 0; r < nrows; ++r) {
+    double ga, gb;
+    gamma2(seed, stream, 0xFFFFFFFFu, (uint32_t)r, step, df / 2.0, &ga, &gb);
+    s[r] = sqrt(2.0 * ga / df);
+  }
+}

@@ -13,8 +13,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libviabel_amd.so')
 
 VB_OK, VB_EINVAL, VB_EDEVICE, VB_ENOMEM, VB_EUNSUPPORTED = 0, -1, -2, -3, -4
-FAMILY_MF_GAUSSIAN, FAMILY_MF_T = 0, 1
+FAMILY_MF_GAUSSIAN, FAMILY_MF_T, FAMILY_FR_T = 0, 1, 2
 TARGET_ISOGAUSS, TARGET_MIXTURE, TARGET_FUNNEL, TARGET_EIGHT_SCHOOLS_NCP = 0, 1, 2, 3
+TARGET_CORR_GAUSS = 4
 OBJ_KLVI, OBJ_CHIVI = 0, 1
 NOISE_HOST, NOISE_PHILOX = 0, 1
 
@@ -28,7 +29,8 @@ class Family(ctypes.Structure):
 
 
 class Target(ctypes.Structure):
-    _fields_ = [('kind', ctypes.c_int32), ('reserved', ctypes.c_int32), ('dim', ctypes.c_int64)]
+    _fields_ = [('kind', ctypes.c_int32), ('reserved', ctypes.c_int32), ('dim', ctypes.c_int64),
+                ('params', c_double_p), ('n_params', ctypes.c_int64)]
 
 
 class Objective(ctypes.Structure):
@@ -60,6 +62,8 @@ _SIGNATURES = {
                           c_double_p], ctypes.c_int),
     'vb_family_logdensity': ([ctypes.c_void_p, P(Family), c_double_p, c_double_p,
                               ctypes.c_int64, c_double_p], ctypes.c_int),
+    'vb_family_moments': ([ctypes.c_void_p, P(Family), c_double_p, c_double_p, c_double_p],
+                          ctypes.c_int),
     'vb_target_logdensity': ([ctypes.c_void_p, P(Target), c_double_p, ctypes.c_int64,
                               c_double_p, c_double_p], ctypes.c_int),
     'vb_objective_value_grad': ([ctypes.c_void_p, P(Family), P(Target), P(Objective),

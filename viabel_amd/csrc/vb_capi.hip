@@ -81,12 +81,23 @@ struct DevBuf {
 
 }  // namespace
 
+int vbk::vb_set_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
 struct vb_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
-  DevBuf slot[12];
-  std::vector<void*> pending_frees;
+  DevBuf slot[16];
+  vbk::FrWork* fr = nullptr;  // full-rank workspace, created on first use
+  ~vb_ctx() { vbk::fr_work_destroy(fr); }
 };
 
 namespace {
@@ -156,18 +167,30 @@ int check_ctx(vb_ctx* c) {
 struct FamInfo {
   int kind;
   int D;
+  size_t P;  // length of lambda
   double df, t_scale, shape, t_const;
 };
 
 int check_family(const vb_family* f, FamInfo* o) {
   if (!f) return fail(VB_EINVAL, "null vb_family");
-  if (f->kind != VB_FAMILY_MF_GAUSSIAN && f->kind != VB_FAMILY_MF_T)
+  if (f->kind != VB_FAMILY_MF_GAUSSIAN && f->kind != VB_FAMILY_MF_T && f->kind != VB_FAMILY_FR_T)
     return fail(VB_EUNSUPPORTED, "family kind %d is not implemented on the device", f->kind);
   if (f->dim < 1 || f->dim > (1LL << 30)) return fail(VB_EINVAL, "invalid dimension %lld", (long long)f->dim);
   o->kind = f->kind;
   o->D = (int)f->dim;
+  o->P = 2 * (size_t)f->dim;
   o->df = f->df;
   o->t_scale = o->shape = o->t_const = 0.0;
+  if (f->kind == VB_FAMILY_FR_T) {
+    if (!(f->df > 2)) return fail(VB_EINVAL, "df must be greater than 2");  // vb.py:193-194
+    if (f->dim > 8192) return fail(VB_EUNSUPPORTED, "full-rank family needs D <= 8192");
+    const double D = (double)f->dim;
+    o->P = (size_t)f->dim + (size_t)f->dim * (f->dim + 1) / 2;
+    // multivariate_t_logpdf constant (_distributions.py:33-34)
+    o->t_const = std::lgamma(0.5 * (f->df + D)) - std::lgamma(0.5 * f->df) -
+                 0.5 * D * std::log(M_PI * f->df);
+    return VB_OK;
+  }
   if (f->kind == VB_FAMILY_MF_T) {
     if (!(f->df > 2)) return fail(VB_EINVAL, "df must be greater than 2");  // vb.py:141-142
     o->t_scale = std::sqrt(f->df / 2.0);
@@ -181,8 +204,11 @@ int check_family(const vb_family* f, FamInfo* o) {
 
 int check_target(const vb_target* t, int D) {
   if (!t) return fail(VB_EINVAL, "null vb_target");
-  if (t->kind < VB_TARGET_ISOGAUSS || t->kind > VB_TARGET_EIGHT_SCHOOLS_NCP)
+  if (t->kind < VB_TARGET_ISOGAUSS || t->kind > VB_TARGET_CORR_GAUSS)
     return fail(VB_EUNSUPPORTED, "target kind %d is not implemented on the device", t->kind);
+  if (t->kind == VB_TARGET_CORR_GAUSS &&
+      (!t->params || t->n_params != (int64_t)t->dim * t->dim + 1))
+    return fail(VB_EINVAL, "corr_gauss target needs D*D + 1 parameters (precision, log normaliser)");
   if (t->dim != D)
     return fail(VB_EINVAL, "target dimension %lld does not match family dimension %d",
                 (long long)t->dim, D);
@@ -196,6 +222,78 @@ int check_target(const vb_target* t, int D) {
 void key_of(uint64_t seed, uint32_t* k0, uint32_t* k1) {
   *k0 = (uint32_t)(seed & 0xffffffffu);
   *k1 = (uint32_t)(seed >> 32);
+}
+
+// Device copy of a target's parameters and its scalar log normaliser.
+int target_params(vb_ctx* c, int s, const vb_target* t, const double** dev, double* tconst) {
+  *dev = nullptr;
+  *tconst = 0.0;
+  if (t->kind != VB_TARGET_CORR_GAUSS) return VB_OK;
+  const size_t dd = (size_t)t->dim * t->dim;
+  In in;
+  VB_TRY(in.stage(c, s, t->params, dd + 1));
+  *dev = in.d;
+  VB_HIP(hipMemcpyAsync(tconst, in.d + dd, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  VB_HIP(hipStreamSynchronize(c->stream));
+  return VB_OK;
+}
+
+int fr_work(vb_ctx* c, vbk::FrWork** w) {
+  if (!c->fr) c->fr = vbk::fr_work_create();
+  if (!c->fr) return fail(VB_ENOMEM, "out of host memory");
+  *w = c->fr;
+  return VB_OK;
+}
+
+int require_fr(int fam_kind, int tgt_kind) {
+  if (tgt_kind == VB_TARGET_CORR_GAUSS && fam_kind != VB_FAMILY_FR_T)
+    return fail(VB_EUNSUPPORTED, "the corr_gauss target is implemented for the full-rank family only");
+  return VB_OK;
+}
+
+vbk::FrSpec fr_spec(const FamInfo& fi, const vb_target* tgt, const vb_objective* obj,
+                    const double* tparams, double tconst) {
+  vbk::FrSpec f{};
+  f.D = fi.D;
+  f.N = (int)obj->n_samples;
+  f.tgt = tgt->kind;
+  f.chivi = obj->kind == VB_OBJ_CHIVI;
+  f.df = fi.df;
+  f.t_const = fi.t_const;
+  f.alpha = obj->alpha;
+  f.tparams = tparams;
+  f.tconst = tconst;
+  return f;
+}
+
+// vb_objective_value_grad for the full-rank t family
+int fr_objective(vb_ctx* c, const FamInfo& fi, const vb_target* tgt, const vb_objective* obj,
+                 const double* lam, const vb_noise* noise, double* value, double* grad) {
+  const bool host = noise->kind == VB_NOISE_HOST;
+  if (host && !noise->eps) return fail(VB_EINVAL, "host noise requires eps");
+  const size_t N = (size_t)obj->n_samples;
+  In dl, dn;
+  Out dg;
+  VB_TRY(dl.stage(c, 0, lam, fi.P));
+  if (host) VB_TRY(dn.stage(c, 1, noise->eps, N * fi.D + N));
+  VB_TRY(dg.stage(c, 2, grad, fi.P));
+  const double* tp;
+  double tc;
+  VB_TRY(target_params(c, 3, tgt, &tp, &tc));
+  VB_TRY(c->slot[4].reserve(sizeof(double) * 2));
+  uint32_t k0, k1;
+  key_of(noise->seed, &k0, &k1);
+  vbk::FrWork* W;
+  VB_TRY(fr_work(c, &W));
+  VB_TRY(vbk::fr_value_grad(W, fr_spec(fi, tgt, obj, tp, tc), dl.d, host ? dn.d : nullptr, k0, k1,
+                            noise->stream, (uint32_t)noise->step, c->slot[4].d(), dg.d,
+                            c->stream));
+  VB_HIP(hipMemcpyAsync(value, c->slot[4].p, sizeof(double), hipMemcpyDefault, c->stream));
+  VB_TRY(dg.finish(c));
+  VB_TRY(sync(c));
+  if (int info = vbk::fr_info(W, c->stream))
+    return fail(VB_EDEVICE, "eigendecomposition of Sigma did not converge (info %d)", info);
+  return VB_OK;
 }
 
 vbk::LrSched make_sched(long long n, double lr, double lr_end) {
@@ -270,6 +368,27 @@ int vb_family_sample(vb_ctx* c, const vb_family* fam, const double* lam, int64_t
   VB_TRY(check_family(fam, &fi));
   if (!lam || !x_out || !noise || n < 0) return fail(VB_EINVAL, "null argument");
   const size_t nd = (size_t)n * fi.D;
+  if (fi.kind == VB_FAMILY_FR_T) {
+    const bool host = noise->kind == VB_NOISE_HOST;
+    if (host && !noise->eps) return fail(VB_EINVAL, "host noise requires eps");
+    if (n == 0) return VB_OK;
+    In dl, dn;
+    Out dx;
+    VB_TRY(dl.stage(c, 0, lam, fi.P));
+    if (host) VB_TRY(dn.stage(c, 1, noise->eps, nd + n));
+    VB_TRY(dx.stage(c, 2, x_out, nd));
+    uint32_t k0, k1;
+    key_of(noise->seed, &k0, &k1);
+    vbk::FrWork* W;
+    VB_TRY(fr_work(c, &W));
+    VB_TRY(vbk::fr_prepare(W, fi.D, dl.d, true, c->stream));
+    const double *s, *z;
+    VB_TRY(vbk::fr_draw(W, fi.D, n, fi.df, host ? dn.d : nullptr, k0, k1, noise->stream,
+                        (uint32_t)noise->step, &s, &z, c->stream));
+    VB_TRY(vbk::fr_transform(W, fi.D, n, dl.d, s, z, dx.d, c->stream));
+    VB_TRY(dx.finish(c));
+    return sync(c);
+  }
   In dl, dn;
   Out dx;
   VB_TRY(dl.stage(c, 0, lam, 2 * (size_t)fi.D));
@@ -295,6 +414,17 @@ int vb_family_logdensity(vb_ctx* c, const vb_family* fam, const double* lam, con
   if (!lam || !x || !out || n < 0) return fail(VB_EINVAL, "null argument");
   In dl, dxx;
   Out dout;
+  if (fi.kind == VB_FAMILY_FR_T) {
+    if (n == 0) return VB_OK;
+    VB_TRY(dl.stage(c, 0, lam, fi.P));
+    VB_TRY(dxx.stage(c, 1, x, (size_t)n * fi.D));
+    VB_TRY(dout.stage(c, 2, out, (size_t)n));
+    vbk::FrWork* W;
+    VB_TRY(fr_work(c, &W));
+    VB_TRY(vbk::fr_logdensity(W, fi.D, fi.df, fi.t_const, dl.d, dxx.d, n, dout.d, c->stream));
+    VB_TRY(dout.finish(c));
+    return sync(c);
+  }
   VB_TRY(dl.stage(c, 0, lam, 2 * (size_t)fi.D));
   VB_TRY(dxx.stage(c, 1, x, (size_t)n * fi.D));
   VB_TRY(dout.stage(c, 2, out, (size_t)n));
@@ -302,6 +432,33 @@ int vb_family_logdensity(vb_ctx* c, const vb_family* fam, const double* lam, con
                                        c->stream));
   VB_TRY(dout.finish(c));
   return sync(c);
+}
+
+int vb_family_moments(vb_ctx* c, const vb_family* fam, const double* lam, double* sigma_out,
+                      double* eig_out) {
+  VB_TRY(check_ctx(c));
+  FamInfo fi;
+  VB_TRY(check_family(fam, &fi));
+  if (!lam) return fail(VB_EINVAL, "null argument");
+  if (fi.kind != VB_FAMILY_FR_T)
+    return fail(VB_EUNSUPPORTED, "vb_family_moments is for the full-rank family");
+  const size_t dd = (size_t)fi.D * fi.D;
+  In dl;
+  Out ds, de;
+  VB_TRY(dl.stage(c, 0, lam, fi.P));
+  VB_TRY(ds.stage(c, 1, sigma_out, sigma_out ? dd : 0));
+  VB_TRY(de.stage(c, 2, eig_out, eig_out ? (size_t)fi.D : 0));
+  vbk::FrWork* W;
+  VB_TRY(fr_work(c, &W));
+  VB_TRY(vbk::fr_moments(W, fi.D, dl.d, ds.d, de.d, c->stream));
+  VB_TRY(ds.finish(c));
+  VB_TRY(de.finish(c));
+  VB_TRY(sync(c));
+  if (eig_out) {
+    if (int info = vbk::fr_info(W, c->stream))
+      return fail(VB_EDEVICE, "eigendecomposition of Sigma did not converge (info %d)", info);
+  }
+  return VB_OK;
 }
 
 int vb_target_logdensity(vb_ctx* c, const vb_target* tgt, const double* x, int64_t n,
@@ -316,7 +473,17 @@ int vb_target_logdensity(vb_ctx* c, const vb_target* tgt, const double* x, int64
   VB_TRY(dxx.stage(c, 0, x, (size_t)n * D));
   VB_TRY(dout.stage(c, 1, out, (size_t)n));
   VB_TRY(dg.stage(c, 2, grad_out, grad_out ? (size_t)n * D : 0));
-  VB_HIP(vbk::launch_target_logdensity(tgt->kind, D, n, dxx.d, dout.d, dg.d, c->stream));
+  if (tgt->kind == VB_TARGET_CORR_GAUSS) {
+    if (n == 0) return VB_OK;
+    const double* tp;
+    double tc;
+    VB_TRY(target_params(c, 3, tgt, &tp, &tc));
+    vbk::FrWork* W;
+    VB_TRY(fr_work(c, &W));
+    VB_TRY(vbk::fr_target(W, tgt->kind, D, n, tp, tc, dxx.d, dout.d, dg.d, c->stream));
+  } else {
+    VB_HIP(vbk::launch_target_logdensity(tgt->kind, D, n, dxx.d, dout.d, dg.d, c->stream));
+  }
   VB_TRY(dout.finish(c));
   VB_TRY(dg.finish(c));
   return sync(c);
@@ -335,6 +502,8 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
     return fail(VB_EINVAL, "n_samples must be positive");
   if (obj->kind == VB_OBJ_CHIVI && !(obj->alpha > 0))
     return fail(VB_EINVAL, "alpha must be positive");
+  VB_TRY(require_fr(fi.kind, tgt->kind));
+  if (fi.kind == VB_FAMILY_FR_T) return fr_objective(c, fi, tgt, obj, lam, noise, value, grad);
   const int D = fi.D, N = (int)obj->n_samples;
   const size_t P = 2 * (size_t)D;
   const bool host = noise->kind == VB_NOISE_HOST;
@@ -435,6 +604,10 @@ struct vb_run {
   int n_waves = 0;
   int max_chunk = 256;
   DevBuf lam, ring, hist, values, vpart, noise, smooth;
+  // full-rank family: one fr_value_grad + adagrad update per step
+  bool fr = false;
+  vbk::FrSpec spec{};
+  DevBuf tparams, grad;
 };
 
 extern "C" {
@@ -448,6 +621,7 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
   FamInfo fi;
   VB_TRY(check_family(fam, &fi));
   VB_TRY(check_target(tgt, fi.D));
+  VB_TRY(require_fr(fi.kind, tgt->kind));
   if (!obj || !cfg || !init) return fail(VB_EINVAL, "null argument");
   if (!(cfg->learning_rate > 0)) return fail(VB_EINVAL, "learning rate must be positive");
   if (!std::isnan(cfg->learning_rate_end) && cfg->learning_rate <= cfg->learning_rate_end)
@@ -458,9 +632,10 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
   if (obj->n_samples < 1 || obj->n_samples > (1LL << 31))
     return fail(VB_EINVAL, "n_samples must be positive");
   const int D = fi.D;
-  const bool sep = vbk::target_separable(tgt->kind) && obj->kind == VB_OBJ_KLVI &&
+  const bool fr = fi.kind == VB_FAMILY_FR_T;
+  const bool sep = !fr && vbk::target_separable(tgt->kind) && obj->kind == VB_OBJ_KLVI &&
                    (D > vbk::kBlockDMax);
-  if (!sep && D > vbk::kBlockDMax)
+  if (!fr && !sep && D > vbk::kBlockDMax)
     return fail(VB_EUNSUPPORTED,
                 "device adagrad for objective %d / target %d needs D <= %d (got %d)", obj->kind,
                 tgt->kind, vbk::kBlockDMax, D);
@@ -484,12 +659,27 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
   r->sched = make_sched(cfg->n_iters, cfg->learning_rate, cfg->learning_rate_end);
   r->sep = sep;
   r->n_waves = (D + 1) / 2;
-  const size_t P = 2 * (size_t)D;
+  const size_t P = fi.P;
   auto bail = [&](int rc) {
     delete r;
     return rc;
   };
   int rc;
+  if (fr) {
+    r->fr = true;
+    const double* tp;
+    double tc;
+    if ((rc = target_params(c, 1, tgt, &tp, &tc)) != VB_OK) return bail(rc);
+    if (tp) {
+      const size_t np = (size_t)tgt->n_params;
+      if ((rc = r->tparams.reserve(sizeof(double) * np)) != VB_OK) return bail(rc);
+      hipError_t e = hipMemcpyAsync(r->tparams.p, tp, sizeof(double) * np, hipMemcpyDeviceToDevice,
+                                    c->stream);
+      if (e != hipSuccess) return bail(fail(VB_EDEVICE, "hipMemcpy failed: %s", hipGetErrorString(e)));
+    }
+    r->spec = fr_spec(fi, tgt, obj, r->tparams.d(), tc);
+    if ((rc = r->grad.reserve(sizeof(double) * P)) != VB_OK) return bail(rc);
+  }
   if ((rc = r->lam.reserve(sizeof(double) * P * n_problems)) != VB_OK) return bail(rc);
   if ((rc = r->ring.reserve(sizeof(double) * P * r->W * n_problems)) != VB_OK) return bail(rc);
   if ((rc = r->hist.reserve(sizeof(double) * P * std::max<long long>(r->n_hist, 1) * n_problems)) != VB_OK)
@@ -521,8 +711,8 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
   if (n_steps == 0) return VB_OK;
   const bool host = noise->kind == VB_NOISE_HOST;
   const int D = r->fi.D, N = r->N;
-  const size_t P = 2 * (size_t)D;
-  const size_t per_step = (size_t)N * D;
+  const size_t P = r->fi.P;
+  const size_t per_step = (size_t)N * D + (r->fr ? (size_t)N : 0);
   if (host) {
     if (!noise->eps) return fail(VB_EINVAL, "host noise requires eps");
     const size_t tot = per_step * n_steps * r->nprob;
@@ -539,7 +729,30 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
   uint32_t k0, k1;
   key_of(noise->seed, &k0, &k1);
 
-  if (r->sep) {
+  if (r->fr) {
+    vbk::FrWork* W;
+    VB_TRY(fr_work(c, &W));
+    const uint32_t stride = noise->stream_stride ? noise->stream_stride : 1;
+    for (long long off = 0; off < n_steps; ++off) {
+      const long long step = r->done + off;
+      const double lr = r->sched.at(step);
+      for (long long q = 0; q < r->nprob; ++q) {
+        double* lam = r->lam.d() + q * P;
+        const double* eps =
+            host ? noise_base + ((size_t)q * n_steps + off) * per_step : nullptr;
+        VB_TRY(vbk::fr_value_grad(W, r->spec, lam, eps, k0, k1,
+                                  noise->stream + (uint32_t)q * stride,
+                                  (uint32_t)(noise->step + off),
+                                  r->values.d() + q * r->n_iters + step, r->grad.d(), c->stream));
+        VB_HIP(vbk::launch_adagrad_update((long long)P, lam, r->grad.d(),
+                                          r->ring.d() + q * P * r->W, r->W, step, lr, r->eps,
+                                          c->stream));
+        if (step >= r->hist_start)
+          VB_HIP(hipMemcpyAsync(r->hist.d() + (q * r->n_hist + (step - r->hist_start)) * P, lam,
+                                sizeof(double) * P, hipMemcpyDeviceToDevice, c->stream));
+      }
+    }
+  } else if (r->sep) {
     long long off = 0;
     while (off < n_steps) {
       const int cs = (int)std::min<long long>(r->max_chunk, n_steps - off);
@@ -606,6 +819,14 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
     VB_HIP(vbk::launch_block(r->fi.kind, r->tgt, host, a, (int)r->nprob, c->stream));
   }
   r->done += n_steps;
+  if (r->fr) {
+    VB_TRY(sync(c));
+    vbk::FrWork* W;
+    VB_TRY(fr_work(c, &W));
+    if (int info = vbk::fr_info(W, c->stream))
+      return fail(VB_EDEVICE, "eigendecomposition of Sigma did not converge (info %d)", info);
+    return VB_OK;
+  }
   // host noise staging buffer is reused by the next call: finish before returning
   if (host) return sync(c);
   return VB_OK;
@@ -622,7 +843,7 @@ int vb_run_result(vb_run* r, double* lam_out, double* hist_out, double* values_o
   if (!r) return fail(VB_EINVAL, "null vb_run");
   vb_ctx* c = r->ctx;
   VB_TRY(check_ctx(c));
-  const size_t P = 2 * (size_t)r->fi.D;
+  const size_t P = r->fi.P;
   auto copy_out = [&](double* dst, const void* src, size_t n) -> int {
     if (!dst || n == 0) return VB_OK;
     VB_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDefault, c->stream));
@@ -678,6 +899,37 @@ int vb_log_weights(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const 
   VB_TRY(check_family(fam, &fi));
   VB_TRY(check_target(tgt, fi.D));
   if (!lam || !noise || !lw_out || m < 0) return fail(VB_EINVAL, "null argument");
+  VB_TRY(require_fr(fi.kind, tgt->kind));
+  if (fi.kind == VB_FAMILY_FR_T) {
+    const bool host = noise->kind == VB_NOISE_HOST;
+    if (host && !noise->eps) return fail(VB_EINVAL, "host noise requires eps");
+    if (m == 0) return VB_OK;
+    In dl, dn;
+    Out dlw, dxs;
+    VB_TRY(dl.stage(c, 0, lam, fi.P));
+    if (host) VB_TRY(dn.stage(c, 1, noise->eps, (size_t)m * fi.D + m));
+    VB_TRY(dlw.stage(c, 2, lw_out, (size_t)m));
+    VB_TRY(dxs.stage(c, 3, samples_out, samples_out ? (size_t)m * fi.D : 0));
+    const double* tp;
+    double tc;
+    VB_TRY(target_params(c, 4, tgt, &tp, &tc));
+    vbk::FrSpec f{};
+    f.D = fi.D;
+    f.tgt = tgt->kind;
+    f.df = fi.df;
+    f.t_const = fi.t_const;
+    f.tparams = tp;
+    f.tconst = tc;
+    uint32_t k0, k1;
+    key_of(noise->seed, &k0, &k1);
+    vbk::FrWork* W;
+    VB_TRY(fr_work(c, &W));
+    VB_TRY(vbk::fr_log_weights(W, f, dl.d, m, host ? dn.d : nullptr, k0, k1, noise->stream,
+                               (uint32_t)noise->step, dlw.d, dxs.d, c->stream));
+    VB_TRY(dlw.finish(c));
+    VB_TRY(dxs.finish(c));
+    return sync(c);
+  }
   if (!vbk::target_separable(tgt->kind) && fi.D > vbk::kBlockDMax)
     return fail(VB_EUNSUPPORTED, "log weights for target %d need D <= %d", tgt->kind, vbk::kBlockDMax);
   const bool host = noise->kind == VB_NOISE_HOST;

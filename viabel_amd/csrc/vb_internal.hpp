@@ -109,3 +109,65 @@ hipError_t psis_gpinv(const double* p, long long n, double k, double sigma, doub
 hipError_t psis_sumlogs(const double* x, long long n, void* scratch, double* out, hipStream_t s);
 
 }  // namespace vbk
+
+// ---- full-rank Student-t family (vb_fr.hip) ----------------------------------
+namespace vbk {
+
+int vb_set_error(int code, const char* fmt, ...);  // defined in vb_capi.hip
+
+constexpr int kFamilyFrT = 2;
+constexpr int kTargetCorrGauss = 4;
+
+// C[M][N] = alpha * op(A) diag(kscale) op(B) [/ row_div[i]] [+ col_bias[j]] + beta C,
+// row-major with leading dimensions; fp64 MFMA.
+struct GemmOp {
+  bool ta, tb;
+  int M, N, K;
+  const double* A;
+  long long lda;
+  const double* B;
+  long long ldb;
+  double* C;
+  long long ldc;
+  double alpha, beta;
+  const double* kscale;    // [K] or null
+  const double* row_div;   // [M] or null
+  const double* col_bias;  // [N] or null
+};
+hipError_t gemm(const GemmOp& g, hipStream_t s);
+
+struct FrWork;  // per-context workspace + rocBLAS handle
+FrWork* fr_work_create();
+void fr_work_destroy(FrWork* w);
+
+struct FrSpec {
+  int D, N, tgt, chivi;
+  double df, t_const, alpha;
+  const double* tparams;  // device; corr_gauss: P*[D][D]
+  double tconst;          // corr_gauss log normaliser
+};
+
+// All return 0 or a VB_E* code (message via vb_set_error).
+int fr_prepare(FrWork* W, int D, const double* lam, bool need_sqrt, hipStream_t st);
+int fr_draw(FrWork* W, int D, long long n, double df, const double* host_eps, uint32_t k0,
+            uint32_t k1, uint32_t stream, uint32_t step, const double** s_out,
+            const double** z_out, hipStream_t st);
+int fr_transform(FrWork* W, int D, long long n, const double* mu, const double* s,
+                 const double* z, double* x, hipStream_t st);
+int fr_target(FrWork* W, int tgt, int D, long long n, const double* tparams, double tconst,
+              const double* x, double* logp, double* G, hipStream_t st);
+int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* host_eps,
+                  uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
+                  double* grad, hipStream_t st);
+int fr_logdensity(FrWork* W, int D, double df, double t_const, const double* lam, const double* x,
+                  long long n, double* out, hipStream_t st);
+int fr_log_weights(FrWork* W, const FrSpec& f, const double* lam, long long m,
+                   const double* host_eps, uint32_t k0, uint32_t k1, uint32_t stream,
+                   uint32_t step, double* lw, double* xs, hipStream_t st);
+int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, hipStream_t st);
+int fr_info(FrWork* W, hipStream_t st);
+hipError_t launch_fr_lw(int D, long long m, double df, double t_const, const double* logp,
+                        const double* zz, const double* s, const double* scal, double* lw,
+                        hipStream_t st);
+
+}  // namespace vbk

@@ -5,6 +5,7 @@ error messages) for the hot path:
 
   mean_field_gaussian_variational_family  vb.py:48-82
   mean_field_t_variational_family         vb.py:140-182
+  t_variational_family (full rank)        vb.py:185-233, _distributions.py:8-38
   black_box_klvi                          vb.py:236-245
   black_box_chivi                         vb.py:248-266
   learning_rate_schedule                  vb.py:324-342
@@ -37,6 +38,7 @@ from .targets import Target
 __all__ = [
     'mean_field_gaussian_variational_family',
     'mean_field_t_variational_family',
+    't_variational_family',
     'black_box_klvi',
     'black_box_chivi',
     'learning_rate_schedule',
@@ -71,6 +73,10 @@ class NativeVariationalFamily(VariationalFamily):
         rs = self.rs if seed is None else np.random.RandomState(seed)
         if self.kind == nat.FAMILY_MF_GAUSSIAN:
             return rs.randn(n, self.dim)
+        if self.kind == nat.FAMILY_FR_T:
+            # vb.py:204-206: chisquare first, then randn; flat [s (n), z (n x D)]
+            s = np.sqrt(rs.chisquare(self.df, n) / self.df)
+            return np.concatenate([s, rs.randn(n, self.dim).ravel()])
         return rs.standard_t(self.df, size=(n, self.dim))
 
     def _philox_noise(self, seed=None, steps=1):
@@ -162,6 +168,86 @@ def _make_family(kind, dim, df, rng):
     return fam
 
 
+def t_variational_family(dim, df, rng=None):
+    """vb.py:192-233.  var_param = [mu (dim), tril(M) (dim (dim + 1) / 2)] in
+    paragami's free layout: row-major lower triangle, log diagonal,
+    Sigma = L L^T.  Every method runs on the device (sqrtm / eigh through the
+    eigendecomposition of Sigma)."""
+    if df <= 2:
+        raise ValueError('df must be greater than 2')
+    rng = _DEFAULT_RNG[0] if rng is None else rng
+    if rng not in ('numpy', 'philox'):
+        raise ValueError("rng must be 'numpy' or 'philox'")
+    dim = int(dim)
+    df = float(df)
+    P = dim + dim * (dim + 1) // 2
+
+    def _lam(var_param):
+        lam = nat.as_f64(var_param)
+        if lam.shape != (P,):
+            raise ValueError('var_param must have shape (%d,)' % P)
+        return lam
+
+    def sample(var_param, n_samples, seed=None):
+        lam = _lam(var_param)
+        out = np.empty((int(n_samples), dim))
+        if fam.rng == 'numpy':
+            eps = nat.as_f64(fam._draw(int(n_samples), seed))
+            nz = nat.Noise(nat.NOISE_HOST, 0, 0, 0, nat.dptr(eps))
+        else:
+            nz = fam._philox_noise(seed)
+        nat.check(nat.lib().vb_family_sample(nat.context().handle, fam._struct(), nat.dptr(lam),
+                                             int(n_samples), nz, nat.dptr(out)))
+        return out
+
+    def logdensity(x, var_param):
+        lam = _lam(var_param)
+        xx = np.asarray(x, dtype=float)
+        one_d = xx.ndim == 1
+        xx = nat.as_f64(np.atleast_2d(xx))
+        out = np.empty(xx.shape[0])
+        nat.check(nat.lib().vb_family_logdensity(nat.context().handle, fam._struct(),
+                                                 nat.dptr(lam), nat.dptr(xx), xx.shape[0],
+                                                 nat.dptr(out)))
+        return out[0] if one_d else out
+
+    def _moments(var_param, sigma=False):
+        lam = _lam(var_param)
+        eig = np.empty(dim)
+        sig = np.empty((dim, dim)) if sigma else None
+        nat.check(nat.lib().vb_family_moments(nat.context().handle, fam._struct(), nat.dptr(lam),
+                                              nat.dptr(sig) if sigma else None, nat.dptr(eig)))
+        return eig, sig
+
+    def entropy(var_param):
+        # .5 log det Sigma (vb.py:210-213), from the device eigenvalues
+        return .5 * np.sum(np.log(_moments(var_param)[0]))
+
+    def mean_and_cov(var_param):
+        lam = _lam(var_param)
+        sig = np.empty((dim, dim))
+        nat.check(nat.lib().vb_family_moments(nat.context().handle, fam._struct(), nat.dptr(lam),
+                                              nat.dptr(sig), None))
+        return lam[:dim].copy(), df / (df - 2.) * sig                      # vb.py:215-217
+
+    def pth_moment(p, var_param):
+        if p not in [2, 4]:
+            raise ValueError('only p = 2 or 4 supported')
+        if df <= p:
+            raise ValueError('df must be greater than p')
+        sq_scales = _moments(var_param)[0]                                  # vb.py:225
+        c = df / (df - 2)
+        if p == 2:
+            return c * np.sum(sq_scales)
+        return c ** 2 * (2 * (df - 1) / (df - 4) * np.sum(sq_scales ** 2) + np.sum(sq_scales) ** 2)
+
+    fam = NativeVariationalFamily(sample, entropy, logdensity, mean_and_cov, pth_moment, P)
+    fam.kind, fam.dim, fam.df, fam.rng = nat.FAMILY_FR_T, dim, df, rng
+    fam.rs = np.random.RandomState(0)      # vb.py:195
+    fam.seed, fam.stream, fam.step = 0, next(_STREAMS) & 0xFFFFFF, 0
+    return fam
+
+
 def mean_field_gaussian_variational_family(dim, rng=None):
     """vb.py:48-82.  var_param = [mean (dim), log_std (dim)]."""
     return _make_family(nat.FAMILY_MF_GAUSSIAN, dim, None, rng)
@@ -205,8 +291,8 @@ class NativeObjective:
 
     def __call__(self, var_param):
         lam = nat.as_f64(var_param)
-        if lam.shape != (2 * self.family.dim,):
-            raise ValueError('var_param must have shape (%d,)' % (2 * self.family.dim))
+        if lam.shape != (self.family.var_param_dim,):
+            raise ValueError('var_param must have shape (%d,)' % self.family.var_param_dim)
         fam = self.family
         if fam.rng == 'numpy':
             eps = nat.as_f64(self._eps_one_call())
@@ -323,7 +409,7 @@ def _native_adagrad(n_iters, obj, init_param, window, learning_rate, epsilon,
         run.advance_philox(n_iters, fam.seed, fam.stream, fam.step)
         fam.step += n_iters
     else:
-        per_step = obj.n_samples * fam.dim
+        per_step = obj.n_samples * (fam.dim + 1)
         chunk = max(1, min(n_iters, _HOST_CHUNK_ELEMS // max(per_step, 1)))
         done = 0
         while done < n_iters:
