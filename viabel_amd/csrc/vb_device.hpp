@@ -260,6 +260,30 @@ __device__ __forceinline__ double stride4_sum(double k) {
   return k;
 }
 
+__device__ __forceinline__ double swap_max16(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return fmax(__hiloint2double((int)b[0], (int)a[0]), __hiloint2double((int)b[1], (int)a[1]));
+}
+
+__device__ __forceinline__ double swap_max32(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return fmax(__hiloint2double((int)b[0], (int)a[0]), __hiloint2double((int)b[1], (int)a[1]));
+}
+
+// Wave-wide max with DPP + permlane swaps (every lane receives the maximum).
+__device__ __forceinline__ double wave_max_dpp(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));
+  v = fmax(v, dpp_f64<0x4E>(v));
+  v = fmax(v, dpp_f64<0x141>(v));
+  v = fmax(v, dpp_f64<0x140>(v));
+  v = swap_max16(v);
+  return swap_max32(v);
+}
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));

@@ -286,7 +286,7 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double (*red)[K + 1], 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const double t = wave_sum(v[k]);
+    const double t = wave_sum_dpp(v[k]);
     if (lane == 0) red[wid][k] = t;
   }
   __syncthreads();
@@ -309,15 +309,16 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
 
   using Row = RowOf<TGT>;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int NT = blockDim.x, NW = NT >> 6;  // 64..256 threads (sized to N by the launcher)
   const int prob = blockIdx.x;
   const int D = a.D, N = a.N, W = a.W, P = a.P;
   const double dN = (double)N;
   double* lam_g = a.lam + (long long)prob * P;
   double* ring_g = a.ring ? a.ring + (long long)prob * W * P : nullptr;
 
-  for (int p = tid; p < P; p += 256) s_lam[p] = lam_g[p];
+  for (int p = tid; p < P; p += NT) s_lam[p] = lam_g[p];
   if (!a.emit_grad)
-    for (int q = tid; q < W * P; q += 256) s_ring[q] = ring_g[q];
+    for (int q = tid; q < W * P; q += NT) s_ring[q] = ring_g[q];
   __syncthreads();
 
   const Rng rng{a.k0, a.k1, (uint32_t)(a.stream + (uint32_t)prob * a.stream_stride)};
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
     double mloc = -INFINITY;  // CHIVI: running max of this thread's log weights
 
-    for (int n = tid; n < N; n += 256) {
+    for (int n = tid; n < N; n += NT) {
       double e[DMAX], x[DMAX], g[DMAX];
       if constexpr (HOST) {
         const double* row = a.noise + (((long long)prob * a.n_steps + s) * N + n) * D;
@@ -407,15 +408,16 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
 
     double M = 0.0;
     if (a.chivi) {
-      const double wm = wave_max(mloc);
+      const double wm = wave_max_dpp(mloc);
       if (lane == 0) s_max[wid] = wm;
       __syncthreads();
-      M = fmax(fmax(s_max[0], s_max[1]), fmax(s_max[2], s_max[3]));
+      M = s_max[0];
+      for (int q = 1; q < NW; ++q) M = fmax(M, s_max[q]);
       const double f = (mloc == -INFINITY) ? 0.0 : exp(a.alpha * (mloc - M));
 #pragma unroll
       for (int k = 0; k <= 2 * DMAX; ++k) acc[k] *= f;
     }
-    block_sum<K>(acc, s_red, 4);
+    block_sum<K>(acc, s_red, NW);
 
     // gradient + adagrad update: thread p owns parameter p
     if (tid < P) {
@@ -464,8 +466,8 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
   }
 
   if (!a.emit_grad) {
-    for (int p = tid; p < P; p += 256) lam_g[p] = s_lam[p];
-    for (int q = tid; q < W * P; q += 256) ring_g[q] = s_ring[q];
+    for (int p = tid; p < P; p += NT) lam_g[p] = s_lam[p];
+    for (int q = tid; q < W * P; q += NT) ring_g[q] = s_ring[q];
   }
 }
 
@@ -740,12 +742,16 @@ hipError_t launch_sep(int fam, int tgt, bool host, const SepArgs& a, hipStream_t
   }
 }
 
-template <class TGT>
-static hipError_t block_dispatch(int fam, bool host, const BlockArgs& a, int nprob,
-                                 hipStream_t s) {
-  constexpr int DM = kBlockDMax;
-  const dim3 grid(nprob), block(256);
-  if (host) {
+// Threads per problem: the draws of one step spread over ceil(N/64) waves (<= 4).
+inline unsigned block_threads(int N) { return 64u * (unsigned)std::min(4, std::max(1, (N + 63) / 64)); }
+
+template <class TGT, int DM>
+static hipError_t block_dispatch_dm(int fam, bool host, const BlockArgs& a, int nprob,
+                                    hipStream_t s) {
+  const dim3 grid(nprob), block(block_threads(a.N));
+  if (host && fam == 1) {
+    hipLaunchKernelGGL((block_kernel<TGT, true, true, DM>), grid, block, 0, s, a);
+  } else if (host) {
     hipLaunchKernelGGL((block_kernel<TGT, false, true, DM>), grid, block, 0, s, a);
   } else if (fam == 1) {
     hipLaunchKernelGGL((block_kernel<TGT, true, false, DM>), grid, block, 0, s, a);
@@ -753,6 +759,20 @@ static hipError_t block_dispatch(int fam, bool host, const BlockArgs& a, int npr
     hipLaunchKernelGGL((block_kernel<TGT, false, false, DM>), grid, block, 0, s, a);
   }
   return hipGetLastError();
+}
+
+// Register arrays are sized by DMAX: pick the smallest instantiation >= D.
+template <class TGT>
+static hipError_t block_dispatch(int fam, bool host, const BlockArgs& a, int nprob,
+                                 hipStream_t s) {
+  if constexpr (std::is_same_v<TGT, EightSchools>) {
+    return block_dispatch_dm<TGT, 10>(fam, host, a, nprob, s);
+  } else {
+    if (a.D <= 2) return block_dispatch_dm<TGT, 2>(fam, host, a, nprob, s);
+    if (a.D <= 4) return block_dispatch_dm<TGT, 4>(fam, host, a, nprob, s);
+    if (a.D <= 10) return block_dispatch_dm<TGT, 10>(fam, host, a, nprob, s);
+    return block_dispatch_dm<TGT, kBlockDMax>(fam, host, a, nprob, s);
+  }
 }
 
 // In host-noise mode the t family's CHIVI log q still needs df: the kernel reads
@@ -763,13 +783,7 @@ static hipError_t block_dispatch(int fam, bool host, const BlockArgs& a, int npr
 template <class TGT>
 static hipError_t block_dispatch_full(int fam, bool host, const BlockArgs& a, int nprob,
                                       hipStream_t s) {
-  constexpr int DM = kBlockDMax;
-  const dim3 grid(nprob), block(256);
-  if (host && fam == 1)
-    hipLaunchKernelGGL((block_kernel<TGT, true, true, DM>), grid, block, 0, s, a);
-  else
-    return block_dispatch<TGT>(fam, host, a, nprob, s);
-  return hipGetLastError();
+  return block_dispatch<TGT>(fam, host, a, nprob, s);
 }
 
 hipError_t launch_block(int fam, int tgt, bool host, const BlockArgs& a, int nprob,
