@@ -381,7 +381,7 @@ int vb_family_sample(vb_ctx* c, const vb_family* fam, const double* lam, int64_t
     key_of(noise->seed, &k0, &k1);
     vbk::FrWork* W;
     VB_TRY(fr_work(c, &W));
-    VB_TRY(vbk::fr_prepare(W, fi.D, dl.d, true, c->stream));
+    VB_TRY(vbk::fr_sqrt(W, fi.D, dl.d, c->stream));
     const double *s, *z;
     VB_TRY(vbk::fr_draw(W, fi.D, n, fi.df, host ? dn.d : nullptr, k0, k1, noise->stream,
                         (uint32_t)noise->step, &s, &z, c->stream));

@@ -6,21 +6,23 @@
 // lambda = [mu (D), tril(M) row-major (D(D+1)/2)], L = M with exp'd diagonal,
 // Sigma = L L^T (paragami PSDSymmetricMatrixPattern).
 //
-// One step (D x D products on fp64 MFMA, v_mfma_f64_16x16x4_f64):
-//   L <- unpack(lambda);  E <- L L^T;  (V, w) <- eigh(E)  [rocSOLVER dsyevd]
-//   S = V diag(sqrt w) V^T                       (= sqrtm(Sigma), vb.py:207)
+// One step, GEMMs only (fp64 MFMA, vb_gemm.hpp), no eigendecomposition:
+//   L <- unpack(lambda);  Sigma <- L L^T;  0.5 log det Sigma = sum log L_ii
+//   S = sqrtm(Sigma) by coupled Newton-Schulz on Sigma / ||Sigma||_F (fr_sqrt)
 //   X = mu + (Z S) / s                           (vb.py:208, fused epilogue)
 //   G = d log p / dx, log p                      (corr_gauss: G = -X P*, GEMM)
 //   KLVI : r_n = -1/N,            c = -1/2       (entropy .5 log det Sigma)
 //   CHIVI: r_n = alpha w_n / N,   c = +1/2 sum r (log q's -.5 log det Sigma; the
 //          Mahalanobis term is invariant under the reparameterisation)
 //   G_S = Z^T diag(r / s) G                       (cotangent of S)
-//   autograd's sqrtm VJP solves S X + X S = G_S; in the eigenbasis
-//   M = V^T G_S V, X = V [M_ij / (sqrt w_i + sqrt w_j)] V^T, and the Sigma
-//   cotangent is X + c Sigma^-1.  Sigma = L L^T gives (G + G^T) L, so only the
-//   symmetric part is needed: Msym = (M + M^T) / (sqrt w_i + sqrt w_j) + 2c/w_i
-//   on the diagonal;  H = V Msym V^T;  G_L = H L;  grad = [sum r G, tril(G_L)
-//   with the diagonal times L_ii].
+//   autograd's sqrtm VJP solves S X + X S = G_S (solve_sylvester); Sigma = L L^T
+//   only needs the symmetric part, so X_sym solves S X + X S = G_S + G_S^T,
+//   computed as the forward-mode tangent of the same Newton-Schulz iteration
+//   (fr_sylvester).  H = X_sym + 2 c Sigma^-1 (Sigma^-1 = Z_K^2 / ||Sigma||_F);
+//   G_L = H L;  grad = [sum r G, tril(G_L) with the diagonal times L_ii].
+// The eigendecomposition (rocSOLVER dsyevd) remains only for log q of arbitrary
+// points (multivariate_t_logpdf's pinv cutoff) and the eigenvalues of
+// mean_and_cov / pth_moment, off the optimisation loop.
 #include "vb_device.hpp"
 #include "vb_internal.hpp"
 
@@ -33,82 +35,6 @@
 
 namespace vbk {
 using namespace vbd;
-
-using d4 = double __attribute__((ext_vector_type(4)));
-
-// ---- fp64 MFMA GEMM ---------------------------------------------------------
-// Block tile 32x32 (4 waves, one 16x16 MFMA tile each), K staged 16 at a time
-// through LDS.  v_mfma_f64_16x16x4_f64 operand maps (cdna_hip_programming.md):
-// A[l&15][k=l>>4], B[k=l>>4][l&15]; C row = (l>>4) + 4 r, col = l&15.
-constexpr int kGT = 32;
-constexpr int kGK = 16;
-
-template <bool TA, bool TB, bool KS>
-__global__ __launch_bounds__(256) void gemm_f64_kernel(GemmOp g) {
-  __shared__ double As[kGK][kGT + 1];
-  __shared__ double Bs[kGK][kGT + 1];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const int i0 = blockIdx.y * kGT, j0 = blockIdx.x * kGT;
-  d4 acc = {0.0, 0.0, 0.0, 0.0};
-  for (int k0 = 0; k0 < g.K; k0 += kGK) {
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int idx = t + 256 * e;
-      const int ia = TA ? idx % kGT : idx / kGK;
-      const int ka = TA ? idx / kGT : idx % kGK;
-      const int gi = i0 + ia, gka = k0 + ka;
-      double v = 0.0;
-      if (gi < g.M && gka < g.K) {
-        v = TA ? g.A[(long long)gka * g.lda + gi] : g.A[(long long)gi * g.lda + gka];
-        if (KS) v *= g.kscale[gka];
-      }
-      As[ka][ia] = v;
-      const int jb = TB ? idx / kGK : idx % kGT;
-      const int kb = TB ? idx % kGK : idx / kGT;
-      const int gj = j0 + jb, gkb = k0 + kb;
-      double u = 0.0;
-      if (gj < g.N && gkb < g.K)
-        u = TB ? g.B[(long long)gj * g.ldb + gkb] : g.B[(long long)gkb * g.ldb + gj];
-      Bs[kb][jb] = u;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < kGK; kk += 4) {
-      const double a = As[kk + (lane >> 4)][wm * 16 + (lane & 15)];
-      const double b = Bs[kk + (lane >> 4)][wn * 16 + (lane & 15)];
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  const int col = j0 + wn * 16 + (lane & 15);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = i0 + wm * 16 + (lane >> 4) + 4 * r;
-    if (row < g.M && col < g.N) {
-      double v = g.alpha * acc[r];
-      if (g.row_div) v = v / g.row_div[row];
-      if (g.col_bias) v = g.col_bias[col] + v;
-      double* c = g.C + (long long)row * g.ldc + col;
-      if (g.beta != 0.0) v += g.beta * *c;
-      *c = v;
-    }
-  }
-}
-
-hipError_t gemm(const GemmOp& g, hipStream_t s) {
-  if (g.M <= 0 || g.N <= 0) return hipSuccess;
-  const dim3 grid((unsigned)((g.N + kGT - 1) / kGT), (unsigned)((g.M + kGT - 1) / kGT));
-  const bool ks = g.kscale != nullptr;
-#define VB_GEMM(TA, TB, KS) \
-  hipLaunchKernelGGL((gemm_f64_kernel<TA, TB, KS>), grid, dim3(256), 0, s, g)
-  if (!g.ta && !g.tb) { if (ks) VB_GEMM(false, false, true); else VB_GEMM(false, false, false); }
-  else if (!g.ta && g.tb) { if (ks) VB_GEMM(false, true, true); else VB_GEMM(false, true, false); }
-  else if (g.ta && !g.tb) { if (ks) VB_GEMM(true, false, true); else VB_GEMM(true, false, false); }
-  else { if (ks) VB_GEMM(true, true, true); else VB_GEMM(true, true, false); }
-#undef VB_GEMM
-  return hipGetLastError();
-}
 
 namespace {
 
@@ -143,18 +69,6 @@ __global__ __launch_bounds__(256) void fr_unpack_kernel(int D, const double* lam
   if (j < i) v = lam[base + j];
   else if (j == i) v = exp(lam[base + i]);
   L[idx] = v;
-}
-
-// sq[k] = sqrt(w_k); T[k][j] = sq[k] * Vt[k][j]
-__global__ __launch_bounds__(256) void fr_scale_rows_kernel(int D, const double* w,
-                                                            const double* Vt, double* sq,
-                                                            double* T) {
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)D * D) return;
-  const int k = (int)(idx / D);
-  const double r = sqrt(w[k]);
-  T[idx] = r * Vt[idx];
-  if (idx % D == 0) sq[k] = r;
 }
 
 // Block-wide sum / max over 1024 threads.
@@ -298,18 +212,6 @@ __global__ __launch_bounds__(256) void fr_colsum_kernel(int N, int D, const doub
   out[j] = a;
 }
 
-// Msym_ij = (M_ij + M_ji) / (sq_i + sq_j) + [i == j] 2 c / w_i
-__global__ __launch_bounds__(256) void fr_sylv_kernel(int D, const double* M, const double* sq,
-                                                      const double* w, const double* scal,
-                                                      double* out) {
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)D * D) return;
-  const int i = (int)(idx / D), j = (int)(idx % D);
-  double v = (M[idx] + M[(long long)j * D + i]) / (sq[i] + sq[j]);
-  if (i == j) v += 2.0 * scal[1] / w[i];
-  out[idx] = v;
-}
-
 // grad[D + i(i+1)/2 + j] = G_L[i][j] (j < i), G_L[i][i] * L[i][i] (exp on the diagonal)
 __global__ __launch_bounds__(256) void fr_pack_kernel(int D, const double* GL, const double* L,
                                                       double* grad) {
@@ -349,6 +251,84 @@ __global__ __launch_bounds__(256) void fr_logq_kernel(int D, long long n, const 
   if (lane == 0) out[row] = (t_const - scal[0]) - 0.5 * (df + D) * log(1.0 + a / df);
 }
 
+// 0.5 log det Sigma = sum_i log L_ii = the sum of the free log-diagonal entries
+__global__ __launch_bounds__(1024) void fr_logdet_lam_kernel(int D, const double* lam,
+                                                             double* scal) {
+  __shared__ double red[16];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < D; i += blockDim.x) a += lam[D + (long long)i * (i + 1) / 2 + i];
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) scal[0] = a;
+}
+
+// *out = ||X - shift I||_F^2 for an n x n X.  Per-block partials; the last block
+// to finish (self-resetting ticket) sums them in block order: deterministic.
+constexpr int kNormBlocks = 128;
+__global__ __launch_bounds__(256) void fr_frob2_kernel(int n, const double* X, double shift,
+                                                       double* partial, unsigned* ticket,
+                                                       double* out) {
+  __shared__ double red[16];
+  __shared__ bool last;
+  const long long nn = (long long)n * n;
+  double a = 0.0;
+  for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < nn;
+       idx += 256LL * gridDim.x) {
+    double v = X[idx];
+    if (idx % (n + 1) == 0) v -= shift;
+    a += v * v;
+  }
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = a;
+    __threadfence();
+    last = atomicInc(ticket, gridDim.x - 1) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __threadfence();
+    const volatile double* vp = partial;
+    double t = 0.0;
+    for (unsigned b = 0; b < gridDim.x; ++b) t += vp[b];
+    *out = t;
+  }
+}
+
+// Y0 = Sigma / c, Z0 = I, c = ||Sigma||_F >= lambda_max: the coupled
+// Newton-Schulz iteration converges for eigenvalues of Sigma / c in (0, 1].
+__global__ __launch_bounds__(256) void fr_ns_init_kernel(int D, const double* Sig,
+                                                         const double* nrm2, double* Y0,
+                                                         double* Z0, double* cout) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)D * D) return;
+  const double c = sqrt(*nrm2);
+  Y0[idx] = Sig[idx] / c;
+  Z0[idx] = (idx % (D + 1) == 0) ? 1.0 : 0.0;
+  if (idx == 0) *cout = c;
+}
+
+// dY0 = (G + G^T) / c   (symmetric part of the S cotangent, scaled like Sigma)
+__global__ __launch_bounds__(256) void fr_symscale_kernel(int D, const double* G,
+                                                          const double* cdev, double* out) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)D * D) return;
+  const int i = (int)(idx / D), j = (int)(idx % D);
+  out[idx] = (G[idx] + G[(long long)j * D + i]) / *cdev;
+}
+
+__global__ __launch_bounds__(256) void fr_axpby_kernel(long long n, double a, const double* X,
+                                                       double* Y) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx < n) Y[idx] = a * X[idx];
+}
+
+// H = sqrt(c) dY + 2 coef Sigma^-1   (coef = scal[1], Sigma^-1 = Z_K^2 / c)
+__global__ __launch_bounds__(256) void fr_h_kernel(long long n, double sc, const double* dY,
+                                                   const double* SigInv, const double* scal,
+                                                   double* H) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx < n) H[idx] = sc * dY[idx] + 2.0 * scal[1] * SigInv[idx];
+}
+
 }  // namespace
 
 // ---- workspace ---------------------------------------------------------------
@@ -370,18 +350,23 @@ struct FrWork {
       if (p) (void)hipFree(p);
     }
   };
+  static constexpr int kNSMax = 64;  // Newton-Schulz iterations kept for the tangent pass
   rocblas_handle blas = nullptr;
   int D = 0;
   // D x D
-  Buf L, E, T, S, GS, M, H;
+  Buf L, E, T, S, GS, M, H, Sig, SigInv, dY, dZ, dYn, dZn, dT;
+  Buf nsY[kNSMax], nsZ[kNSMax], nsT[kNSMax];
   // D
   Buf w, sq, offd, scal;
-  Buf info;
+  Buf info, part, ticket, res;
+  double* host_res = nullptr;  // pinned copy of res
+  int K = 0, K_prev = 0;       // Newton-Schulz iterations of the current / previous root
+  double c = 0.0;              // its scaling ||Sigma||_F
   // N x D / N
   Buf Z, X, G, s, logp, zz, r, rk;
-  long long cap_n = 0;
   ~FrWork() {
     if (blas) rocblas_destroy_handle(blas);
+    if (host_res) (void)hipHostFree(host_res);
   }
 };
 
@@ -407,10 +392,25 @@ int reserve_d(FrWork* W, int D, hipStream_t st) {
     return vb_set_error(-2, "rocblas_set_stream failed");
   if (W->D >= D) return 0;
   const size_t dd = sizeof(double) * (size_t)D * D;
-  for (FrWork::Buf* b : {&W->L, &W->E, &W->T, &W->S, &W->GS, &W->M, &W->H}) FR_HIP(b->reserve(dd));
+  for (FrWork::Buf* b : {&W->L, &W->E, &W->T, &W->S, &W->GS, &W->M, &W->H, &W->Sig, &W->SigInv,
+                         &W->dY, &W->dZ, &W->dYn, &W->dZn, &W->dT})
+    FR_HIP(b->reserve(dd));
+  for (int k = 0; k < FrWork::kNSMax; ++k)
+    if (W->nsY[k].p) {  // grow the kept iterates too
+      FR_HIP(W->nsY[k].reserve(dd));
+      FR_HIP(W->nsZ[k].reserve(dd));
+      FR_HIP(W->nsT[k].reserve(dd));
+    }
   for (FrWork::Buf* b : {&W->w, &W->sq, &W->offd}) FR_HIP(b->reserve(sizeof(double) * D));
   FR_HIP(W->scal.reserve(sizeof(double) * 8));
   FR_HIP(W->info.reserve(sizeof(int) * 4));
+  if (!W->ticket.p) {
+    FR_HIP(W->ticket.reserve(sizeof(unsigned) * 4));
+    FR_HIP(hipMemsetAsync(W->ticket.p, 0, sizeof(unsigned) * 4, st));
+  }
+  FR_HIP(W->part.reserve(sizeof(double) * kNormBlocks));
+  FR_HIP(W->res.reserve(sizeof(double) * (FrWork::kNSMax + 2)));
+  if (!W->host_res) FR_HIP(hipHostMalloc(&W->host_res, sizeof(double) * (FrWork::kNSMax + 2)));
   W->D = D;
   return 0;
 }
@@ -426,8 +426,9 @@ int reserve_n(FrWork* W, int D, long long n) {
 
 }  // namespace
 
-// L, eigh(L L^T) -> (w ascending, Vt rows = eigenvectors), half log det, S = sqrtm(Sigma)
-int fr_prepare(FrWork* W, int D, const double* lam, bool need_sqrt, hipStream_t st) {
+// L, eigh(L L^T) -> (w ascending, Vt rows = eigenvectors), half log det from the
+// eigenvalues (multivariate_t_logpdf's log_pdet, _distributions.py:27-32)
+int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st) {
   if (int rc = reserve_d(W, D, st)) return rc;
   hipLaunchKernelGGL(fr_unpack_kernel, dim3(blocks((long long)D * D)), dim3(256), 0, st, D, lam,
                      W->L.d());
@@ -439,11 +440,127 @@ int fr_prepare(FrWork* W, int D, const double* lam, bool need_sqrt, hipStream_t 
                                        static_cast<rocblas_int*>(W->info.p));
   if (rs != rocblas_status_success) return vb_set_error(-2, "rocsolver_dsyevd failed (%d)", (int)rs);
   hipLaunchKernelGGL(fr_logdet_kernel, dim3(1), dim3(1024), 0, st, D, W->w.d(), W->scal.d());
-  if (need_sqrt) {
-    hipLaunchKernelGGL(fr_scale_rows_kernel, dim3(blocks((long long)D * D)), dim3(256), 0, st, D,
-                       W->w.d(), W->E.d(), W->sq.d(), W->T.d());
-    FR_HIP(gemm(mm(D, D, D, W->E.d(), true, W->T.d(), false, W->S.d()), st));
+  FR_HIP(hipGetLastError());
+  return 0;
+}
+
+namespace {
+int frob2(FrWork* W, int n, const double* X, double shift, double* out, hipStream_t st) {
+  const long long nn = (long long)n * n;
+  const unsigned nb = (unsigned)std::min<long long>(kNormBlocks, std::max(1LL, (nn + 255) / 256));
+  hipLaunchKernelGGL(fr_frob2_kernel, dim3(nb), dim3(256), 0, st, n, X, shift, W->part.d(),
+                     static_cast<unsigned*>(W->ticket.p), out);
+  FR_HIP(hipGetLastError());
+  return 0;
+}
+}  // namespace
+
+// S = sqrtm(Sigma) without an eigendecomposition: coupled Newton-Schulz on
+// A = Sigma / c (Higham, Functions of Matrices §6.3):
+//   T_k = 3I - Z_k Y_k,  Y_{k+1} = Y_k T_k / 2,  Z_{k+1} = T_k Z_k / 2
+//   Y_k -> (Sigma / c)^{1/2},  Z_k -> (Sigma / c)^{-1/2}.
+// The iterates are kept for the tangent (Sylvester) pass.  Converged when
+// ||I - Z_k Y_k||_F <= 1e-12 sqrt(D) or has stalled at rounding level; the host
+// reads the residuals at most once per iteration after the previous root's count.
+// Also: L, Sigma = L L^T, scal[0] = 0.5 log det Sigma = sum log L_ii.
+int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st) {
+  if (int rc = reserve_d(W, D, st)) return rc;
+  const long long dd = (long long)D * D;
+  const size_t bytes = sizeof(double) * (size_t)dd;
+  hipLaunchKernelGGL(fr_unpack_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, lam, W->L.d());
+  hipLaunchKernelGGL(fr_logdet_lam_kernel, dim3(1), dim3(1024), 0, st, D, lam, W->scal.d());
+  FR_HIP(gemm(mm(D, D, D, W->L.d(), false, W->L.d(), true, W->Sig.d()), st));
+  double* res = W->res.d();
+  const int KM = FrWork::kNSMax;
+  if (int rc = frob2(W, D, W->Sig.d(), 0.0, res + KM, st)) return rc;
+  FR_HIP(W->nsY[0].reserve(bytes));
+  FR_HIP(W->nsZ[0].reserve(bytes));
+  hipLaunchKernelGGL(fr_ns_init_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, W->Sig.d(), res + KM,
+                     W->nsY[0].d(), W->nsZ[0].d(), res + KM + 1);
+  const int kmin = std::max(2, W->K_prev);
+  const double tol = 1e-12 * std::sqrt((double)D), stall = 1e-8 * std::sqrt((double)D);
+  int K = -1;
+  for (int k = 0; k < KM; ++k) {
+    FR_HIP(W->nsT[k].reserve(bytes));
+    GemmOp g = mm(D, D, D, W->nsZ[k].d(), false, W->nsY[k].d(), false, W->nsT[k].d(), -1.0);
+    g.diag = 3.0;
+    FR_HIP(gemm(g, st));
+    if (int rc = frob2(W, D, W->nsT[k].d(), 2.0, res + k, st)) return rc;
+    if (k >= kmin) {
+      FR_HIP(hipMemcpyAsync(W->host_res, res, sizeof(double) * (KM + 2), hipMemcpyDeviceToHost, st));
+      FR_HIP(hipStreamSynchronize(st));
+      const double rk = std::sqrt(W->host_res[k]), rp = std::sqrt(W->host_res[k - 1]);
+      if (!(rk < 1e30))
+        return vb_set_error(-2, "Newton-Schulz square root of Sigma diverged (residual %g)", rk);
+      if (rk <= tol || (rk <= stall && rk >= 0.25 * rp)) {
+        K = k;
+        break;
+      }
+    }
+    if (k + 1 >= KM) break;
+    FR_HIP(W->nsY[k + 1].reserve(bytes));
+    FR_HIP(W->nsZ[k + 1].reserve(bytes));
+    FR_HIP(gemm(mm(D, D, D, W->nsY[k].d(), false, W->nsT[k].d(), false, W->nsY[k + 1].d(), 0.5), st));
+    FR_HIP(gemm(mm(D, D, D, W->nsT[k].d(), false, W->nsZ[k].d(), false, W->nsZ[k + 1].d(), 0.5), st));
   }
+  if (K < 0)
+    return vb_set_error(-2, "Newton-Schulz square root of Sigma did not converge in %d iterations "
+                            "(Sigma too ill-conditioned)", KM);
+  W->K = K;
+  W->K_prev = K;
+  W->c = W->host_res[KM + 1];
+  FR_HIP(hipGetLastError());
+  return 0;
+}
+
+// Sylvester solve of autograd's sqrtm VJP, S X + X S = G_S + G_S^T, as the
+// forward-mode derivative of the Newton-Schulz iteration (the Frechet
+// derivative of sqrtm at a symmetric Sigma is self-adjoint), then
+// H = X + 2 c_inv Sigma^-1 (the symmetric Sigma cotangent, doubled).
+//   dT_k = -(dZ_k Y_k + Z_k dY_k)
+//   dY_{k+1} = (dY_k T_k + Y_k dT_k) / 2,  dZ_{k+1} = (dT_k Z_k + T_k dZ_k) / 2
+// with dY_0 = (G_S + G_S^T) / c, dZ_0 = 0; X = sqrt(c) dY_{K+1}.
+int fr_sylvester(FrWork* W, int D, double* H, hipStream_t st) {
+  const long long dd = (long long)D * D;
+  const int K = W->K;
+  const double* cdev = W->res.d() + FrWork::kNSMax + 1;
+  hipLaunchKernelGGL(fr_symscale_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, W->GS.d(), cdev,
+                     W->dY.d());
+  double *dY = W->dY.d(), *dZ = W->dZ.d(), *dYn = W->dYn.d(), *dZn = W->dZn.d(), *dT = W->dT.d();
+  // k = 0: Z_0 = I, dZ_0 = 0, dT_0 = -dY_0
+  {
+    FR_HIP(gemm(mm(D, D, D, dY, false, W->nsT[0].d(), false, dYn, 0.5), st));
+    GemmOp g = mm(D, D, D, W->nsY[0].d(), false, dY, false, dYn, -0.5);
+    g.beta = 1.0;
+    FR_HIP(gemm(g, st));
+    hipLaunchKernelGGL(fr_axpby_kernel, dim3(blocks(dd)), dim3(256), 0, st, dd, -0.5, dY, dZn);
+    std::swap(dY, dYn);
+    std::swap(dZ, dZn);
+  }
+  for (int k = 1; k <= K; ++k) {
+    const double *Yk = W->nsY[k].d(), *Zk = W->nsZ[k].d(), *Tk = W->nsT[k].d();
+    FR_HIP(gemm(mm(D, D, D, dZ, false, Yk, false, dT, -1.0), st));
+    GemmOp g = mm(D, D, D, Zk, false, dY, false, dT, -1.0);
+    g.beta = 1.0;
+    FR_HIP(gemm(g, st));
+    FR_HIP(gemm(mm(D, D, D, dY, false, Tk, false, dYn, 0.5), st));
+    g = mm(D, D, D, Yk, false, dT, false, dYn, 0.5);
+    g.beta = 1.0;
+    FR_HIP(gemm(g, st));
+    if (k < K) {
+      FR_HIP(gemm(mm(D, D, D, dT, false, Zk, false, dZn, 0.5), st));
+      g = mm(D, D, D, Tk, false, dZ, false, dZn, 0.5);
+      g.beta = 1.0;
+      FR_HIP(gemm(g, st));
+    }
+    std::swap(dY, dYn);
+    std::swap(dZ, dZn);
+  }
+  // Sigma^-1 = Z_K^2 / c
+  FR_HIP(gemm(mm(D, D, D, W->nsZ[K].d(), false, W->nsZ[K].d(), false, W->SigInv.d(), 1.0 / W->c),
+              st));
+  hipLaunchKernelGGL(fr_h_kernel, dim3(blocks(dd)), dim3(256), 0, st, dd, std::sqrt(W->c), dY,
+                     W->SigInv.d(), W->scal.d(), H);
   FR_HIP(hipGetLastError());
   return 0;
 }
@@ -468,10 +585,10 @@ int fr_draw(FrWork* W, int D, long long n, double df, const double* host_eps, ui
   return 0;
 }
 
-// x = mu + (z S) / s  (after fr_prepare with need_sqrt)
+// x = mu + (z S) / s, S = sqrt(c) Y_K  (after fr_sqrt)
 int fr_transform(FrWork* W, int D, long long n, const double* mu, const double* s,
                  const double* z, double* x, hipStream_t st) {
-  GemmOp g = mm((int)n, D, D, z, false, W->S.d(), false, x);
+  GemmOp g = mm((int)n, D, D, z, false, W->nsY[W->K].d(), false, x, std::sqrt(W->c));
   g.row_div = s;
   g.col_bias = mu;
   FR_HIP(gemm(g, st));
@@ -503,7 +620,7 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
                   uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
                   double* grad, hipStream_t st) {
   const int D = f.D, N = f.N;
-  if (int rc = fr_prepare(W, D, lam, true, st)) return rc;
+  if (int rc = fr_sqrt(W, D, lam, st)) return rc;
   if (int rc = reserve_n(W, D, N)) return rc;
   const double *s, *z;
   if (int rc = fr_draw(W, D, N, f.df, host_eps, k0, k1, stream, step, &s, &z, st)) return rc;
@@ -529,13 +646,8 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
   FR_HIP(gemm(g, st));
   hipLaunchKernelGGL(fr_colsum_kernel, dim3(blocks(D)), dim3(256), 0, st, N, D, W->r.d(), W->G.d(),
                      grad);
-  // Sylvester solve in the eigenbasis (Vt = E rows)
-  FR_HIP(gemm(mm(D, D, D, W->E.d(), false, W->GS.d(), false, W->T.d()), st));
-  FR_HIP(gemm(mm(D, D, D, W->T.d(), false, W->E.d(), true, W->M.d()), st));
-  hipLaunchKernelGGL(fr_sylv_kernel, dim3(blocks((long long)D * D)), dim3(256), 0, st, D, W->M.d(),
-                     W->sq.d(), W->w.d(), W->scal.d(), W->H.d());
-  FR_HIP(gemm(mm(D, D, D, W->E.d(), true, W->H.d(), false, W->T.d()), st));
-  FR_HIP(gemm(mm(D, D, D, W->T.d(), false, W->E.d(), false, W->M.d()), st));
+  // Sylvester solve (sqrtm VJP) + entropy / log q term -> symmetric Sigma cotangent
+  if (int rc = fr_sylvester(W, D, W->M.d(), st)) return rc;
   // G_L = H L, packed with the exp-diagonal chain rule
   FR_HIP(gemm(mm(D, D, D, W->M.d(), false, W->L.d(), false, W->H.d()), st));
   hipLaunchKernelGGL(fr_pack_kernel, dim3(blocks((long long)D * D)), dim3(256), 0, st, D, W->H.d(),
@@ -547,7 +659,7 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
 // log q(x) for arbitrary x (n x D) at lam
 int fr_logdensity(FrWork* W, int D, double df, double t_const, const double* lam, const double* x,
                   long long n, double* out, hipStream_t st) {
-  if (int rc = fr_prepare(W, D, lam, false, st)) return rc;
+  if (int rc = fr_prepare(W, D, lam, st)) return rc;
   if (int rc = reserve_n(W, D, n)) return rc;
   hipLaunchKernelGGL(fr_center_kernel, dim3(blocks(n * D)), dim3(256), 0, st, D, n, x, lam,
                      W->X.d());
@@ -564,7 +676,7 @@ int fr_log_weights(FrWork* W, const FrSpec& f, const double* lam, long long m,
                    const double* host_eps, uint32_t k0, uint32_t k1, uint32_t stream,
                    uint32_t step, double* lw, double* xs, hipStream_t st) {
   const int D = f.D;
-  if (int rc = fr_prepare(W, D, lam, true, st)) return rc;
+  if (int rc = fr_sqrt(W, D, lam, st)) return rc;
   if (int rc = reserve_n(W, D, m)) return rc;
   const double *s, *z;
   if (int rc = fr_draw(W, D, m, f.df, host_eps, k0, k1, stream, step, &s, &z, st)) return rc;
@@ -612,7 +724,7 @@ int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, 
                      W->L.d());
   if (sigma) FR_HIP(gemm(mm(D, D, D, W->L.d(), false, W->L.d(), true, sigma), st));
   if (eig) {
-    if (int rc = fr_prepare(W, D, lam, false, st)) return rc;
+    if (int rc = fr_prepare(W, D, lam, st)) return rc;
     FR_HIP(hipMemcpyAsync(eig, W->w.d(), sizeof(double) * D, hipMemcpyDeviceToDevice, st));
   }
   return 0;

@@ -1,0 +1,195 @@
+// vb_gemm.hpp — fp64 GEMM on CDNA4 matrix cores (v_mfma_f64_16x16x4_f64) with
+// the epilogues the full-rank path fuses (row divide, column bias, beta C).
+//
+// C[M][N] = alpha * op(A) diag(kscale) op(B) [/ row_div[i]] [+ col_bias[j]] [+ diag I] + beta C
+// (row-major, leading dimensions lda/ldb/ldc; op = transpose when ta / tb).
+//
+// Block tile 32 x 32 computed by 8 waves: 4 output quadrants of 16 x 16 x 2 halves
+// of every k tile (intra-block split-K, reduced through LDS at the end), each
+// wave running 4 independent MFMA accumulator chains.  K is staged 64 at a time
+// through double-buffered LDS with the next tile's global loads in flight while
+// the current one feeds the MFMAs (one barrier per tile).
+// LDS layout per operand follows its contiguous global dimension so both the
+// coalesced store and the fragment read are conflict-free at the 2-pass minimum:
+//   contiguous in k  -> [row][k]  (stride 36 doubles)
+//   contiguous in row -> [k][row] (stride 48 doubles)
+// MFMA operand maps (cdna_hip_programming.md): A[l&15][k=l>>4], B[k=l>>4][l&15];
+// C row = (l>>4) + 4 r, col = l&15.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace vbk {
+
+struct GemmOp {
+  bool ta, tb;
+  int M, N, K;
+  const double* A;
+  long long lda;
+  const double* B;
+  long long ldb;
+  double* C;
+  long long ldc;
+  double alpha, beta;
+  const double* kscale;    // [K] or null
+  const double* row_div;   // [M] or null
+  const double* col_bias;  // [N] or null
+  double diag;             // added to C[i][i] (after the bias)
+};
+
+namespace gemm_detail {
+
+using d4 = double __attribute__((ext_vector_type(4)));
+constexpr int BT = 32;   // block tile (rows and columns)
+#ifndef VB_GEMM_KT
+#define VB_GEMM_KT 64
+#endif
+constexpr int KT = VB_GEMM_KT;  // k tile
+constexpr int SR = KT + 4;      // [row][k] stride
+constexpr int SK = BT + 16;     // [k][row] stride
+constexpr int BUF = (BT * SR > KT * SK) ? BT * SR : KT * SK;  // doubles per operand buffer
+constexpr int NTH = 512;                                       // 8 waves
+constexpr int PER = BT * KT / NTH;                             // elements per thread per tile
+
+// One operand tile (BT rows x KT k) of a row-major matrix X with leading
+// dimension ld; KCONTIG: X is [row][k] in memory (k contiguous), else [k][row].
+template <bool KCONTIG, bool KS>
+struct Tile {
+  double v[PER];
+  __device__ __forceinline__ void load(const double* X, long long ld, int r0, int k0, int R,
+                                       int K, const double* kscale, int t) {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int idx = t + NTH * e;
+      const int r = KCONTIG ? idx / KT : idx % BT;
+      const int k = KCONTIG ? idx % KT : idx / BT;
+      const int gr = r0 + r, gk = k0 + k;
+      double x = 0.0;
+      if (gr < R && gk < K) {
+        x = KCONTIG ? X[(long long)gr * ld + gk] : X[(long long)gk * ld + gr];
+        if (KS) x *= kscale[gk];
+      }
+      v[e] = x;
+    }
+  }
+  __device__ __forceinline__ void store(double* s, int t) const {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int idx = t + NTH * e;
+      const int r = KCONTIG ? idx / KT : idx % BT;
+      const int k = KCONTIG ? idx % KT : idx / BT;
+      s[KCONTIG ? r * SR + k : k * SK + r] = v[e];
+    }
+  }
+};
+
+template <bool KCONTIG>
+__device__ __forceinline__ double frag(const double* s, int r, int k) {
+  return KCONTIG ? s[r * SR + k] : s[k * SK + r];
+}
+
+template <bool TA, bool TB, bool KS>
+__global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmOp g) {
+  // A is k-contiguous when not transposed; B is k-contiguous when transposed.
+  constexpr bool AK = !TA, BK = TB;
+  __shared__ double sA[2][BUF];
+  __shared__ double sB[2][BUF];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int q = w & 3, h = w >> 2;           // output quadrant, k half of each tile
+  const int wm = q >> 1, wn = q & 1;
+  const int i0 = blockIdx.y * BT, j0 = blockIdx.x * BT;
+  const int nt = (g.K + KT - 1) / KT;
+  // two register stages: tile it+2 is loaded while tile it feeds the MFMAs
+  // and tile it+1 (loaded one iteration earlier) moves to LDS
+  Tile<AK, KS> ta0, ta1;
+  Tile<BK, false> tb0, tb1;
+  ta0.load(g.A, g.lda, i0, 0, g.M, g.K, g.kscale, t);
+  tb0.load(g.B, g.ldb, j0, 0, g.N, g.K, nullptr, t);
+  if (nt > 1) {
+    ta1.load(g.A, g.lda, i0, KT, g.M, g.K, g.kscale, t);
+    tb1.load(g.B, g.ldb, j0, KT, g.N, g.K, nullptr, t);
+  }
+  ta0.store(sA[0], t);
+  tb0.store(sB[0], t);
+  __syncthreads();
+  // four independent accumulator chains (interleaved k4 steps): one dependent
+  // f64 MFMA chain per wave is latency-bound on gfx950
+  d4 acc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+  const int ra = wm * 16 + (lane & 15), cb = wn * 16 + (lane & 15), kq = lane >> 4;
+  const int kb = h * (KT / 2);
+  auto mma = [&](const double* a_s, const double* b_s) {
+#pragma unroll
+    for (int s = 0; s < KT / 8; ++s) {
+      const int kk = kb + 4 * s;
+      const double a = frag<AK>(a_s, ra, kk + kq);
+      const double b = frag<BK>(b_s, cb, kk + kq);
+      acc[s & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[s & 3], 0, 0, 0);
+    }
+  };
+  for (int it = 0; it < nt; it += 2) {
+    if (it + 2 < nt) {
+      ta0.load(g.A, g.lda, i0, (it + 2) * KT, g.M, g.K, g.kscale, t);
+      tb0.load(g.B, g.ldb, j0, (it + 2) * KT, g.N, g.K, nullptr, t);
+    }
+    mma(sA[0], sB[0]);
+    if (it + 1 < nt) {
+      ta1.store(sA[1], t);
+      tb1.store(sB[1], t);
+    }
+    __syncthreads();
+    if (it + 1 >= nt) break;
+    if (it + 3 < nt) {
+      ta1.load(g.A, g.lda, i0, (it + 3) * KT, g.M, g.K, g.kscale, t);
+      tb1.load(g.B, g.ldb, j0, (it + 3) * KT, g.N, g.K, nullptr, t);
+    }
+    mma(sA[1], sB[1]);
+    if (it + 2 < nt) {
+      ta0.store(sA[0], t);
+      tb0.store(sB[0], t);
+    }
+    __syncthreads();
+  }
+  d4 r4 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  // k-half 1 hands its partial tile to k-half 0 through LDS
+  double* red = sA[0];
+  if (h == 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(q * 4 + r) * 64 + lane] = r4[r];
+  }
+  __syncthreads();
+  if (h == 1) return;
+  const int col = j0 + wn * 16 + (lane & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = i0 + wm * 16 + kq + 4 * r;
+    if (row < g.M && col < g.N) {
+      double v = g.alpha * (r4[r] + red[(q * 4 + r) * 64 + lane]);
+      if (g.row_div) v = v / g.row_div[row];
+      if (g.col_bias) v = g.col_bias[col] + v;
+      if (row == col) v += g.diag;
+      double* c = g.C + (long long)row * g.ldc + col;
+      if (g.beta != 0.0) v += g.beta * *c;
+      *c = v;
+    }
+  }
+}
+
+}  // namespace gemm_detail
+
+inline hipError_t gemm(const GemmOp& g, hipStream_t s) {
+  using namespace gemm_detail;
+  if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((g.N + BT - 1) / BT), (unsigned)((g.M + BT - 1) / BT));
+  const bool ks = g.kscale != nullptr;
+#define VB_GEMM(TA, TB, KS) \
+  hipLaunchKernelGGL((gemm_f64_kernel<TA, TB, KS>), grid, dim3(NTH), 0, s, g)
+  if (!g.ta && !g.tb) { if (ks) VB_GEMM(false, false, true); else VB_GEMM(false, false, false); }
+  else if (!g.ta && g.tb) { if (ks) VB_GEMM(false, true, true); else VB_GEMM(false, true, false); }
+  else if (g.ta && !g.tb) { if (ks) VB_GEMM(true, false, true); else VB_GEMM(true, false, false); }
+  else { if (ks) VB_GEMM(true, true, true); else VB_GEMM(true, true, false); }
+#undef VB_GEMM
+  return hipGetLastError();
+}
+
+}  // namespace vbk

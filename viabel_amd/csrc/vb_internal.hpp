@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "vb_gemm.hpp"
+
 namespace vbk {
 
 constexpr int kBlockDMax = 16;  // largest D handled by the block-per-problem kernel
@@ -118,23 +120,6 @@ int vb_set_error(int code, const char* fmt, ...);  // defined in vb_capi.hip
 constexpr int kFamilyFrT = 2;
 constexpr int kTargetCorrGauss = 4;
 
-// C[M][N] = alpha * op(A) diag(kscale) op(B) [/ row_div[i]] [+ col_bias[j]] + beta C,
-// row-major with leading dimensions; fp64 MFMA.
-struct GemmOp {
-  bool ta, tb;
-  int M, N, K;
-  const double* A;
-  long long lda;
-  const double* B;
-  long long ldb;
-  double* C;
-  long long ldc;
-  double alpha, beta;
-  const double* kscale;    // [K] or null
-  const double* row_div;   // [M] or null
-  const double* col_bias;  // [N] or null
-};
-hipError_t gemm(const GemmOp& g, hipStream_t s);
 
 struct FrWork;  // per-context workspace + rocBLAS handle
 FrWork* fr_work_create();
@@ -148,7 +133,8 @@ struct FrSpec {
 };
 
 // All return 0 or a VB_E* code (message via vb_set_error).
-int fr_prepare(FrWork* W, int D, const double* lam, bool need_sqrt, hipStream_t st);
+int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st);  // eigh of Sigma
+int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st);     // Newton-Schulz sqrtm
 int fr_draw(FrWork* W, int D, long long n, double df, const double* host_eps, uint32_t k0,
             uint32_t k1, uint32_t stream, uint32_t step, const double** s_out,
             const double** z_out, hipStream_t st);
