@@ -202,14 +202,19 @@ __global__ __launch_bounds__(1024) void fr_weights_kernel(int N, int D, int chiv
   }
 }
 
-// gmu[j] = sum_n r_n G[n][j]
+// gmu[j] = sum_n r_n G[n][j]: 64 columns per block, the 4 waves take every
+// 4th row, fixed-order combine in LDS
 __global__ __launch_bounds__(256) void fr_colsum_kernel(int N, int D, const double* r,
                                                         const double* G, double* out) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= D) return;
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
   double a = 0.0;
-  for (int n = 0; n < N; ++n) a += r[n] * G[(long long)n * D + j];
-  out[j] = a;
+  if (j < D)
+    for (int n = wv; n < N; n += 4) a += r[n] * G[(long long)n * D + j];
+  part[wv][lane] = a;
+  __syncthreads();
+  if (wv == 0 && j < D) out[j] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
 }
 
 // grad[D + i(i+1)/2 + j] = G_L[i][j] (j < i), G_L[i][i] * L[i][i] (exp on the diagonal)
@@ -284,23 +289,64 @@ __global__ __launch_bounds__(256) void fr_frob2_kernel(int n, const double* X, d
     last = atomicInc(ticket, gridDim.x - 1) == gridDim.x - 1;
   }
   __syncthreads();
-  if (last && threadIdx.x == 0) {
+  if (last) {
     __threadfence();
-    const volatile double* vp = partial;
-    double t = 0.0;
-    for (unsigned b = 0; b < gridDim.x; ++b) t += vp[b];
-    *out = t;
+    __shared__ double ps[kNormBlocks];
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += 256)
+      ps[b] = __hip_atomic_load(partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (unsigned b = 0; b < gridDim.x; ++b) t += ps[b];  // fixed order
+      *out = t;
+    }
   }
 }
 
-// Y0 = Sigma / c, Z0 = I, c = ||Sigma||_F >= lambda_max: the coupled
-// Newton-Schulz iteration converges for eigenvalues of Sigma / c in (0, 1].
+// Power iteration for lambda_max(Sigma): y = Sigma x / ||x||, 8 rows per block
+// (two per wave).  x0 = ones.
+__global__ __launch_bounds__(256) void fr_power_kernel(int D, const double* Sig, const double* x,
+                                                       double* y) {
+  __shared__ double red[16];
+  __shared__ double inv_n;
+  double a = 0.0;
+  for (int i = threadIdx.x; i < D; i += 256) {
+    const double v = x ? x[i] : 1.0;
+    a += v * v;
+  }
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) inv_n = 1.0 / sqrt(a);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int rr = 0; rr < 2; ++rr) {
+    const int row = blockIdx.x * 8 + wv * 2 + rr;
+    if (row >= D) break;
+    double t = 0.0;
+    for (int j = lane; j < D; j += 64) t += Sig[(long long)row * D + j] * (x ? x[j] : 1.0);
+    t = wave_sum(t);
+    if (lane == 0) y[row] = t * inv_n;
+  }
+}
+
+// *out = ||x||^2 (one block)
+__global__ __launch_bounds__(256) void fr_norm2_kernel(int n, const double* x, double* out) {
+  __shared__ double red[16];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) a += x[i] * x[i];
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) *out = a;
+}
+
+// Y0 = Sigma / c, Z0 = I.  The coupled Newton-Schulz iteration converges for
+// eigenvalues of Sigma / c in (0, 3) (p -> p (3 - p)^2 / 4), fastest when the
+// largest is near 1: c = 1.25 x the power-iteration estimate of lambda_max
+// (which is <= lambda_max), capped by ||Sigma||_F (>= lambda_max).
 __global__ __launch_bounds__(256) void fr_ns_init_kernel(int D, const double* Sig,
                                                          const double* nrm2, double* Y0,
                                                          double* Z0, double* cout) {
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (long long)D * D) return;
-  const double c = sqrt(*nrm2);
+  const double c = fmin(1.25 * sqrt(nrm2[1]), sqrt(nrm2[0]));
   Y0[idx] = Sig[idx] / c;
   Z0[idx] = (idx % (D + 1) == 0) ? 1.0 : 0.0;
   if (idx == 0) *cout = c;
@@ -361,7 +407,7 @@ struct FrWork {
   Buf info, part, ticket, res;
   double* host_res = nullptr;  // pinned copy of res
   int K = 0, K_prev = 0;       // Newton-Schulz iterations of the current / previous root
-  double c = 0.0;              // its scaling ||Sigma||_F
+  double c = 0.0;              // its scaling (~1.25 lambda_max)
   // N x D / N
   Buf Z, X, G, s, logp, zz, r, rk;
   ~FrWork() {
@@ -409,8 +455,8 @@ int reserve_d(FrWork* W, int D, hipStream_t st) {
     FR_HIP(hipMemsetAsync(W->ticket.p, 0, sizeof(unsigned) * 4, st));
   }
   FR_HIP(W->part.reserve(sizeof(double) * kNormBlocks));
-  FR_HIP(W->res.reserve(sizeof(double) * (FrWork::kNSMax + 2)));
-  if (!W->host_res) FR_HIP(hipHostMalloc(&W->host_res, sizeof(double) * (FrWork::kNSMax + 2)));
+  FR_HIP(W->res.reserve(sizeof(double) * (FrWork::kNSMax + 3)));
+  if (!W->host_res) FR_HIP(hipHostMalloc(&W->host_res, sizeof(double) * (FrWork::kNSMax + 3)));
   W->D = D;
   return 0;
 }
@@ -473,10 +519,22 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st) {
   double* res = W->res.d();
   const int KM = FrWork::kNSMax;
   if (int rc = frob2(W, D, W->Sig.d(), 0.0, res + KM, st)) return rc;
+  // lambda_max estimate: 8 power steps (vectors in the sq / offd / w scratch)
+  {
+    const unsigned nb = (unsigned)((D + 7) / 8);
+    double *xa = W->sq.d(), *xb = W->offd.d();
+    hipLaunchKernelGGL(fr_power_kernel, dim3(nb), dim3(256), 0, st, D, W->Sig.d(), nullptr, xa);
+    for (int p = 1; p < 8; ++p) {
+      hipLaunchKernelGGL(fr_power_kernel, dim3(nb), dim3(256), 0, st, D, W->Sig.d(), xa, xb);
+      std::swap(xa, xb);
+    }
+    hipLaunchKernelGGL(fr_power_kernel, dim3(nb), dim3(256), 0, st, D, W->Sig.d(), xa, xb);
+    hipLaunchKernelGGL(fr_norm2_kernel, dim3(1), dim3(256), 0, st, D, xb, res + KM + 1);
+  }
   FR_HIP(W->nsY[0].reserve(bytes));
   FR_HIP(W->nsZ[0].reserve(bytes));
   hipLaunchKernelGGL(fr_ns_init_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, W->Sig.d(), res + KM,
-                     W->nsY[0].d(), W->nsZ[0].d(), res + KM + 1);
+                     W->nsY[0].d(), W->nsZ[0].d(), res + KM + 2);
   const int kmin = std::max(2, W->K_prev);
   const double tol = 1e-12 * std::sqrt((double)D), stall = 1e-8 * std::sqrt((double)D);
   int K = -1;
@@ -487,7 +545,7 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st) {
     FR_HIP(gemm(g, st));
     if (int rc = frob2(W, D, W->nsT[k].d(), 2.0, res + k, st)) return rc;
     if (k >= kmin) {
-      FR_HIP(hipMemcpyAsync(W->host_res, res, sizeof(double) * (KM + 2), hipMemcpyDeviceToHost, st));
+      FR_HIP(hipMemcpyAsync(W->host_res, res, sizeof(double) * (KM + 3), hipMemcpyDeviceToHost, st));
       FR_HIP(hipStreamSynchronize(st));
       const double rk = std::sqrt(W->host_res[k]), rp = std::sqrt(W->host_res[k - 1]);
       if (!(rk < 1e30))
@@ -508,7 +566,7 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st) {
                             "(Sigma too ill-conditioned)", KM);
   W->K = K;
   W->K_prev = K;
-  W->c = W->host_res[KM + 1];
+  W->c = W->host_res[KM + 2];
   FR_HIP(hipGetLastError());
   return 0;
 }
@@ -523,7 +581,7 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st) {
 int fr_sylvester(FrWork* W, int D, double* H, hipStream_t st) {
   const long long dd = (long long)D * D;
   const int K = W->K;
-  const double* cdev = W->res.d() + FrWork::kNSMax + 1;
+  const double* cdev = W->res.d() + FrWork::kNSMax + 2;
   hipLaunchKernelGGL(fr_symscale_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, W->GS.d(), cdev,
                      W->dY.d());
   double *dY = W->dY.d(), *dZ = W->dZ.d(), *dYn = W->dYn.d(), *dZn = W->dZn.d(), *dT = W->dT.d();
@@ -644,8 +702,8 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
   GemmOp g = mm(D, D, N, z, true, W->G.d(), false, W->GS.d());
   g.kscale = W->rk.d();
   FR_HIP(gemm(g, st));
-  hipLaunchKernelGGL(fr_colsum_kernel, dim3(blocks(D)), dim3(256), 0, st, N, D, W->r.d(), W->G.d(),
-                     grad);
+  hipLaunchKernelGGL(fr_colsum_kernel, dim3(blocks(D, 64)), dim3(256), 0, st, N, D, W->r.d(),
+                     W->G.d(), grad);
   // Sylvester solve (sqrtm VJP) + entropy / log q term -> symmetric Sigma cotangent
   if (int rc = fr_sylvester(W, D, W->M.d(), st)) return rc;
   // G_L = H L, packed with the exp-diagonal chain rule
