@@ -22,7 +22,11 @@
  *                          eigvalsh / entropy det)
  *   vb_objective_value_grad viabel/vb.py:236-245 (black_box_klvi),
  *                          viabel/vb.py:248-266 (black_box_chivi)
- *   vb_run_*               viabel/vb.py:324-389 (learning_rate_schedule, adagrad_optimize)
+ *   vb_run_*               viabel/vb.py:324-389 (learning_rate_schedule, adagrad_optimize),
+ *                          viabel/vb.py:392-712 (the RMSProp-IA / Adam-IA updates)
+ *   vb_rhat                viabel/functions.py:8-65 (compute_R_hat and its windowed /
+ *                          halfway drivers)
+ *   vb_iterate_average     viabel/functions.py:68-77 (stochastic_iterate_averaging)
  *   vb_adagrad_update      viabel/vb.py:364-374 (one adagrad step for a foreign objective)
  *   vb_log_weights         notebooks/experiments.py:60-63 (get_samples_and_log_weights)
  *   vb_divergence_bound    viabel/bounds.py:142-192 (divergence_bound, mean_and_check_mc_error)
@@ -120,11 +124,21 @@ typedef struct vb_noise {
   uint32_t reserved;
 } vb_noise;
 
-/* Adagrad settings, vb.py:345-347 defaults: window 10, lr .01, eps .1. */
+enum vb_optimizer_kind {
+  VB_OPT_ADAGRAD = 0,      /* adagrad_optimize, vb.py:345-389 (window of W gradients) */
+  VB_OPT_RMSPROP_IA = 1,   /* rmsprop_IA_optimize_with_rhat's update, vb.py:436-453 */
+  VB_OPT_ADAM_IA = 2       /* adam_IA_optimize_with_rhat's update, vb.py:606-617 */
+};
+
+/* Optimiser settings, vb.py:345-347 defaults: window 10, lr .01, eps .1.
+ * ADAGRAD: window = gradient window (<= 64); history = parameters AFTER the
+ * update for the last n_iters - 3 n_iters / 4 iterations (vb.py:375-376).
+ * RMSPROP_IA / ADAM_IA: history = parameters BEFORE each update for the last
+ * min(n_iters, 100 window) iterations (vb.py:455-457, 622-624). */
 typedef struct vb_adagrad_config {
   int64_t n_iters;
   int32_t window;
-  int32_t reserved;
+  int32_t optimizer; /* vb_optimizer_kind */
   double learning_rate;
   double learning_rate_end; /* NaN = None (constant schedule) */
   double epsilon;
@@ -178,7 +192,7 @@ int vb_run_create(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,
 int vb_run_advance(vb_run* run, int64_t n_steps, const vb_noise* noise);
 int vb_run_steps_done(vb_run* run, int64_t* out);
 /* Results (all nullable): lam_out [n_problems][P]; hist_out
- * [n_problems][n_iters - 3*n_iters/4][P]; values_out [n_problems][n_iters];
+ * [n_problems][n_hist][P] (n_hist per vb_adagrad_config); values_out [n_problems][n_iters];
  * smoothed_out [n_problems][P] = mean of the history rows (vb.py:386-387). */
 int vb_run_result(vb_run* run, double* lam_out, double* hist_out,
                   double* values_out, double* smoothed_out);
@@ -190,6 +204,18 @@ int vb_run_destroy(vb_run* run);
 int vb_adagrad_update(vb_ctx* ctx, int64_t P, double* lam, const double* grad,
                       double* ring, int32_t window, int64_t step, double lr,
                       double epsilon);
+
+/* ---- convergence diagnostics (functions.py:8-77) ------------------------ */
+/* Split-chain R-hat (compute_R_hat) of chains [n_chains][n_iters][P] on n_jobs
+ * iteration segments [job_start[j], job_start[j] + job_len[j]) (job_len even):
+ * var_hat_out (nullable) and rhat_out are [n_jobs][P]. */
+int vb_rhat(vb_ctx* ctx, const double* chains, int64_t n_chains, int64_t n_iters, int64_t P,
+            int64_t n_jobs, const int64_t* job_start, const int64_t* job_len,
+            double* var_hat_out, double* rhat_out);
+/* stochastic_iterate_averaging: out [n - start][cols] = cumulative means of
+ * x[start:, 0:cols] (row stride ld). */
+int vb_iterate_average(vb_ctx* ctx, const double* x, int64_t n, int64_t ld, int64_t cols,
+                       int64_t start, double* out);
 
 /* ---- log weights for bounds / PSIS (experiments.py:60-63) ------------ */
 int vb_log_weights(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,

@@ -3,6 +3,7 @@
 The product path has no CPU fallback: if the HIP library is missing, or no
 GPU is visible when a computation is requested, this module raises.
 """
+import atexit
 import ctypes
 import os
 import threading
@@ -17,6 +18,7 @@ FAMILY_MF_GAUSSIAN, FAMILY_MF_T, FAMILY_FR_T = 0, 1, 2
 TARGET_ISOGAUSS, TARGET_MIXTURE, TARGET_FUNNEL, TARGET_EIGHT_SCHOOLS_NCP = 0, 1, 2, 3
 TARGET_CORR_GAUSS = 4
 OBJ_KLVI, OBJ_CHIVI = 0, 1
+OPT_ADAGRAD, OPT_RMSPROP_IA, OPT_ADAM_IA = 0, 1, 2
 NOISE_HOST, NOISE_PHILOX = 0, 1
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
@@ -46,7 +48,7 @@ class Noise(ctypes.Structure):
 
 class AdagradConfig(ctypes.Structure):
     _fields_ = [('n_iters', ctypes.c_int64), ('window', ctypes.c_int32),
-                ('reserved', ctypes.c_int32), ('learning_rate', ctypes.c_double),
+                ('optimizer', ctypes.c_int32), ('learning_rate', ctypes.c_double),
                 ('learning_rate_end', ctypes.c_double), ('epsilon', ctypes.c_double)]
 
 
@@ -93,6 +95,10 @@ _SIGNATURES = {
     'vb_gpinv': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
                   c_double_p], ctypes.c_int),
     'vb_sumlogs': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, c_double_p], ctypes.c_int),
+    'vb_rhat': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                 ctypes.c_int64, c_int64_p, c_int64_p, c_double_p, c_double_p], ctypes.c_int),
+    'vb_iterate_average': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,
+                            ctypes.c_int64, ctypes.c_int64, c_double_p], ctypes.c_int),
 }
 
 _lib = None
@@ -150,11 +156,31 @@ class Context:
 
     def __del__(self):
         try:
-            if self.handle and _lib is not None:
+            if self.handle and _lib is not None and not _SHUTDOWN[0]:
                 _lib.vb_ctx_destroy(self.handle)
         except Exception:
             pass
         self.handle = None
+
+
+# At interpreter exit native objects are released by process teardown, not by
+# finalizers: a finalizer running after the HIP / rocBLAS runtimes' own static
+# destructors would call into torn-down libraries.
+_SHUTDOWN = [False]
+
+
+@atexit.register
+def _mark_shutdown():
+    for c in list(_ctx.values()):
+        try:
+            c.synchronize()
+        except Exception:
+            pass
+    _SHUTDOWN[0] = True
+
+
+def shutting_down():
+    return _SHUTDOWN[0]
 
 
 _ctx = {}

@@ -600,6 +600,7 @@ struct vb_run {
   long long nprob = 1, n_iters = 0, hist_start = 0, n_hist = 0, done = 0;
   double eps = 0.1;
   vbk::LrSched sched{};
+  int opt = 0;  // vb_optimizer_kind
   bool sep = false;
   int n_waves = 0;
   int max_chunk = 256;
@@ -626,7 +627,11 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
   if (!(cfg->learning_rate > 0)) return fail(VB_EINVAL, "learning rate must be positive");
   if (!std::isnan(cfg->learning_rate_end) && cfg->learning_rate <= cfg->learning_rate_end)
     return fail(VB_EINVAL, "initial learning rate must be greater than final learning rate");
-  if (cfg->window < 1 || cfg->window > 64) return fail(VB_EINVAL, "window must be in [1, 64]");
+  if (cfg->optimizer < VB_OPT_ADAGRAD || cfg->optimizer > VB_OPT_ADAM_IA)
+    return fail(VB_EINVAL, "unknown optimizer %d", cfg->optimizer);
+  const bool ia = cfg->optimizer != VB_OPT_ADAGRAD;
+  if (cfg->window < 1 || (!ia && cfg->window > 64))
+    return fail(VB_EINVAL, "window must be in [1, 64]");
   if (cfg->n_iters < 0) return fail(VB_EINVAL, "n_iters must be non-negative");
   if (n_problems < 1) return fail(VB_EINVAL, "n_problems must be positive");
   if (obj->n_samples < 1 || obj->n_samples > (1LL << 31))
@@ -639,6 +644,9 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
     return fail(VB_EUNSUPPORTED,
                 "device adagrad for objective %d / target %d needs D <= %d (got %d)", obj->kind,
                 tgt->kind, vbk::kBlockDMax, D);
+  if (sep && ia)
+    return fail(VB_EUNSUPPORTED, "the IA optimisers run on the block (D <= %d) and full-rank paths",
+                vbk::kBlockDMax);
   if (sep && n_problems != 1)
     return fail(VB_EUNSUPPORTED, "wide (D > %d) runs hold one problem per vb_run", vbk::kBlockDMax);
 
@@ -650,11 +658,17 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
   r->obj = obj->kind;
   r->alpha = obj->alpha;
   r->N = (int)obj->n_samples;
-  r->W = cfg->window;
+  r->W = ia ? 2 : cfg->window;  // IA: the ring holds the two moment vectors
+  r->opt = cfg->optimizer;
   r->nprob = n_problems;
   r->n_iters = cfg->n_iters;
-  r->hist_start = (3 * cfg->n_iters) / 4;
-  r->n_hist = cfg->n_iters - r->hist_start;
+  if (ia) {
+    r->n_hist = std::min<long long>(cfg->n_iters, 100LL * cfg->window);
+    r->hist_start = cfg->n_iters - r->n_hist;
+  } else {
+    r->hist_start = (3 * cfg->n_iters) / 4;
+    r->n_hist = cfg->n_iters - r->hist_start;
+  }
   r->eps = cfg->epsilon;
   r->sched = make_sched(cfg->n_iters, cfg->learning_rate, cfg->learning_rate_end);
   r->sep = sep;
@@ -744,12 +758,21 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
                                   noise->stream + (uint32_t)q * stride,
                                   (uint32_t)(noise->step + off),
                                   r->values.d() + q * r->n_iters + step, r->grad.d(), c->stream));
-        VB_HIP(vbk::launch_adagrad_update((long long)P, lam, r->grad.d(),
-                                          r->ring.d() + q * P * r->W, r->W, step, lr, r->eps,
-                                          c->stream));
-        if (step >= r->hist_start)
-          VB_HIP(hipMemcpyAsync(r->hist.d() + (q * r->n_hist + (step - r->hist_start)) * P, lam,
-                                sizeof(double) * P, hipMemcpyDeviceToDevice, c->stream));
+        double* hrow = step >= r->hist_start
+                           ? r->hist.d() + (q * r->n_hist + (step - r->hist_start)) * P
+                           : nullptr;
+        if (r->opt != VB_OPT_ADAGRAD) {
+          VB_HIP(vbk::launch_ia_update(r->opt, (long long)P, lam, r->grad.d(),
+                                       r->ring.d() + q * P * r->W, step, lr, r->eps, hrow,
+                                       c->stream));
+        } else {
+          VB_HIP(vbk::launch_adagrad_update((long long)P, lam, r->grad.d(),
+                                            r->ring.d() + q * P * r->W, r->W, step, lr, r->eps,
+                                            c->stream));
+          if (hrow)
+            VB_HIP(hipMemcpyAsync(hrow, lam, sizeof(double) * P, hipMemcpyDeviceToDevice,
+                                  c->stream));
+        }
       }
     }
   } else if (r->sep) {
@@ -794,6 +817,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
     a.n_steps = (int)n_steps;
     a.emit_grad = 0;
     a.chivi = r->obj == VB_OBJ_CHIVI;
+    a.opt = r->opt;
     a.step0 = r->done;
     a.hist_start = r->hist_start;
     a.n_iters = r->n_iters;
@@ -1089,6 +1113,51 @@ int vb_gpinv(vb_ctx* c, const double* p, int64_t n, double k, double sigma, doub
   VB_TRY(dp.stage(c, 0, p, (size_t)n));
   VB_TRY(dout.stage(c, 1, out, (size_t)n));
   VB_HIP(vbk::psis_gpinv(dp.d, n, k, sigma, dout.d, c->stream));
+  VB_TRY(dout.finish(c));
+  return sync(c);
+}
+
+int vb_rhat(vb_ctx* c, const double* chains, int64_t n_chains, int64_t n_iters, int64_t P,
+            int64_t n_jobs, const int64_t* job_start, const int64_t* job_len, double* var_hat_out,
+            double* rhat_out) {
+  VB_TRY(check_ctx(c));
+  if (!chains || !job_start || !job_len || !rhat_out) return fail(VB_EINVAL, "null argument");
+  if (n_chains < 1 || n_iters < 0 || P < 1 || n_jobs < 0) return fail(VB_EINVAL, "invalid sizes");
+  if (n_jobs == 0) return VB_OK;
+  for (int64_t j = 0; j < n_jobs; ++j) {
+    if (job_len[j] < 2 || job_len[j] % 2 || job_start[j] < 0 || job_start[j] + job_len[j] > n_iters)
+      return fail(VB_EINVAL, "R-hat segment %lld: [%lld, +%lld) invalid for %lld iterations",
+                  (long long)j, (long long)job_start[j], (long long)job_len[j], (long long)n_iters);
+  }
+  In dc;
+  VB_TRY(dc.stage(c, 0, chains, (size_t)n_chains * n_iters * P));
+  VB_TRY(c->slot[1].reserve(sizeof(long long) * 2 * n_jobs));
+  long long* dj = static_cast<long long*>(c->slot[1].p);
+  VB_HIP(hipMemcpyAsync(dj, job_start, sizeof(long long) * n_jobs, hipMemcpyHostToDevice, c->stream));
+  VB_HIP(hipMemcpyAsync(dj + n_jobs, job_len, sizeof(long long) * n_jobs, hipMemcpyHostToDevice,
+                        c->stream));
+  Out dv, dr;
+  VB_TRY(dv.stage(c, 2, var_hat_out, var_hat_out ? (size_t)n_jobs * P : 0));
+  VB_TRY(dr.stage(c, 3, rhat_out, (size_t)n_jobs * P));
+  VB_HIP(vbk::launch_rhat(dc.d, n_chains, n_iters, P, n_jobs, dj, dj + n_jobs, dv.d, dr.d,
+                          c->stream));
+  VB_TRY(dv.finish(c));
+  VB_TRY(dr.finish(c));
+  return sync(c);
+}
+
+int vb_iterate_average(vb_ctx* c, const double* x, int64_t n, int64_t ld, int64_t cols,
+                       int64_t start, double* out) {
+  VB_TRY(check_ctx(c));
+  if (!x || !out) return fail(VB_EINVAL, "null argument");
+  if (n - start <= 0)  // functions.py:70-71
+    return fail(VB_EINVAL, "Start of stationary distribution must be lower than number of iterates");
+  if (start < 0 || cols < 1 || ld < cols) return fail(VB_EINVAL, "invalid sizes");
+  In dx;
+  VB_TRY(dx.stage(c, 0, x, (size_t)(n - 1) * ld + cols));
+  Out dout;
+  VB_TRY(dout.stage(c, 1, out, (size_t)(n - start) * cols));
+  VB_HIP(vbk::launch_iterate_average(dx.d, n, ld, cols, start, dout.d, c->stream));
   VB_TRY(dout.finish(c));
   return sync(c);
 }

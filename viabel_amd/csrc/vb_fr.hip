@@ -407,6 +407,7 @@ struct FrWork {
   Buf info, part, ticket, res;
   double* host_res = nullptr;  // pinned copy of res
   int K = 0, K_prev = 0;       // Newton-Schulz iterations of the current / previous root
+  bool eig_pending = false;    // a dsyevd ran since the last fr_info
   double c = 0.0;              // its scaling (~1.25 lambda_max)
   // N x D / N
   Buf Z, X, G, s, logp, zz, r, rk;
@@ -485,6 +486,7 @@ int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st) {
                                        W->E.d(), D, W->w.d(), W->offd.d(),
                                        static_cast<rocblas_int*>(W->info.p));
   if (rs != rocblas_status_success) return vb_set_error(-2, "rocsolver_dsyevd failed (%d)", (int)rs);
+  W->eig_pending = true;
   hipLaunchKernelGGL(fr_logdet_kernel, dim3(1), dim3(1024), 0, st, D, W->w.d(), W->scal.d());
   FR_HIP(hipGetLastError());
   return 0;
@@ -790,7 +792,8 @@ int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, 
 
 int fr_info(FrWork* W, hipStream_t st) {
   int info = 0;
-  if (!W->info.p) return 0;
+  if (!W->info.p || !W->eig_pending) return 0;
+  W->eig_pending = false;
   FR_HIP(hipMemcpyAsync(&info, W->info.p, sizeof(int), hipMemcpyDeviceToHost, st));
   FR_HIP(hipStreamSynchronize(st));
   return info;

@@ -46,6 +46,8 @@ struct SepArgs {
 // Arguments of the block-per-problem kernel (any target, D <= kBlockDMax).
 struct BlockArgs {
   int D, N, W, P, n_steps, emit_grad, chivi;
+  int opt;  // 0 adagrad window (history: post-update, tail quarter); 1 RMSProp-IA, 2 Adam-IA
+            // (state in ring rows 0/1, history: pre-update, last n_hist iterations)
   long long step0, hist_start, n_iters, n_hist, rng_step0;
   double alpha;
   double t_scale, shape, t_const, df;  // t family constants
@@ -87,6 +89,20 @@ hipError_t launch_log_weights(int fam, int tgt, int D, long long m, const double
                               uint32_t step, double* lw, double* xs, hipStream_t s);
 hipError_t launch_adagrad_update(long long P, double* lam, const double* g, double* ring, int W,
                                  long long step, double lr, double eps, hipStream_t s);
+// RMSProp-IA / Adam-IA step (opt 1 / 2) on device state [2][P]; old_out (nullable)
+// receives the pre-update parameters.
+hipError_t launch_ia_update(int opt, long long P, double* lam, const double* g, double* state,
+                            long long step, double lr, double eps, double* old_out,
+                            hipStream_t s);
+// R-hat (functions.py:8-31) of chains [nc][n][P] (row stride P) over n_jobs
+// iteration segments [start, start + len) (len even): out [n_jobs][P] (var_hat
+// in var_out when non-null).
+hipError_t launch_rhat(const double* chains, long long nc, long long n, long long P,
+                       long long n_jobs, const long long* start, const long long* len,
+                       double* var_out, double* rhat_out, hipStream_t s);
+// cumulative means (functions.py:68-77) of x[start:, cols] with row stride ld
+hipError_t launch_iterate_average(const double* x, long long n, long long ld, long long cols,
+                                  long long start, double* out, hipStream_t s);
 
 // bounds
 hipError_t bounds_divergence(const double* lw, long long n, double alpha, int has_elbo,

@@ -433,6 +433,30 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
       }
       if (a.emit_grad) {
         a.grad[(long long)prob * P + p] = gp;
+      } else if (a.opt != 0) {
+        // RMSProp-IA (vb.py:436-453) / Adam-IA (vb.py:606-617): state in
+        // s_ring[0..P) (second moment) and s_ring[P..2P) (first moment); the
+        // history keeps the PRE-update parameters of the last n_hist iterations.
+        const double old = s_lam[p];
+        if (i >= a.hist_start) a.hist[((long long)prob * a.n_hist + (i - a.hist_start)) * P + p] = old;
+        const double g2 = __dmul_rn(gp, gp);
+        double nl;
+        if (a.opt == 1) {
+          const double sgs = i == 0 ? g2 : __dadd_rn(__dmul_rn(s_ring[p], 0.9), __dmul_rn(1.0 - 0.9, g2));
+          s_ring[p] = sgs;
+          nl = __dsub_rn(old, __dmul_rn(a.lr.at(i), gp) / sqrt(__dadd_rn(a.eps, sgs)));
+        } else {
+          const double v = i == 0 ? __dmul_rn(0.9, g2)
+                                  : __dadd_rn(__dmul_rn(s_ring[p], 0.999), __dmul_rn(1.0 - 0.999, g2));
+          const double m = i == 0 ? __dmul_rn(0.9, gp)
+                                  : __dadd_rn(__dmul_rn(s_ring[P + p], 0.9), __dmul_rn(1.0 - 0.9, gp));
+          s_ring[p] = v;
+          s_ring[P + p] = m;
+          const double mh = m / (1.0 - pow(0.9, (double)(i + 2)));
+          const double vh = v / (1.0 - pow(0.999, (double)(i + 2)));
+          nl = __dsub_rn(old, __dmul_rn(a.lr.at(i), mh) / sqrt(__dadd_rn(a.eps, vh)));
+        }
+        s_lam[p] = nl;
       } else {
         const int slot = (int)(i % W);
         s_ring[slot * P + p] = gp;
@@ -574,6 +598,33 @@ __global__ __launch_bounds__(256) void adagrad_update_kernel(long long P, double
     q = __dadd_rn(q, __dmul_rn(t, t));
   }
   lam[p] = __dsub_rn(lam[p], __dmul_rn(lr, g[p]) / sqrt(__dadd_rn(eps, q)));
+}
+
+__global__ __launch_bounds__(256) void ia_update_kernel(int opt, long long P, double* lam,
+                                                       const double* g, double* state,
+                                                       long long i, double lr, double eps,
+                                                       double* old_out) {
+  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const double old = lam[p], gp = g[p], g2 = __dmul_rn(gp, gp);
+  if (old_out) old_out[p] = old;
+  double nl;
+  if (opt == 1) {
+    const double sgs = i == 0 ? g2 : __dadd_rn(__dmul_rn(state[p], 0.9), __dmul_rn(1.0 - 0.9, g2));
+    state[p] = sgs;
+    nl = __dsub_rn(old, __dmul_rn(lr, gp) / sqrt(__dadd_rn(eps, sgs)));
+  } else {
+    const double v = i == 0 ? __dmul_rn(0.9, g2)
+                            : __dadd_rn(__dmul_rn(state[p], 0.999), __dmul_rn(1.0 - 0.999, g2));
+    const double m = i == 0 ? __dmul_rn(0.9, gp)
+                            : __dadd_rn(__dmul_rn(state[P + p], 0.9), __dmul_rn(1.0 - 0.9, gp));
+    state[p] = v;
+    state[P + p] = m;
+    const double mh = m / (1.0 - pow(0.9, (double)(i + 2)));
+    const double vh = v / (1.0 - pow(0.999, (double)(i + 2)));
+    nl = __dsub_rn(old, __dmul_rn(lr, mh) / sqrt(__dadd_rn(eps, vh)));
+  }
+  lam[p] = nl;
 }
 
 // log weights lw[r] = log p(x_r) - log q(x_r; lam) for x_r ~ q   (experiments.py:60-63)
@@ -917,6 +968,14 @@ hipError_t launch_adagrad_update(long long P, double* lam, const double* g, doub
                                  long long step, double lr, double eps, hipStream_t s) {
   hipLaunchKernelGGL(adagrad_update_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P,
                      lam, g, ring, W, step, lr, eps);
+  return hipGetLastError();
+}
+
+hipError_t launch_ia_update(int opt, long long P, double* lam, const double* g, double* state,
+                            long long step, double lr, double eps, double* old_out,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(ia_update_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, opt, P,
+                     lam, g, state, step, lr, eps, old_out);
   return hipGetLastError();
 }
 

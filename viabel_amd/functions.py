@@ -1,0 +1,101 @@
+"""Convergence diagnostics of viabel/functions.py:8-77 on the device.
+
+  compute_R_hat                  functions.py:8-31
+  compute_R_hat_adaptive_numpy   functions.py:44-52
+  compute_R_hat_halfway          functions.py:54-65
+  stochastic_iterate_averaging   functions.py:68-77
+
+Chains are [n_chains, n_iters, K] float64 (host or torch device tensors).  Every
+R-hat of a call is one segment of a single batched kernel launch (vb_rhat);
+the segment bookkeeping below mirrors the reference's slicing, including its
+odd-length quirk (two iterations dropped, then the reshape fails).
+"""
+import numpy as np
+
+from . import _native as nat
+
+__all__ = ['compute_R_hat', 'compute_R_hat_adaptive_numpy', 'compute_R_hat_halfway',
+           'stochastic_iterate_averaging']
+
+
+def _chains(chains):
+    c = nat.as_f64(chains)
+    if c.ndim != 3:
+        raise ValueError('chains must have shape (n_chains, n_iters, K)')
+    return c
+
+
+def _segment(n_chains, n_iters, K, warmup):
+    """(start, length) of compute_R_hat(chains[:, warmup:, :]) (functions.py:12-21)."""
+    start = min(max(int(warmup), 0), n_iters) if warmup >= 0 else max(n_iters + int(warmup), 0)
+    n = n_iters - start
+    if n % 2 == 1:
+        # the reference drops two iterations here, then its reshape cannot succeed
+        raise ValueError('cannot reshape array of size %d into shape (%d,%d,%d)'
+                         % (n_chains * (n - 2) * K, 2 * n_chains, (n - 1) // 2, K))
+    return start, n
+
+
+def _rhat_batch(c, segs, return_var=False):
+    n_chains, n_iters, K = c.shape
+    starts = np.array([s for s, _ in segs], dtype=np.int64)
+    lens = np.array([n for _, n in segs], dtype=np.int64)
+    out = np.empty((len(segs), K))
+    var = np.empty((len(segs), K)) if return_var else None
+    nat.check(nat.lib().vb_rhat(nat.context().handle, nat.dptr(c), n_chains, n_iters, K, len(segs),
+                                nat.i64ptr(starts), nat.i64ptr(lens), nat.dptr(var),
+                                nat.dptr(out)))
+    return var, out
+
+
+def compute_R_hat(chains, warmup=500):
+    """Split-chain R-hat; returns (var_hat, R_hat), each of shape (K,)."""
+    c = _chains(chains)
+    nc, n, K = c.shape
+    seg = _segment(nc, n, K, warmup)
+    if seg[1] < 2:
+        raise ValueError('R-hat needs at least two iterations after warm-up')
+    var, out = _rhat_batch(c, [seg], return_var=True)
+    return var[0], out[0]
+
+
+def compute_R_hat_adaptive_numpy(chains, window_size=100):
+    """R-hat of consecutive windows of `window_size` iterations: (n_windows, K)."""
+    c = _chains(chains)
+    nc, n, K = c.shape
+    n_windows = n // window_size
+    if n_windows * window_size != n:
+        raise ValueError('cannot reshape array of size %d into shape (%d,%d,%d,newaxis)'
+                         % (c.size, nc, n_windows, window_size))
+    if window_size % 2 == 1:
+        _segment(nc, window_size, K, 0)
+    return _rhat_batch(c, [(i * window_size, window_size) for i in range(n_windows)])[1]
+
+
+def compute_R_hat_halfway(chains, interval=100, start=1000):
+    """R-hat of chains[:, :start + (i+1) interval] after discarding its first half."""
+    c = _chains(chains)
+    nc, n, K = c.shape
+    segs = []
+    for i in range(n // interval):
+        sub_n = min(start + (i + 1) * interval, n)
+        segs.append(_segment(nc, sub_n, K, sub_n // 2))
+    if not segs:
+        return np.zeros((0,))
+    return _rhat_batch(c, segs)[1]
+
+
+def stochastic_iterate_averaging(estimate, start):
+    """Cumulative means of estimate[start:] (rows = iterations); returns
+    (estimate_iters, estimate_mean)."""
+    x = nat.as_f64(estimate)
+    if x.ndim == 1:
+        x = x[:, None]
+    N, cols = x.shape
+    start = int(start)
+    if N - start <= 0:
+        raise ValueError('Start of stationary distribution must be lower than number of iterates')
+    out = np.empty((N - start, cols))
+    nat.check(nat.lib().vb_iterate_average(nat.context().handle, nat.dptr(x), N, cols, cols, start,
+                                           nat.dptr(out)))
+    return out, out[-1]

@@ -10,6 +10,8 @@ error messages) for the hot path:
   black_box_chivi                         vb.py:248-266
   learning_rate_schedule                  vb.py:324-342
   adagrad_optimize                        vb.py:345-389
+  rmsprop_IA_optimize_with_rhat           vb.py:392-553
+  adam_IA_optimize_with_rhat              vb.py:556-712
 
 Computation runs in libviabel_amd.so (HIP, gfx950).  Two noise sources:
 
@@ -43,6 +45,8 @@ __all__ = [
     'black_box_chivi',
     'learning_rate_schedule',
     'adagrad_optimize',
+    'rmsprop_IA_optimize_with_rhat',
+    'adam_IA_optimize_with_rhat',
     'set_default_rng',
 ]
 
@@ -348,14 +352,16 @@ class DeviceRun:
     """Device-resident adagrad state for one or more problems (vb_run)."""
 
     def __init__(self, objective, n_iters, init_params, window=10, learning_rate=.01,
-                 epsilon=.1, learning_rate_end=None):
+                 epsilon=.1, learning_rate_end=None, optimizer=nat.OPT_ADAGRAD):
         init = nat.as_f64(np.atleast_2d(init_params))
+        self.optimizer = optimizer
+        self.window = int(window)
         self.obj = objective
         self.n_iters = int(n_iters)
         self.n_problems = init.shape[0]
         self.P = init.shape[1]
         f, t, o = objective._structs()
-        cfg = nat.AdagradConfig(self.n_iters, int(window), 0, float(learning_rate),
+        cfg = nat.AdagradConfig(self.n_iters, int(window), int(optimizer), float(learning_rate),
                                 nat.NAN if learning_rate_end is None else float(learning_rate_end),
                                 float(epsilon))
         import ctypes
@@ -380,7 +386,10 @@ class DeviceRun:
         self.done += n_steps
 
     def result(self):
-        n_hist = self.n_iters - 3 * self.n_iters // 4
+        if self.optimizer == nat.OPT_ADAGRAD:
+            n_hist = self.n_iters - 3 * self.n_iters // 4
+        else:
+            n_hist = min(self.n_iters, 100 * self.window)
         lam = np.empty((self.n_problems, self.P))
         hist = np.empty((self.n_problems, n_hist, self.P))
         vals = np.empty((self.n_problems, self.n_iters))
@@ -394,7 +403,7 @@ class DeviceRun:
 
     def __del__(self):
         try:
-            if getattr(self, 'handle', None) and nat._lib is not None:
+            if getattr(self, 'handle', None) and nat._lib is not None and not nat.shutting_down():
                 nat._lib.vb_run_destroy(self.handle)
         except Exception:
             pass
@@ -470,3 +479,111 @@ def adagrad_optimize(n_iters, objective_and_grad, init_param,
                                learning_rate, epsilon, learning_rate_end)
     return _foreign_adagrad(int(n_iters), objective_and_grad, init_param, has_log_norm,
                             int(window), learning_rate, epsilon, learning_rate_end)
+
+
+def _ia_optimize(opt, n_iters, objective_and_grad, init_param, K, has_log_norm, window,
+                 learning_rate, epsilon, rhat_window, n_optimisers, r_mean_threshold,
+                 r_sigma_threshold, tail_avg_iters, learning_rate_end, perturb_scale):
+    from . import functions
+    if not isinstance(objective_and_grad, NativeObjective):
+        raise NotImplementedError('the device IA optimisers need a native objective '
+                                  '(viabel_amd.vb.black_box_klvi / black_box_chivi)')
+    if has_log_norm:
+        raise ValueError('not enough values to unpack (expected 3, got 2)')
+    if learning_rate <= 0:
+        raise ValueError('learning rate must be positive')
+    if learning_rate_end is not None and learning_rate <= learning_rate_end:
+        raise ValueError('initial learning rate must be greater than final learning rate')
+    obj = objective_and_grad
+    fam = obj.family
+    init_param = np.asarray(init_param, dtype=float)
+    n_iters = int(n_iters)
+    inits = []
+    for o in range(n_optimisers):
+        np.random.seed(seed=o)                                       # vb.py:418 / 584
+        if o == 0:
+            inits.append(init_param.copy())
+        else:
+            inits.append(init_param + np.random.randn(len(init_param)) * (o + 1) * perturb_scale)
+        if fam.rng == 'numpy':
+            # chains run one after another like the reference: the objective's
+            # draws (family stream / global-RNG CHIVI seeds) follow seed(o)
+            run = DeviceRun(obj, n_iters, inits[o][None, :], window, learning_rate, epsilon,
+                            learning_rate_end, optimizer=opt)
+            per_step = obj.n_samples * (fam.dim + 1)
+            chunk = max(1, min(n_iters, _HOST_CHUNK_ELEMS // max(per_step, 1)))
+            done = 0
+            while done < n_iters:
+                cs = min(chunk, n_iters - done)
+                run.advance_host(np.stack([obj._eps_one_call() for _ in range(cs)])[None])
+                done += cs
+            lam, hist, vals, _ = run.result()
+            if o == 0:
+                lams, hists, valss = [], [], []
+            lams.append(lam[0])
+            hists.append(hist[0])
+            valss.append(vals[0])
+    if fam.rng == 'philox':
+        # independent chains: one launch chain, one Philox stream per chain
+        run = DeviceRun(obj, n_iters, np.stack(inits), window, learning_rate, epsilon,
+                        learning_rate_end, optimizer=opt)
+        run.advance_philox(n_iters, fam.seed, fam.stream, fam.step, stream_stride=1)
+        fam.step += n_iters
+        lam, hist, vals, _ = run.result()
+        lams, hists, valss = list(lam), list(hist), list(vals)
+    chains = np.stack(hists, axis=0)
+    rhats = functions.compute_R_hat_adaptive_numpy(chains, window_size=rhat_window)
+    rhats_halfway = functions.compute_R_hat_halfway(chains, interval=100, start=200)
+    rm, rs = rhats[:, :K], rhats[:, K:]
+    start_m = start_s = n_iters - tail_avg_iters
+    for ee in range(rm.shape[0] - 1):
+        if (rm[ee] < r_mean_threshold).all() and (rm[ee + 1] < r_mean_threshold).all():
+            start_m = ee * rhat_window
+            break
+    for ee in range(rs.shape[0] - 1):
+        if (rs[ee] < r_sigma_threshold).all() and (rs[ee + 1] < r_sigma_threshold).all():
+            start_s = ee * rhat_window
+            break
+    means, sigmas = [], []
+    for o in range(n_optimisers):
+        means.append(functions.stochastic_iterate_averaging(chains[o, :, :K], start_m)[0])
+        sigmas.append(functions.stochastic_iterate_averaging(chains[o, :, K:], start_s)[0])
+    log = {'start_avg_mean_iters': start_m, 'start_avg_sigma_iters': start_s,
+           'r_hat_mean': rm, 'r_hat_sigma': rs,
+           'r_hat_mean_halfway': rhats_halfway[:, :K], 'r_hat_sigma_halfway': rhats_halfway[:, K:]}
+    values = np.concatenate(valss)
+    return (lams[-1], chains, means, sigmas, values, np.zeros(len(values)), log)
+
+
+def rmsprop_IA_optimize_with_rhat(n_iters, objective_and_grad, init_param, K,
+                                  has_log_norm=False, window=500, learning_rate=.01,
+                                  epsilon=.000001, rhat_window=500, averaging=True,
+                                  n_optimisers=1, r_mean_threshold=1.15, r_sigma_threshold=1.20,
+                                  tail_avg_iters=2000, avg_grad_norm=False,
+                                  learning_rate_end=None):
+    """vb.py:392-553: RMSProp (decay .9) chains, windowed / halfway R-hat, and
+    iterate averaging from the first pair of windows whose R-hat is below the
+    thresholds.  Returns (final param of the last chain, history chains
+    [n_optimisers, n_hist, P], averaged means per chain, averaged sigmas per
+    chain, values, log norms, log dict).  The updates run on the device
+    (vb_run, optimizer RMSPROP_IA); R-hat and averaging too (vb_rhat,
+    vb_iterate_average)."""
+    if avg_grad_norm:
+        raise NotImplementedError('avg_grad_norm=True is not supported by the device optimiser')
+    return _ia_optimize(nat.OPT_RMSPROP_IA, n_iters, objective_and_grad, init_param, K,
+                        has_log_norm, window, learning_rate, epsilon, rhat_window, n_optimisers,
+                        r_mean_threshold, r_sigma_threshold, tail_avg_iters, learning_rate_end,
+                        0.5)
+
+
+def adam_IA_optimize_with_rhat(n_iters, objective_and_grad, init_param, K,
+                               has_log_norm=False, window=500, learning_rate=.01,
+                               epsilon=.000001, rhat_window=500, averaging=True, n_optimisers=1,
+                               r_mean_threshold=1.15, r_sigma_threshold=1.20,
+                               tail_avg_iters=2000, learning_rate_end=None):
+    """vb.py:556-712: Adam (beta1 .9, beta2 .999, bias correction with i + 2)
+    chains; same diagnostics and return value as rmsprop_IA_optimize_with_rhat."""
+    return _ia_optimize(nat.OPT_ADAM_IA, n_iters, objective_and_grad, init_param, K,
+                        has_log_norm, window, learning_rate, epsilon, rhat_window, n_optimisers,
+                        r_mean_threshold, r_sigma_threshold, tail_avg_iters, learning_rate_end,
+                        0.2)
