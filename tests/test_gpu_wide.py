@@ -1,0 +1,126 @@
+"""GPU parity of the materialised mean-field path (D > 16 with CHIVI or a
+non-separable target, and the IA optimisers at D > 16) against the oracle on
+identical numpy-stream draws.  Tolerances as tests/test_gpu_vb.py: single
+calls 1e-10 relative, trajectories 1e-7."""
+import numpy as np
+import pytest
+
+from tests.conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason='needs an MI355X')]
+
+FAMS = [('gauss', None), ('t', 40.0)]
+
+
+def _mods():
+    from viabel_amd import vb, targets
+    from oracle import vb_oracle
+    return vb, targets, vb_oracle
+
+
+def _family(vb, kind, df, D):
+    if kind == 'gauss':
+        return vb.mean_field_gaussian_variational_family(D, rng='numpy')
+    return vb.mean_field_t_variational_family(D, df, rng='numpy')
+
+
+def _target(targets, name, D):
+    return {'isogauss': targets.isogauss, 'mixture': targets.mixture,
+            'funnel': targets.funnel}[name](D)
+
+
+def _lam(D, seed):
+    rs = np.random.RandomState(seed)
+    return np.concatenate([rs.randn(D) * 0.3, rs.randn(D) * 0.2 - 0.5])
+
+
+def _close(a, b, rtol):
+    a, b = np.asarray(a), np.asarray(b)
+    scale = max(1.0, float(np.max(np.abs(b))))
+    err = float(np.max(np.abs(a - b))) / scale
+    assert err <= rtol, 'max scaled error %.3e > %.1e' % (err, rtol)
+
+
+@pytest.mark.parametrize('kind,df', FAMS)
+@pytest.mark.parametrize('target,D', [('isogauss', 17), ('mixture', 300), ('funnel', 40),
+                                      ('funnel', 1000)])
+@pytest.mark.parametrize('alpha', [2.0, 1.5])
+def test_chivi_wide_numpy_stream(kind, df, target, D, alpha):
+    vb, targets, vo = _mods()
+    fam = _family(vb, kind, df, D)
+    ofam = vo.Family(kind, D, df)
+    obj = vb.black_box_chivi(alpha, fam, _target(targets, target, D), 64)
+    for call in range(2):
+        lam = _lam(D, call)
+        np.random.seed(10 + call)
+        v, g = obj(lam)
+        np.random.seed(10 + call)
+        ov, og = vo.chivi_value_grad(ofam, target, lam, 64, alpha)
+        assert abs(v - ov) <= 1e-10 * max(1.0, abs(ov))
+        _close(g, og, 1e-10)
+
+
+@pytest.mark.parametrize('kind,df', FAMS)
+@pytest.mark.parametrize('D', [17, 500])
+def test_klvi_funnel_wide(kind, df, D):
+    vb, targets, vo = _mods()
+    fam = _family(vb, kind, df, D)
+    ofam = vo.Family(kind, D, df)
+    obj = vb.black_box_klvi(fam, targets.funnel(D), 100)
+    lam = _lam(D, 5)
+    v, g = obj(lam)
+    ov, og = vo.klvi_value_grad(ofam, 'funnel', lam, 100)
+    assert abs(v - ov) <= 1e-10 * max(1.0, abs(ov))
+    _close(g, og, 1e-10)
+
+
+@pytest.mark.parametrize('objective,target', [('chivi', 'mixture'), ('klvi', 'funnel')])
+def test_adagrad_wide_numpy_stream(objective, target):
+    vb, targets, vo = _mods()
+    D, N, n_iters = 33, 40, 120
+    fam = _family(vb, 'gauss', None, D)
+    ofam = vo.Family('gauss', D)
+    tgt = _target(targets, target, D)
+    lam0 = _lam(D, 1)
+    if objective == 'chivi':
+        obj = vb.black_box_chivi(2.0, fam, tgt, N)
+        ofn = lambda lam: vo.chivi_value_grad(ofam, target, lam, N, 2.0)
+    else:
+        obj = vb.black_box_klvi(fam, tgt, N)
+        ofn = lambda lam: vo.klvi_value_grad(ofam, target, lam, N)
+    np.random.seed(4)
+    sm, hist, vals, _ = vb.adagrad_optimize(n_iters, obj, lam0, learning_rate=.02)
+    np.random.seed(4)
+    osm, ohist, ovals = vo.adagrad_optimize(n_iters, ofn, lam0, learning_rate=.02)[:3]
+    _close(vals, ovals, 1e-7)
+    _close(hist, ohist, 1e-7)
+
+
+@pytest.mark.parametrize('kind,df', FAMS)
+def test_log_weights_funnel_wide(kind, df):
+    vb, targets, vo = _mods()
+    from viabel_amd import experiments
+    D = 30
+    fam = _family(vb, kind, df, D)
+    ofam = vo.Family(kind, D, df)
+    lam = _lam(D, 2)
+    xs, lw = experiments.log_weights(targets.funnel(D), fam, lam, 2000)
+    ox, olw = vo.log_weights(ofam, 'funnel', lam, 2000)
+    _close(xs, ox, 1e-12)
+    _close(lw, olw, 1e-10)
+
+
+def test_rmsprop_ia_wide():
+    vb, targets, vo = _mods()
+    from oracle import functions_oracle as fo
+    D, N = 20, 30
+    fam = _family(vb, 'gauss', None, D)
+    ofam = vo.Family('gauss', D)
+    obj = vb.black_box_klvi(fam, targets.isogauss(D), N)
+    ofn = lambda lam: vo.klvi_value_grad(ofam, 'isogauss', lam, N)
+    kw = dict(window=500, rhat_window=100, n_optimisers=2, tail_avg_iters=100)
+    res = vb.rmsprop_IA_optimize_with_rhat(400, obj, np.zeros(2 * D), D, **kw)
+    ores = fo.rmsprop_IA_optimize_with_rhat(400, ofn, np.zeros(2 * D), D, **kw)
+    _close(res[1], ores[1], 1e-7)
+    _close(res[4], ores[4], 1e-7)

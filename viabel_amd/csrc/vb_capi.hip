@@ -212,8 +212,7 @@ int check_target(const vb_target* t, int D) {
   if (t->dim != D)
     return fail(VB_EINVAL, "target dimension %lld does not match family dimension %d",
                 (long long)t->dim, D);
-  if (t->kind == VB_TARGET_FUNNEL && (D < 2 || D > vbk::kBlockDMax))
-    return fail(VB_EUNSUPPORTED, "funnel target needs 2 <= D <= %d", vbk::kBlockDMax);
+  if (t->kind == VB_TARGET_FUNNEL && D < 2) return fail(VB_EINVAL, "funnel target needs D >= 2");
   if (t->kind == VB_TARGET_EIGHT_SCHOOLS_NCP && D != 10)
     return fail(VB_EINVAL, "eight_schools_ncp target has dimension 10, got %d", D);
   return VB_OK;
@@ -263,6 +262,21 @@ vbk::FrSpec fr_spec(const FamInfo& fi, const vb_target* tgt, const vb_objective*
   f.alpha = obj->alpha;
   f.tparams = tparams;
   f.tconst = tconst;
+  return f;
+}
+
+vbk::MfSpec mf_spec(const FamInfo& fi, const vb_target* tgt, const vb_objective* obj) {
+  vbk::MfSpec f{};
+  f.fam = fi.kind;
+  f.D = fi.D;
+  f.N = obj ? (int)obj->n_samples : 0;
+  f.tgt = tgt->kind;
+  f.chivi = obj && obj->kind == VB_OBJ_CHIVI;
+  f.alpha = obj ? obj->alpha : 2.0;
+  f.t_scale = fi.t_scale;
+  f.shape = fi.shape;
+  f.df = fi.df;
+  f.t_const = fi.t_const;
   return f;
 }
 
@@ -578,10 +592,12 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
     a.stream_stride = 1;
     VB_HIP(vbk::launch_block(fi.kind, tgt->kind, host, a, 1, c->stream));
   } else {
-    return fail(VB_EUNSUPPORTED,
-                "objective %d with target %d at D=%d is not implemented on the device "
-                "(non-separable targets and CHIVI need D <= %d)",
-                obj->kind, tgt->kind, D, vbk::kBlockDMax);
+    // CHIVI or a non-separable target at D > kBlockDMax: materialised path
+    vbk::FrWork* W;
+    VB_TRY(fr_work(c, &W));
+    VB_TRY(vbk::mf_wide_value_grad(W, mf_spec(fi, tgt, obj), c->slot[3].d(), host ? dn.d : nullptr,
+                                   k0, k1, noise->stream, (uint32_t)noise->step, dval, dg.d,
+                                   c->stream));
   }
   VB_HIP(hipMemcpyAsync(value, dval, sizeof(double), hipMemcpyDeviceToHost, c->stream));
   VB_TRY(dg.finish(c));
@@ -605,9 +621,10 @@ struct vb_run {
   int n_waves = 0;
   int max_chunk = 256;
   DevBuf lam, ring, hist, values, vpart, noise, smooth;
-  // full-rank family: one fr_value_grad + adagrad update per step
-  bool fr = false;
+  // full-rank family / wide mean-field: one value_grad + update per step
+  bool fr = false, wide = false;
   vbk::FrSpec spec{};
+  vbk::MfSpec mspec{};
   DevBuf tparams, grad;
 };
 
@@ -640,13 +657,11 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
   const bool fr = fi.kind == VB_FAMILY_FR_T;
   const bool sep = !fr && vbk::target_separable(tgt->kind) && obj->kind == VB_OBJ_KLVI &&
                    (D > vbk::kBlockDMax);
-  if (!fr && !sep && D > vbk::kBlockDMax)
-    return fail(VB_EUNSUPPORTED,
-                "device adagrad for objective %d / target %d needs D <= %d (got %d)", obj->kind,
-                tgt->kind, vbk::kBlockDMax, D);
-  if (sep && ia)
-    return fail(VB_EUNSUPPORTED, "the IA optimisers run on the block (D <= %d) and full-rank paths",
-                vbk::kBlockDMax);
+  // D > kBlockDMax without the fused kernel (CHIVI, non-separable targets, IA
+  // optimisers): the materialised mean-field path, one problem per run
+  const bool wide = !fr && D > vbk::kBlockDMax && (!sep || ia);
+  if (wide && n_problems != 1)
+    return fail(VB_EUNSUPPORTED, "wide (D > %d) runs hold one problem per vb_run", vbk::kBlockDMax);
   if (sep && n_problems != 1)
     return fail(VB_EUNSUPPORTED, "wide (D > %d) runs hold one problem per vb_run", vbk::kBlockDMax);
 
@@ -671,7 +686,8 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
   }
   r->eps = cfg->epsilon;
   r->sched = make_sched(cfg->n_iters, cfg->learning_rate, cfg->learning_rate_end);
-  r->sep = sep;
+  r->sep = sep && !wide;
+  r->wide = wide;
   r->n_waves = (D + 1) / 2;
   const size_t P = fi.P;
   auto bail = [&](int rc) {
@@ -679,6 +695,10 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
     return rc;
   };
   int rc;
+  if (wide) {
+    if ((rc = r->grad.reserve(sizeof(double) * P)) != VB_OK) return bail(rc);
+    r->mspec = mf_spec(fi, tgt, obj);
+  }
   if (fr) {
     r->fr = true;
     const double* tp;
@@ -743,7 +763,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
   uint32_t k0, k1;
   key_of(noise->seed, &k0, &k1);
 
-  if (r->fr) {
+  if (r->fr || r->wide) {
     vbk::FrWork* W;
     VB_TRY(fr_work(c, &W));
     const uint32_t stride = noise->stream_stride ? noise->stream_stride : 1;
@@ -754,10 +774,17 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
         double* lam = r->lam.d() + q * P;
         const double* eps =
             host ? noise_base + ((size_t)q * n_steps + off) * per_step : nullptr;
-        VB_TRY(vbk::fr_value_grad(W, r->spec, lam, eps, k0, k1,
-                                  noise->stream + (uint32_t)q * stride,
-                                  (uint32_t)(noise->step + off),
-                                  r->values.d() + q * r->n_iters + step, r->grad.d(), c->stream));
+        if (r->fr)
+          VB_TRY(vbk::fr_value_grad(W, r->spec, lam, eps, k0, k1,
+                                    noise->stream + (uint32_t)q * stride,
+                                    (uint32_t)(noise->step + off),
+                                    r->values.d() + q * r->n_iters + step, r->grad.d(), c->stream));
+        else
+          VB_TRY(vbk::mf_wide_value_grad(W, r->mspec, lam, eps, k0, k1,
+                                         noise->stream + (uint32_t)q * stride,
+                                         (uint32_t)(noise->step + off),
+                                         r->values.d() + q * r->n_iters + step, r->grad.d(),
+                                         c->stream));
         double* hrow = step >= r->hist_start
                            ? r->hist.d() + (q * r->n_hist + (step - r->hist_start)) * P
                            : nullptr;
@@ -843,6 +870,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
     VB_HIP(vbk::launch_block(r->fi.kind, r->tgt, host, a, (int)r->nprob, c->stream));
   }
   r->done += n_steps;
+  if (r->wide) return sync(c);
   if (r->fr) {
     VB_TRY(sync(c));
     vbk::FrWork* W;
@@ -954,8 +982,27 @@ int vb_log_weights(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const 
     VB_TRY(dxs.finish(c));
     return sync(c);
   }
-  if (!vbk::target_separable(tgt->kind) && fi.D > vbk::kBlockDMax)
-    return fail(VB_EUNSUPPORTED, "log weights for target %d need D <= %d", tgt->kind, vbk::kBlockDMax);
+  if (!vbk::target_separable(tgt->kind) && fi.D > vbk::kBlockDMax) {
+    const bool host = noise->kind == VB_NOISE_HOST;
+    if (host && !noise->eps) return fail(VB_EINVAL, "host noise requires eps");
+    if (m == 0) return VB_OK;
+    In dl, dn;
+    Out dlw, dxs;
+    VB_TRY(dl.stage(c, 0, lam, fi.P));
+    if (host) VB_TRY(dn.stage(c, 1, noise->eps, (size_t)m * fi.D));
+    VB_TRY(dlw.stage(c, 2, lw_out, (size_t)m));
+    VB_TRY(dxs.stage(c, 3, samples_out, samples_out ? (size_t)m * fi.D : 0));
+    uint32_t k0, k1;
+    key_of(noise->seed, &k0, &k1);
+    vbk::FrWork* W;
+    VB_TRY(fr_work(c, &W));
+    VB_TRY(vbk::mf_wide_log_weights(W, mf_spec(fi, tgt, nullptr), dl.d, m, host ? dn.d : nullptr,
+                                    k0, k1, noise->stream, (uint32_t)noise->step, dlw.d, dxs.d,
+                                    c->stream));
+    VB_TRY(dlw.finish(c));
+    VB_TRY(dxs.finish(c));
+    return sync(c);
+  }
   const bool host = noise->kind == VB_NOISE_HOST;
   if (host && !noise->eps) return fail(VB_EINVAL, "host noise requires eps");
   In dl, dn;

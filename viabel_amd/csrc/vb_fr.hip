@@ -777,6 +777,134 @@ hipError_t launch_fr_lw(int D, long long m, double df, double t_const, const dou
   return hipGetLastError();
 }
 
+// ---- mean-field families at any D with any objective / target ---------------
+// The materialised path: x [N][D] is written once, the target evaluated by rows,
+// per-sample weights formed, and the gradient reduced column by column.  Used
+// where the fused column-pair kernel does not apply (CHIVI, whose weights couple
+// all coordinates of a sample, and non-separable targets) for D > kBlockDMax.
+namespace {
+
+// KLVI: value = -(entropy + mean logp), r_n = -1/N, rsum = -1 (the entropy's
+// d/dlog sigma).  CHIVI: lw = logp - logq, w = exp(lw - max)^alpha,
+// value = log(mean w)/alpha + max, r_n = alpha w_n / N, rsum = sum_n r_n.
+__global__ __launch_bounds__(1024) void mfw_weights_kernel(int N, int D, int chivi, double alpha,
+                                                           double c0, const double* lam,
+                                                           const double* logp,
+                                                           const double* logq, double* r,
+                                                           double* scal, double* value) {
+  __shared__ double red[16];
+  if (!chivi) {
+    double a = 0.0, e = 0.0;
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+      a += logp[k];
+      r[k] = -1.0 / N;
+    }
+    for (int d = threadIdx.x; d < D; d += blockDim.x) e += lam[D + d];
+    a = block_sum(a, red);
+    e = block_sum(e, red);
+    if (threadIdx.x == 0) {
+      *value = -((c0 + e) + a / N);
+      scal[1] = -1.0;
+    }
+    return;
+  }
+  double mx = -INFINITY;
+  for (int k = threadIdx.x; k < N; k += blockDim.x) {
+    const double lw = logp[k] - logq[k];
+    r[k] = lw;
+    mx = fmax(mx, lw);
+  }
+  mx = block_max(mx, red);
+  double sw = 0.0;
+  for (int k = threadIdx.x; k < N; k += blockDim.x) {
+    const double w = pow(exp(r[k] - mx), alpha);
+    sw += w;
+    r[k] = alpha * w / N;
+  }
+  sw = block_sum(sw, red);
+  if (threadIdx.x == 0) {
+    *value = log(sw / N) / alpha + mx;
+    scal[1] = alpha * sw / N;
+  }
+}
+
+// grad_mu_j = sum_n r_n G_nj;  grad_logsigma_j = sigma_j sum_n r_n G_nj z_nj + rsum,
+// z = (x - mu) / sigma (the standardized draw).  Four waves split the rows.
+__global__ __launch_bounds__(256) void mfw_grad_kernel(int N, int D, const double* lam,
+                                                       const double* X, const double* G,
+                                                       const double* r, const double* scal,
+                                                       double* grad) {
+  __shared__ double pa[4][64], pb[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  double a = 0.0, b = 0.0;
+  if (j < D) {
+    const double mu = lam[j], sg = exp(lam[D + j]);
+    for (int n = wv; n < N; n += 4) {
+      const double g = r[n] * G[(long long)n * D + j];
+      a += g;
+      b += g * ((X[(long long)n * D + j] - mu) / sg);
+    }
+  }
+  pa[wv][lane] = a;
+  pb[wv][lane] = b;
+  __syncthreads();
+  if (wv == 0 && j < D) {
+    const double sa = (pa[0][lane] + pa[1][lane]) + (pa[2][lane] + pa[3][lane]);
+    const double sb = (pb[0][lane] + pb[1][lane]) + (pb[2][lane] + pb[3][lane]);
+    grad[j] = sa;
+    grad[D + j] = exp(lam[D + j]) * sb + scal[1];
+  }
+}
+
+}  // namespace
+
+int mf_wide_value_grad(FrWork* W, const MfSpec& f, const double* lam, const double* host_eps,
+                       uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
+                       double* grad, hipStream_t st) {
+  const int D = f.D, N = f.N;
+  if (int rc = reserve_d(W, 1, st)) return rc;
+  if (int rc = reserve_n(W, D, N)) return rc;
+  FR_HIP(launch_sample(f.fam, D, N, lam, f.t_scale, f.shape, host_eps, k0, k1, stream, step,
+                       W->X.d(), st));
+  if (f.tgt == kTargetCorrGauss)
+    return vb_set_error(-4, "corr_gauss is implemented for the full-rank family only");
+  FR_HIP(launch_target_logdensity(f.tgt, D, N, W->X.d(), W->logp.d(), W->G.d(), st));
+  if (f.chivi)
+    FR_HIP(launch_family_logdensity(f.fam, D, N, lam, f.df, f.t_const, W->X.d(), W->zz.d(), st));
+  const double c0 = f.fam == 1 ? 0.0 : 0.5 * D * (1.0 + kLog2Pi);
+  hipLaunchKernelGGL(mfw_weights_kernel, dim3(1), dim3(1024), 0, st, N, D, f.chivi, f.alpha, c0,
+                     lam, W->logp.d(), W->zz.d(), W->r.d(), W->scal.d(), value);
+  hipLaunchKernelGGL(mfw_grad_kernel, dim3(blocks(D, 64)), dim3(256), 0, st, N, D, lam, W->X.d(),
+                     W->G.d(), W->r.d(), W->scal.d(), grad);
+  FR_HIP(hipGetLastError());
+  return 0;
+}
+
+namespace {
+__global__ __launch_bounds__(256) void sub_kernel(long long n, const double* a, const double* b,
+                                                  double* out) {
+  const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (k < n) out[k] = a[k] - b[k];
+}
+}  // namespace
+
+// lw = log p(x) - log q(x), x ~ q, for any mean-field family / target / D
+int mf_wide_log_weights(FrWork* W, const MfSpec& f, const double* lam, long long m,
+                        const double* host_eps, uint32_t k0, uint32_t k1, uint32_t stream,
+                        uint32_t step, double* lw, double* xs, hipStream_t st) {
+  const int D = f.D;
+  if (int rc = reserve_d(W, 1, st)) return rc;
+  if (int rc = reserve_n(W, D, m)) return rc;
+  double* x = xs ? xs : W->X.d();
+  FR_HIP(launch_sample(f.fam, D, m, lam, f.t_scale, f.shape, host_eps, k0, k1, stream, step, x, st));
+  FR_HIP(launch_target_logdensity(f.tgt, D, m, x, W->logp.d(), nullptr, st));
+  FR_HIP(launch_family_logdensity(f.fam, D, m, lam, f.df, f.t_const, x, W->zz.d(), st));
+  hipLaunchKernelGGL(sub_kernel, dim3(blocks(m)), dim3(256), 0, st, m, W->logp.d(), W->zz.d(), lw);
+  FR_HIP(hipGetLastError());
+  return 0;
+}
+
 // Sigma [D][D] (nullable) and ascending eigenvalues [D] (nullable) of Sigma = L L^T
 int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, hipStream_t st) {
   if (int rc = reserve_d(W, D, st)) return rc;

@@ -167,6 +167,18 @@ int fr_log_weights(FrWork* W, const FrSpec& f, const double* lam, long long m,
                    const double* host_eps, uint32_t k0, uint32_t k1, uint32_t stream,
                    uint32_t step, double* lw, double* xs, hipStream_t st);
 int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, hipStream_t st);
+
+// Mean-field families on the materialised path (any D, any objective / target).
+struct MfSpec {
+  int fam, D, N, tgt, chivi;
+  double alpha, t_scale, shape, df, t_const;
+};
+int mf_wide_value_grad(FrWork* W, const MfSpec& f, const double* lam, const double* host_eps,
+                       uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
+                       double* grad, hipStream_t st);
+int mf_wide_log_weights(FrWork* W, const MfSpec& f, const double* lam, long long m,
+                        const double* host_eps, uint32_t k0, uint32_t k1, uint32_t stream,
+                        uint32_t step, double* lw, double* xs, hipStream_t st);
 int fr_info(FrWork* W, hipStream_t st);
 hipError_t launch_fr_lw(int D, long long m, double df, double t_const, const double* logp,
                         const double* zz, const double* s, const double* scal, double* lw,

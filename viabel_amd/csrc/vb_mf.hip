@@ -564,6 +564,33 @@ __global__ __launch_bounds__(256) void target_sep_kernel(int D, long long n, con
   if (lane == 0) out[r] = acc;
 }
 
+// Funnel at any D: one wavefront per row (x[1] = log sigma broadcast to the row).
+__global__ __launch_bounds__(256) void funnel_wide_kernel(int D, long long n, const double* x,
+                                                          double* out, double* grad) {
+  const long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int lane = threadIdx.x & 63;
+  constexpr double s0 = 1.35;
+  const double v = x[r * D + 1];
+  const double scale = exp(v), inv_s2 = exp(-2.0 * v);
+  double lp = 0.0, gv = 0.0;
+  for (int d = lane; d < D; d += 64) {
+    if (d == 1) continue;
+    const double xd = x[r * D + d];
+    const double z = xd / scale;
+    lp += -0.5 * z * z - v - 0.5 * kLog2Pi;
+    if (grad) grad[r * D + d] = -xd * inv_s2;
+    gv += z * z - 1.0;
+  }
+  lp = wave_sum(lp);
+  gv = wave_sum(gv);
+  if (lane == 0) {
+    const double zv = v / s0;
+    out[r] = (-0.5 * zv * zv - log(s0) - 0.5 * kLog2Pi) + lp;
+    if (grad) grad[r * D + 1] = -zv / s0 + gv;
+  }
+}
+
 template <class TGT, int DMAX>
 __global__ __launch_bounds__(256) void target_row_kernel(int D, long long n, const double* x,
                                                          double* out, double* grad) {
@@ -904,7 +931,11 @@ hipError_t launch_target_logdensity(int tgt, int D, long long n, const double* x
     case 0: hipLaunchKernelGGL((target_sep_kernel<IsoGauss>), gw, block, 0, s, D, n, x, out, grad); break;
     case 1: hipLaunchKernelGGL((target_sep_kernel<Mixture>), gw, block, 0, s, D, n, x, out, grad); break;
     case 2:
-      hipLaunchKernelGGL((target_row_kernel<Funnel, kBlockDMax>), gt, block, 0, s, D, n, x, out, grad);
+      if (D <= kBlockDMax)
+        hipLaunchKernelGGL((target_row_kernel<Funnel, kBlockDMax>), gt, block, 0, s, D, n, x, out,
+                           grad);
+      else
+        hipLaunchKernelGGL(funnel_wide_kernel, gw, block, 0, s, D, n, x, out, grad);
       break;
     case 3:
       hipLaunchKernelGGL((target_row_kernel<EightSchools, kBlockDMax>), gt, block, 0, s, D, n, x,
