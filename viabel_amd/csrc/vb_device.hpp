@@ -36,8 +36,9 @@ __device__ __forceinline__ u4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint
     }
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    // three-input XOR in one v_bitop3_b32 (gfx950, truth table 0x96)
+    const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+    const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
     c1 = (uint32_t)p1;
     c3 = (uint32_t)p0;
     c0 = n0;
@@ -61,6 +62,15 @@ struct Rng {
 // arithmetic and special-case handling the noise path never needs): the
 // transform is ~40% cheaper.  The C oracle uses libm; tests compare at 1e-14.
 
+// Horner step a * b + c as a three-address VOP3 v_fma_f64.  Left to itself the
+// compiler emits v_mov_b64 (copy of the loop-invariant coefficient c) + v_fmac,
+// two instructions per step, because fmac's accumulator is also its destination.
+__device__ __forceinline__ double hfma(double a, double b, double c) {
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
 // log(u) for u in (0, 1]: u = m 2^e with m in [sqrt(1/2), sqrt(2)),
 // log m = 2 atanh(f) = 2 f sum_k f^2k / (2k+1), f = (m-1)/(m+1), |f| <= 0.1716.
 __device__ __forceinline__ double log_unit(double u) {
@@ -77,16 +87,16 @@ __device__ __forceinline__ double log_unit(double u) {
   f = fma(r, fma(-den, f, num), f);
   const double f2 = f * f;
   double p = 0.04347826086956522;            // 1/23
-  p = fma(p, f2, 0.047619047619047616);      // 1/21
-  p = fma(p, f2, 0.05263157894736842);
-  p = fma(p, f2, 0.058823529411764705);
-  p = fma(p, f2, 0.06666666666666667);
-  p = fma(p, f2, 0.07692307692307693);
-  p = fma(p, f2, 0.09090909090909091);
-  p = fma(p, f2, 0.1111111111111111);
-  p = fma(p, f2, 0.14285714285714285);
-  p = fma(p, f2, 0.2);
-  p = fma(p, f2, 0.3333333333333333);
+  p = hfma(p, f2, 0.047619047619047616);      // 1/21
+  p = hfma(p, f2, 0.05263157894736842);
+  p = hfma(p, f2, 0.058823529411764705);
+  p = hfma(p, f2, 0.06666666666666667);
+  p = hfma(p, f2, 0.07692307692307693);
+  p = hfma(p, f2, 0.09090909090909091);
+  p = hfma(p, f2, 0.1111111111111111);
+  p = hfma(p, f2, 0.14285714285714285);
+  p = hfma(p, f2, 0.2);
+  p = hfma(p, f2, 0.3333333333333333);
   const double de = (double)e;
   // ln2 = LN2_HI + LN2_LO, LN2_HI with trailing zero bits so de * LN2_HI is exact
   const double t = fma(2.0 * f * f2, p, 2.0 * f);
@@ -112,25 +122,25 @@ __device__ __forceinline__ void sincospi_unit(double x, double& sn, double& cs) 
   const double th = fma(r, 3.141592653589793, r * 1.2246467991473532e-16);
   const double t2 = th * th;
   double ps = -8.22063524662433e-18;
-  ps = fma(ps, t2, 2.8114572543455206e-15);
-  ps = fma(ps, t2, -7.647163731819816e-13);
-  ps = fma(ps, t2, 1.6059043836821613e-10);
-  ps = fma(ps, t2, -2.505210838544172e-08);
-  ps = fma(ps, t2, 2.7557319223985893e-06);
-  ps = fma(ps, t2, -0.0001984126984126984);
-  ps = fma(ps, t2, 0.008333333333333333);
-  ps = fma(ps, t2, -0.16666666666666666);
+  ps = hfma(ps, t2, 2.8114572543455206e-15);
+  ps = hfma(ps, t2, -7.647163731819816e-13);
+  ps = hfma(ps, t2, 1.6059043836821613e-10);
+  ps = hfma(ps, t2, -2.505210838544172e-08);
+  ps = hfma(ps, t2, 2.7557319223985893e-06);
+  ps = hfma(ps, t2, -0.0001984126984126984);
+  ps = hfma(ps, t2, 0.008333333333333333);
+  ps = hfma(ps, t2, -0.16666666666666666);
   const double s0 = fma(th * t2, ps, th);
   double pc = 4.110317623312165e-19;
-  pc = fma(pc, t2, -1.5619206968586225e-16);
-  pc = fma(pc, t2, 4.779477332387385e-14);
-  pc = fma(pc, t2, -1.1470745597729725e-11);
-  pc = fma(pc, t2, 2.08767569878681e-09);
-  pc = fma(pc, t2, -2.755731922398589e-07);
-  pc = fma(pc, t2, 2.48015873015873e-05);
-  pc = fma(pc, t2, -0.001388888888888889);
-  pc = fma(pc, t2, 0.041666666666666664);
-  pc = fma(pc, t2, -0.5);
+  pc = hfma(pc, t2, -1.5619206968586225e-16);
+  pc = hfma(pc, t2, 4.779477332387385e-14);
+  pc = hfma(pc, t2, -1.1470745597729725e-11);
+  pc = hfma(pc, t2, 2.08767569878681e-09);
+  pc = hfma(pc, t2, -2.755731922398589e-07);
+  pc = hfma(pc, t2, 2.48015873015873e-05);
+  pc = hfma(pc, t2, -0.001388888888888889);
+  pc = hfma(pc, t2, 0.041666666666666664);
+  pc = hfma(pc, t2, -0.5);
   const double c0 = fma(t2, pc, 1.0);
   const int k = ((int)q) & 3;
   const double a = (k & 1) ? c0 : s0;     // |sin| or |cos| swapped on odd octant pairs
