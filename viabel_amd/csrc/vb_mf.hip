@@ -56,19 +56,24 @@ __device__ __forceinline__ double group_sum(double v) {
   return stride4_sum<PPW>(v);
 }
 
-// Value of lane (group base + k) for every lane of the group.
-template <int PPW>
-__device__ __forceinline__ double group_bcast(double v, int k, int grp) {
-  constexpr int LPP = 64 / PPW;
+// Value of lane (group base + K) for every lane of the group.  4 pairs per
+// wave: a group is one DPP row, so row_newbcast:K (dpp_ctrl 0x150 + K) does it;
+// 2 pairs: newbcast, then permlane16_swap copies each even row into the odd
+// row above it; 1 pair: readlane (the value is wave-uniform).
+template <int PPW, int K>
+__device__ __forceinline__ double group_bcast(double v, int /*grp*/) {
   if constexpr (PPW == 1) {
-    return readlane_f64(v, k);
-  } else if constexpr (PPW == 2) {
-    const double lo = readlane_f64(v, k), hi = readlane_f64(v, LPP + k);
-    return grp ? hi : lo;
+    return readlane_f64(v, K);
   } else {
-    const double g0 = readlane_f64(v, k), g1 = readlane_f64(v, LPP + k);
-    const double g2 = readlane_f64(v, 2 * LPP + k), g3 = readlane_f64(v, 3 * LPP + k);
-    return grp == 0 ? g0 : grp == 1 ? g1 : grp == 2 ? g2 : g3;
+    const double t = dpp_f64<0x150 + K>(v);
+    if constexpr (PPW == 4) {
+      return t;
+    } else {
+      const unsigned lo = (unsigned)__double2loint(t), hi = (unsigned)__double2hiint(t);
+      const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+      const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+      return __hiloint2double((int)b[0], (int)a[0]);
+    }
   }
 }
 
@@ -105,8 +110,8 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
   const bool updater = gl < 4 && own_ok;
   double lam_own = own_ok ? a.lam[own_idx] : 0.0;
   double s_own = exp(lam_own);
-  double muA = group_bcast<PPW>(lam_own, 0, grp), muB = group_bcast<PPW>(lam_own, 1, grp);
-  double sA = group_bcast<PPW>(s_own, 2, grp), sB = group_bcast<PPW>(s_own, 3, grp);
+  double muA = group_bcast<PPW, 0>(lam_own, grp), muB = group_bcast<PPW, 1>(lam_own, grp);
+  double sA = group_bcast<PPW, 2>(s_own, grp), sB = group_bcast<PPW, 3>(s_own, grp);
 
   int slot = 0, cnt = 0;
   double rg[PPW];
@@ -168,8 +173,8 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
     const double g_own = own < 2 ? -m : -(1.0 + s_own * m);
     // cross-lane reads with every lane active (a readlane of a lane outside the
     // exec mask may see a register the compiler did not keep for that lane)
-    const double lsA_b = group_bcast<PPW>(lam_own, 2, grp);
-    const double lsB_b = group_bcast<PPW>(lam_own, 3, grp);
+    const double lsA_b = group_bcast<PPW, 2>(lam_own, grp);
+    const double lsB_b = group_bcast<PPW, 3>(lam_own, grp);
     const double vpart = (hasB ? lsA_b + lsB_b : lsA_b) + v * invN;
     if (gl == 0 && live) a.vpart[(long long)s * a.n_waves + w] = vpart;
 
@@ -206,10 +211,10 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
     // lam - lr * g / sqrt(eps + accum)   (vb.py:374)
     lam_own = lam_own - (a.lr.at(i) * g_own) * rsqrt_pos(a.eps + q);
     s_own = exp(lam_own);
-    muA = group_bcast<PPW>(lam_own, 0, grp);
-    muB = group_bcast<PPW>(lam_own, 1, grp);
-    sA = group_bcast<PPW>(s_own, 2, grp);
-    sB = group_bcast<PPW>(s_own, 3, grp);
+    muA = group_bcast<PPW, 0>(lam_own, grp);
+    muB = group_bcast<PPW, 1>(lam_own, grp);
+    sA = group_bcast<PPW, 2>(s_own, grp);
+    sB = group_bcast<PPW, 3>(s_own, grp);
     if (i >= a.hist_start && updater) a.hist[(i - a.hist_start) * P + own_idx] = lam_own;
     slot = (slot + 1 == W) ? 0 : slot + 1;
   }
