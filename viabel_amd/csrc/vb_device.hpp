@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "vb_tables.hpp"
+
 namespace vbd {
 
 constexpr double kLog2Pi = 1.8378770664093454835606594728112;  // log(2*pi)
@@ -149,6 +151,56 @@ __device__ __forceinline__ void sincospi_unit(double x, double& sn, double& cs) 
   cs = (k == 1 || k == 2) ? -b : b;
 }
 
+// ---- table-driven forms (fused kernel; tables in LDS, vb_tables.hpp) ---------
+// log(u), u in (0, 1]: u = m 2^e, m in [sqrt(1/2), sqrt(2)); c = 1 + i/64 the
+// nearest table point, log m = -log(inv_c) + log1p(m inv_c - 1), |r| < 0.0113,
+// log1p to r^9.  At m ~ 1 the entry is exactly (1, 0): no cancellation.
+__device__ __forceinline__ double log_unit_tab(double u, const double2* ltab) {
+  int e;
+  double m = frexp(u, &e);
+  const bool lo = m < 0.70710678118654752440;
+  m = lo ? m + m : m;
+  e = lo ? e - 1 : e;
+  const int i = (int)rint(fma(m, 64.0, -64.0));  // exact: m in [0.5, 2)
+  const double2 t = ltab[i - kLogLo];
+  const double r = fma(m, t.x, -1.0);
+  double p = 0.1111111111111111;                 // 1/9
+  p = hfma(p, r, -0.125);
+  p = hfma(p, r, 0.14285714285714285);
+  p = hfma(p, r, -0.16666666666666666);
+  p = hfma(p, r, 0.2);
+  p = hfma(p, r, -0.25);
+  p = hfma(p, r, 0.3333333333333333);
+  p = hfma(p, r, -0.5);
+  const double l1p = fma(r * r, p, r);
+  const double de = (double)e;
+  return fma(de, 0.6931471805598903, fma(de, 5.497923018708371e-14, t.y + l1p));
+}
+
+// sin(pi x), cos(pi x) for x in [0, 2]: x = i/128 + r, |r| <= 1/256, table
+// (sin, cos)(pi i / 128) rotated by theta = pi r with short Taylor forms.
+__device__ __forceinline__ void sincospi_tab(double x, double& sn, double& cs,
+                                             const double2* sct) {
+  const double q = rint(x * 128.0);                 // 0..256
+  const double r = fma(q, -0.0078125, x);           // exact
+  const double2 t = sct[(int)q];
+  const double th = fma(r, 3.141592653589793, r * 1.2246467991473532e-16);
+  const double t2 = th * th;
+  double ps = hfma(t2, -0.0001984126984126984, 0.008333333333333333);
+  ps = hfma(ps, t2, -0.16666666666666666);
+  const double st = fma(th * t2, ps, th);           // sin(theta)
+  double pc = hfma(t2, 2.48015873015873e-05, -0.001388888888888889);
+  pc = hfma(pc, t2, 0.041666666666666664);
+  pc = hfma(pc, t2, -0.5);
+  const double ct = fma(t2, pc, 1.0);               // cos(theta)
+  sn = fma(t.x, ct, t.y * st);
+  cs = fma(t.y, ct, -(t.x * st));
+}
+
+// Two standard normals (Box-Muller) with the table transcendentals.
+__device__ __forceinline__ void normal_pair_tab(u4 w, double& z0, double& z1, const double2* sct,
+                                                const double2* ltab);
+
 // Uniforms from 52 random bits by filling the mantissa of a double in [1, 2):
 //   u1 = 1.m - (1 - 2^-53) = (2m + 1) 2^-53  in (0, 1)   (never 0: log is finite)
 //   u2 = 1.m - 1            = m 2^-52         in [0, 1)
@@ -156,6 +208,25 @@ __device__ __forceinline__ double unit_mantissa(uint32_t lo, uint32_t hi) {
   const uint32_t mlo = __builtin_amdgcn_alignbit(hi, lo, 12);
   const uint32_t mhi = (hi >> 12) | 0x3FF00000u;
   return __hiloint2double((int)mhi, (int)mlo);
+}
+
+__device__ __forceinline__ void normal_pair_tab(u4 w, double& z0, double& z1, const double2* sct,
+                                                const double2* ltab) {
+  const double u1 = unit_mantissa(w.x, w.y) - 0x1.fffffffffffffp-1;
+  const double u2 = unit_mantissa(w.z, w.w) - 1.0;
+  const double r = sqrt_pos(-2.0 * log_unit_tab(u1, ltab));
+  double s, c;
+  sincospi_tab(2.0 * u2, s, c, sct);
+  z0 = r * c;
+  z1 = r * s;
+}
+
+// Fill the LDS tables (all threads of the block; caller synchronises).
+__device__ __forceinline__ void load_bm_tables(double2* sct, double2* ltab) {
+  for (int i = threadIdx.x; i < kSinCosN; i += blockDim.x)
+    sct[i] = double2{kSinCosPiTab[i][0], kSinCosPiTab[i][1]};
+  for (int i = threadIdx.x; i < kLogN; i += blockDim.x)
+    ltab[i] = double2{kLogTab[i][0], kLogTab[i][1]};
 }
 
 // Two standard normals from one Philox block (Box-Muller).

@@ -90,7 +90,8 @@ __device__ __forceinline__ double rsqrt_pos(double y) {
 // REGRING: the adagrad window (W <= 16) lives in registers, one entry per
 // (lane, j): slot j * (LPP / 4) + gl / 4 of parameter gl & 3; otherwise in LDS.
 template <class TGT, bool TFAM, bool HOST, int PPW, bool REGRING>
-__device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, int wave) {
+__device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, int wave,
+                                         const double2* sct, const double2* ltab) {
   constexpr int LPP = 64 / PPW;       // lanes per column pair
   constexpr int SL = LPP / 4;         // slot lanes per parameter
   const int lane = threadIdx.x & 63;
@@ -147,7 +148,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
         eA = live ? row[dA] : 0.0;
         eB = hasB ? row[dB] : 0.0;
       } else {
-        normal_pair(rng.draw((uint32_t)w, (uint32_t)n, ri, 0u), eA, eB);
+        normal_pair_tab(rng.draw((uint32_t)w, (uint32_t)n, ri, 0u), eA, eB, sct, ltab);
         if constexpr (TFAM) {
           double GA, GB;
           gamma_pair(rng, (uint32_t)w, (uint32_t)n, ri, a.shape, GA, GB);
@@ -241,16 +242,23 @@ template <class TGT, bool TFAM, bool HOST, int PPW_BIG, bool REGRING>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(3)))
 void sep_kernel(SepArgs a) {
   __shared__ double s_ring[REGRING ? 1 : 4][REGRING ? 1 : 64 * 4 * PPW_BIG];
+  // Box-Muller tables (vb_tables.hpp) for the in-kernel Philox draws
+  __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
+  __shared__ double2 s_lt[HOST ? 1 : kLogN];
+  if constexpr (!HOST) {
+    load_bm_tables(s_sct, s_lt);
+    __syncthreads();
+  }
   const int wid = threadIdx.x >> 6;
   double* ring = REGRING ? nullptr : &s_ring[REGRING ? 0 : wid][0];
   if ((int)blockIdx.x < a.blocks2) {
     const int wave = blockIdx.x * 4 + wid;
     if (wave * PPW_BIG >= a.pairs2) return;
-    sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave);
+    sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave, s_sct, s_lt);
   } else {
     const int pair = a.pairs2 + (blockIdx.x - a.blocks2) * 4 + wid;
     if (pair >= a.n_pairs) return;
-    sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair);
+    sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair, s_sct, s_lt);
   }
 }
 
