@@ -161,7 +161,9 @@ __device__ __forceinline__ double log_unit_tab(double u, const double2* ltab) {
   const bool lo = m < 0.70710678118654752440;
   m = lo ? m + m : m;
   e = lo ? e - 1 : e;
-  const int i = (int)rint(fma(m, 64.0, -64.0));  // exact: m in [0.5, 2)
+  // exact: m in [0.5, 2); the clamp only matters for 0 / inf / NaN arguments,
+  // which callers route to the general log (memory safety)
+  const int i = min(max((int)rint(fma(m, 64.0, -64.0)), kLogLo), kLogLo + kLogN - 1);
   const double2 t = ltab[i - kLogLo];
   const double r = fma(m, t.x, -1.0);
   double p = 0.1111111111111111;                 // 1/9
@@ -243,9 +245,13 @@ __device__ __forceinline__ void normal_pair(u4 w, double& z0, double& z1) {
 // Gamma(shape) draws for the two elements of a column pair (Marsaglia-Tsang,
 // ACM TOMS 26(3) 2000).  Proposal k uses Philox purpose 1+k; each proposal
 // block gives two 32-bit-uniform Box-Muller normals and two uniforms.
+// TAB: use the LDS-table log / sincos (sct, ltab) instead of the short forms
+// and the general log of the acceptance test.
+template <bool TAB = false>
 __device__ __forceinline__ void gamma_pair(const Rng& rng, uint32_t pair, uint32_t sample,
                                            uint32_t step, double shape, double& ga,
-                                           double& gb) {
+                                           double& gb, const double2* sct = nullptr,
+                                           const double2* ltab = nullptr) {
   const double d = shape - 1.0 / 3.0;
   const double c = 1.0 / sqrt(9.0 * d);
   bool da = false, db = false;
@@ -255,9 +261,14 @@ __device__ __forceinline__ void gamma_pair(const Rng& rng, uint32_t pair, uint32
     const u4 w = rng.draw(pair, sample, step, 1u + k);
     const double u1 = ((double)w.x + 0.5) * 0x1p-32;
     const double u2 = (double)w.y * 0x1p-32;
-    const double r = sqrt_pos(-2.0 * log_unit(u1));
-    double s, cs;
-    sincospi_unit(2.0 * u2, s, cs);
+    double s, cs, r;
+    if constexpr (TAB) {
+      r = sqrt_pos(-2.0 * log_unit_tab(u1, ltab));
+      sincospi_tab(2.0 * u2, s, cs, sct);
+    } else {
+      r = sqrt_pos(-2.0 * log_unit(u1));
+      sincospi_unit(2.0 * u2, s, cs);
+    }
     const double za = r * cs, zb = r * s;
     const double ua = ((double)w.z + 0.5) * 0x1p-32;
     const double ub = ((double)w.w + 0.5) * 0x1p-32;
@@ -265,7 +276,9 @@ __device__ __forceinline__ void gamma_pair(const Rng& rng, uint32_t pair, uint32
       double v = 1.0 + c * za;
       if (v > 0.0) {
         v = v * v * v;
-        if (log(ua) < 0.5 * za * za + d - d * v + d * log(v)) {
+        const double lu = TAB ? log_unit_tab(ua, ltab) : log(ua);
+        const double lv = (TAB && v >= 0x1p-1022 && v < 0x1p+1023) ? log_unit_tab(v, ltab) : log(v);
+        if (lu < 0.5 * za * za + d - d * v + d * lv) {
           ga = d * v;
           da = true;
         }
@@ -275,7 +288,9 @@ __device__ __forceinline__ void gamma_pair(const Rng& rng, uint32_t pair, uint32
       double v = 1.0 + c * zb;
       if (v > 0.0) {
         v = v * v * v;
-        if (log(ub) < 0.5 * zb * zb + d - d * v + d * log(v)) {
+        const double lu = TAB ? log_unit_tab(ub, ltab) : log(ub);
+        const double lv = (TAB && v >= 0x1p-1022 && v < 0x1p+1023) ? log_unit_tab(v, ltab) : log(v);
+        if (lu < 0.5 * zb * zb + d - d * v + d * lv) {
           gb = d * v;
           db = true;
         }

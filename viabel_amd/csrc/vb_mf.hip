@@ -151,7 +151,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
         normal_pair_tab(rng.draw((uint32_t)w, (uint32_t)n, ri, 0u), eA, eB, sct, ltab);
         if constexpr (TFAM) {
           double GA, GB;
-          gamma_pair(rng, (uint32_t)w, (uint32_t)n, ri, a.shape, GA, GB);
+          gamma_pair<true>(rng, (uint32_t)w, (uint32_t)n, ri, a.shape, GA, GB, sct, ltab);
           eA = a.t_scale * eA / sqrt(GA);
           eB = a.t_scale * eB / sqrt(GB);
         }
@@ -319,6 +319,9 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
   __shared__ double s_ring[WMAX * 2 * DMAX];
   __shared__ double s_red[4][K + 1];
   __shared__ double s_max[4];
+  __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
+  __shared__ double2 s_lt[HOST ? 1 : kLogN];
+  if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
 
   using Row = RowOf<TGT>;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -362,11 +365,12 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
 #pragma unroll
         for (int j = 0; j < DMAX / 2; ++j) {
           if (2 * j < D) {
-            normal_pair(rng.draw((uint32_t)j, (uint32_t)n, (uint32_t)ri, 0u), e[2 * j],
-                        e[2 * j + 1]);
+            normal_pair_tab(rng.draw((uint32_t)j, (uint32_t)n, (uint32_t)ri, 0u), e[2 * j],
+                            e[2 * j + 1], s_sct, s_lt);
             if constexpr (TFAM) {
               double ga, gb;
-              gamma_pair(rng, (uint32_t)j, (uint32_t)n, (uint32_t)ri, a.shape, ga, gb);
+              gamma_pair<true>(rng, (uint32_t)j, (uint32_t)n, (uint32_t)ri, a.shape, ga, gb,
+                               s_sct, s_lt);
               e[2 * j] = a.t_scale * e[2 * j] / sqrt(ga);
               e[2 * j + 1] = a.t_scale * e[2 * j + 1] / sqrt(gb);
             }
