@@ -311,21 +311,29 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double (*red)[K + 1], 
   __syncthreads();
 }
 
+// Philox mode splits a step into a draw phase (every thread takes (sample, pair)
+// items: normal pair [+ gamma pair] -> LDS) and a row phase (one thread per
+// sample: reparameterise, target, accumulate), so one problem's draws spread
+// over up to 8 waves instead of one thread per sample.
+constexpr int kBlockMaxThreads = 512;
+constexpr int kBlockDrawLds = 4096;  // doubles of LDS for one chunk of draws
+
 template <class TGT, bool TFAM, bool HOST, int DMAX>
-__global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
+__global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   constexpr int K = 2 * DMAX + 2;   // G[DMAX], H[DMAX], V/S, spare
   constexpr int WMAX = 64;
   __shared__ double s_lam[2 * DMAX];
   __shared__ double s_ring[WMAX * 2 * DMAX];
-  __shared__ double s_red[4][K + 1];
-  __shared__ double s_max[4];
+  __shared__ double s_red[8][K + 1];
+  __shared__ double s_max[8];
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN];
+  __shared__ double s_e[HOST ? 1 : kBlockDrawLds];
   if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
 
   using Row = RowOf<TGT>;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int NT = blockDim.x, NW = NT >> 6;  // 64..256 threads (sized to N by the launcher)
+  const int NT = blockDim.x, NW = NT >> 6;  // 64..512 threads (sized by the launcher)
   const int prob = blockIdx.x;
   const int D = a.D, N = a.N, W = a.W, P = a.P;
   const double dN = (double)N;
@@ -355,30 +363,38 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
     double mloc = -INFINITY;  // CHIVI: running max of this thread's log weights
 
-    for (int n = tid; n < N; n += NT) {
+    const int NP = (D + 1) / 2;
+    const int CH = HOST ? N : kBlockDrawLds / (2 * NP);  // samples per draw chunk
+    for (int c0n = 0; c0n < N; c0n += CH) {
+    const int nc = min(CH, N - c0n);
+    if constexpr (!HOST) {
+      // draw phase: items (sample, pair) over all threads
+      for (int it = tid; it < nc * NP; it += NT) {
+        const int nl = it / NP, j = it - nl * NP;
+        const uint32_t n = (uint32_t)(c0n + nl);
+        double ea, eb;
+        normal_pair_tab(rng.draw((uint32_t)j, n, (uint32_t)ri, 0u), ea, eb, s_sct, s_lt);
+        if constexpr (TFAM) {
+          double ga, gb;
+          gamma_pair<true>(rng, (uint32_t)j, n, (uint32_t)ri, a.shape, ga, gb, s_sct, s_lt);
+          ea = a.t_scale * ea / sqrt(ga);
+          eb = a.t_scale * eb / sqrt(gb);
+        }
+        s_e[nl * 2 * NP + 2 * j] = ea;
+        s_e[nl * 2 * NP + 2 * j + 1] = eb;
+      }
+      __syncthreads();
+    }
+    for (int n = c0n + tid; n < c0n + nc; n += NT) {
       double e[DMAX], x[DMAX], g[DMAX];
       if constexpr (HOST) {
         const double* row = a.noise + (((long long)prob * a.n_steps + s) * N + n) * D;
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) e[d] = d < D ? row[d] : 0.0;
       } else {
+        const double* row = s_e + (n - c0n) * 2 * NP;
 #pragma unroll
-        for (int j = 0; j < DMAX / 2; ++j) {
-          if (2 * j < D) {
-            normal_pair_tab(rng.draw((uint32_t)j, (uint32_t)n, (uint32_t)ri, 0u), e[2 * j],
-                            e[2 * j + 1], s_sct, s_lt);
-            if constexpr (TFAM) {
-              double ga, gb;
-              gamma_pair<true>(rng, (uint32_t)j, (uint32_t)n, (uint32_t)ri, a.shape, ga, gb,
-                               s_sct, s_lt);
-              e[2 * j] = a.t_scale * e[2 * j] / sqrt(ga);
-              e[2 * j + 1] = a.t_scale * e[2 * j + 1] / sqrt(gb);
-            }
-          } else {
-            e[2 * j] = 0.0;
-            e[2 * j + 1] = 0.0;
-          }
-        }
+        for (int d = 0; d < DMAX; ++d) e[d] = d < D ? row[d] : 0.0;
       }
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
@@ -421,6 +437,8 @@ __global__ __launch_bounds__(256) void block_kernel(BlockArgs a) {
         }
         acc[2 * DMAX] += wgt;
       }
+    }
+    if constexpr (!HOST) __syncthreads();  // s_e is refilled by the next chunk
     }
 
     double M = 0.0;
@@ -838,12 +856,18 @@ hipError_t launch_sep(int fam, int tgt, bool host, const SepArgs& a, hipStream_t
 }
 
 // Threads per problem: the draws of one step spread over ceil(N/64) waves (<= 4).
-inline unsigned block_threads(int N) { return 64u * (unsigned)std::min(4, std::max(1, (N + 63) / 64)); }
+// Threads per problem: host noise -> one thread per sample (<= 4 waves); Philox ->
+// enough waves for the (sample, pair) draw items of a step (<= 8 waves).
+inline unsigned block_threads(int N, int D, bool host) {
+  const long long items = host ? N : (long long)N * ((D + 1) / 2);
+  const int cap = host ? 4 : kBlockMaxThreads / 64;
+  return 64u * (unsigned)std::min<long long>(cap, std::max<long long>(1, (items + 63) / 64));
+}
 
 template <class TGT, int DM>
 static hipError_t block_dispatch_dm(int fam, bool host, const BlockArgs& a, int nprob,
                                     hipStream_t s) {
-  const dim3 grid(nprob), block(block_threads(a.N));
+  const dim3 grid(nprob), block(block_threads(a.N, a.D, host));
   if (host && fam == 1) {
     hipLaunchKernelGGL((block_kernel<TGT, true, true, DM>), grid, block, 0, s, a);
   } else if (host) {
