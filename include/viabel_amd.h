@@ -32,6 +32,7 @@
  *   vb_divergence_bound    viabel/bounds.py:142-192 (divergence_bound, mean_and_check_mc_error)
  *   vb_centered_moments    viabel/bounds.py:127-135 (wasserstein_bounds sample moments)
  *   vb_covariance          viabel/bounds.py:55-56 (np.cov(samples.T), ddof = 1)
+ *   vb_weighted_covariance notebooks/experiments.py:83-85 (PSIS-weighted mean / np.cov)
  *   vb_psislw              notebooks/psis.py:112-208 (psislw)
  *   vb_gpdfit              notebooks/psis.py:211-331 (gpdfitnew)
  *   vb_gpinv               notebooks/psis.py:334-376 (gpinv)
@@ -75,8 +76,10 @@ enum vb_target_kind {
 };
 
 enum vb_objective_kind {
-  VB_OBJ_KLVI = 0,  /* value = -(entropy + mean log p)            vb.py:236-245 */
-  VB_OBJ_CHIVI = 1  /* value = CUBO_alpha, grad = alpha/N sum w dlw vb.py:248-266 */
+  VB_OBJ_KLVI = 0,     /* value = -(entropy + mean log p)              vb.py:236-245 */
+  VB_OBJ_CHIVI = 1,    /* value = CUBO_alpha, grad = alpha/N sum w dlw vb.py:248-266 */
+  VB_OBJ_KLVI_PD = 2   /* value = -(mean log p - mean log q(x)), gradient = KLVI's
+                          (black_box_klvi_pd / _pd2, vb.py:268-295) */
 };
 
 enum vb_noise_kind {
@@ -231,10 +234,15 @@ int vb_divergence_bound(vb_ctx* ctx, const double* lw, int64_t n, double alpha,
 /* c2 = mean_n sum_d (x - xbar)^2, c4 = mean_n sum_d (x - xbar)^4. */
 int vb_centered_moments(vb_ctx* ctx, const double* x, int64_t n, int64_t d,
                         double* c2, double* c4);
-/* column means [d] and covariance [d, d] (ddof = 1, np.cov(x.T)) of x [n, d];
- * d <= 64. */
+/* column means [d] and covariance [d, d] (ddof = 1, np.cov(x.T)) of x [n, d]
+ * (d <= 64: fixed-order pairwise reduction; larger d: fp64 MFMA product). */
 int vb_covariance(vb_ctx* ctx, const double* x, int64_t n, int64_t d,
                   double* mean_out, double* cov_out);
+/* np.cov(x.T, aweights=w, ddof=ddof) and the weighted mean (np.average with
+ * weights) of x [n, d]; w [n] nullable (unweighted).  improve_with_psis
+ * (notebooks/experiments.py:73-89) with the PSIS-smoothed weights. */
+int vb_weighted_covariance(vb_ctx* ctx, const double* x, int64_t n, int64_t d,
+                           const double* w, int32_t ddof, double* mean_out, double* cov_out);
 
 /* ---- PSIS (psis.py:112-395) ------------------------------------------ */
 /* lw [n, m] C order (m columns of n log weights).  lw_out same layout.

@@ -125,6 +125,15 @@ def klvi_value_grad(fam, target, lam, n_samples, draws=None):
     return value, _grad_from_GS(fam, lam, GS, -0.5, -np.mean(g, axis=0))
 
 
+def klvi_pd_value_grad(fam, target, lam, n_samples, draws=None):
+    """black_box_klvi_pd (vb.py:268-278): value -(mean log p - mean log q(x)); the
+    gradient equals KLVI's (log q's total derivative is -1/2 d log det Sigma)."""
+    s, z = fam.draw(n_samples) if draws is None else draws
+    x = fam.transform(lam, s, z)
+    value = -(np.mean(target(x)[0]) - np.mean(fam.logdensity(x, lam)))
+    return value, klvi_value_grad(fam, target, lam, n_samples, draws=(s, z))[1]
+
+
 def chivi_value_grad(fam, target, lam, n_samples, alpha, draws=None):
     """black_box_chivi (vb.py:248-266) for the full-rank t family."""
     if draws is None:

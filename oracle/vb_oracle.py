@@ -103,6 +103,22 @@ def klvi_value_grad(fam, target, lam, n_samples, eps=None):
     return value, np.concatenate([gmu, gls])
 
 
+def klvi_pd_value_grad(fam, target, lam, n_samples, eps=None):
+    """black_box_klvi_pd / _pd2 (vb.py:268-295): value = -(mean log p - mean log q(x)).
+    autograd differentiates log q through x and lambda; for these families the
+    total derivative of log q(x(lambda); lambda) is (0, -1) per coordinate, so the
+    gradient equals klvi_value_grad's (tests pin this with torch.autograd)."""
+    if eps is None:
+        eps = fam.draw(n_samples)
+    x = fam.transform(lam, eps)
+    lp, g = targets_oracle.TARGETS[target](x)
+    value = -(np.mean(lp) - np.mean(fam.logdensity(x, lam)))
+    _, ls = fam.split(lam)
+    gmu = -np.mean(g, axis=0)
+    gls = -(1.0 + np.exp(ls) * np.mean(g * eps, axis=0))
+    return value, np.concatenate([gmu, gls])
+
+
 def chivi_value_grad(fam, target, lam, n_samples, alpha, eps=None):
     """black_box_chivi (vb.py:248-266).  The reference draws a fresh seed from the
     GLOBAL numpy RNG each call (vb.py:258) and samples from RandomState(seed).

@@ -156,3 +156,56 @@ class TestPsis:
         _close(out[:, 0], oout, rtol=1e-11, atol=1e-11)
         # size-independent property: smoothed weights are normalised
         assert abs(np.log(np.sum(np.exp(out))) ) < 1e-10
+
+
+# ---- covariance at any d, PSIS-weighted moments (experiments.py:73-89) -------
+@pytest.mark.parametrize('n,d', [(500, 3), (2000, 100), (700, 300)])
+@pytest.mark.parametrize('weighted', [False, True])
+def test_weighted_covariance_vs_numpy(n, d, weighted):
+    """np.cov(x.T, aweights=w, ddof) / np.average: numpy is the reference's own call."""
+    from viabel_amd import experiments
+    rs = np.random.RandomState(n + d)
+    x = rs.randn(n, d) @ (np.eye(d) + 0.1 * rs.randn(d, d)) + rs.randn(d)
+    w = rs.rand(n) if weighted else None
+    for ddof in (0, 1):
+        m, c = experiments.weighted_mean_and_cov(x, w, ddof=ddof)
+        np.testing.assert_allclose(m, np.average(x, axis=0, weights=w), rtol=1e-11, atol=1e-12)
+        np.testing.assert_allclose(c, np.cov(x.T, aweights=w, ddof=ddof), rtol=1e-10, atol=1e-12)
+
+
+def test_all_bounds_samples_wide():
+    """all_bounds with raw samples at d > 64 (np.cov on the MFMA GEMM path)."""
+    import viabel_amd as va
+    from oracle import bounds_oracle
+    rs = np.random.RandomState(2)
+    lw = rs.randn(4000) * 0.3
+    x = rs.randn(4000, 90)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        res = va.all_bounds(lw, samples=x)
+        ores = bounds_oracle.all_bounds(lw, samples=x)
+    for k in ('W1', 'W2', 'mean_error', 'std_error', 'cov_error', 'd2'):
+        np.testing.assert_allclose(res[k], ores[k], rtol=1e-9)
+
+
+def test_improve_with_psis_vs_oracle():
+    from viabel_amd import vb, targets, experiments
+    from oracle import vb_oracle, psis_oracle
+    D = 4
+    fam = vb.mean_field_gaussian_variational_family(D, rng='numpy')
+    ofam = vb_oracle.Family('gauss', D)
+    lam = np.concatenate([np.zeros(D) + 0.2, np.zeros(D) - 0.1])
+    true_mean, true_cov = np.zeros(D), np.eye(D)
+    res, m, c = experiments.improve_with_psis(targets.isogauss(D), fam, lam, 20000, true_mean,
+                                              true_cov)
+    x, lw = vb_oracle.log_weights(ofam, 'isogauss', lam, 20000)
+    slw, khat = psis_oracle.psislw(lw.copy())
+    slw = slw - np.max(slw)
+    wts = np.exp(slw)
+    wts /= np.sum(wts)
+    om = np.sum(wts[:, None] * x, axis=0)
+    oc = np.cov(x.T, aweights=wts, ddof=0)
+    np.testing.assert_allclose(m, om, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(c, oc, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(res['khat'], khat, rtol=1e-9)
+    np.testing.assert_allclose(res['mean_error'], np.linalg.norm(true_mean - om), rtol=1e-8)

@@ -124,3 +124,44 @@ def test_rmsprop_ia_wide():
     ores = fo.rmsprop_IA_optimize_with_rhat(400, ofn, np.zeros(2 * D), D, **kw)
     _close(res[1], ores[1], 1e-7)
     _close(res[4], ores[4], 1e-7)
+
+
+@pytest.mark.parametrize('kind,df', [('gauss', None), ('t', 40.0), ('t', 5.0)])
+@pytest.mark.parametrize('target,D', [('isogauss', 6), ('mixture', 2000), ('funnel', 10),
+                                      ('funnel', 40), ('isogauss', 17)])
+def test_klvi_pd_numpy_stream(kind, df, target, D):
+    """black_box_klvi_pd / _pd2 (vb.py:268-295) on every mean-field path."""
+    vb, targets, vo = _mods()
+    fam = _family(vb, kind, df, D)
+    ofam = vo.Family(kind, D, df)
+    for k, ctor in enumerate((vb.black_box_klvi_pd, vb.black_box_klvi_pd2)):
+        obj = ctor(fam, _target(targets, target, D), 50)
+        lam = _lam(D, 30 + k)
+        v, g = obj(lam)
+        ov, og = vo.klvi_pd_value_grad(ofam, target, lam, 50)
+        assert abs(v - ov) <= 1e-10 * max(1.0, abs(ov)), (v, ov)
+        _close(g, og, 1e-10)
+
+
+def test_klvi_pd_adagrad_and_fullrank():
+    vb, targets, vo = _mods()
+    from oracle import fullrank_oracle as fr
+    D = 300
+    fam = _family(vb, 'gauss', None, D)
+    ofam = vo.Family('gauss', D)
+    obj = vb.black_box_klvi_pd(fam, targets.isogauss(D), 20)
+    lam0 = _lam(D, 7)
+    sm, hist, vals, _ = vb.adagrad_optimize(50, obj, lam0)
+    osm, ohist, ovals = vo.adagrad_optimize(
+        50, lambda lam: vo.klvi_pd_value_grad(ofam, 'isogauss', lam, 20), lam0)[:3]
+    _close(vals, ovals, 1e-9)
+    _close(hist, ohist, 1e-9)
+    Dr = 7
+    ffam = vb.t_variational_family(Dr, 100.0, rng='numpy')
+    offam = fr.FullRankT(Dr, 100.0)
+    rs = np.random.RandomState(2)
+    lam = np.concatenate([rs.randn(Dr) * 0.2, rs.randn(Dr * (Dr + 1) // 2) * 0.05])
+    v, g = vb.black_box_klvi_pd(ffam, targets.corr_gauss(Dr), 40)(lam)
+    ov, og = fr.klvi_pd_value_grad(offam, fr.target_fn('corr_gauss', Dr), lam, 40)
+    np.testing.assert_allclose(v, ov, rtol=1e-9)
+    _close(g, og, 1e-8)

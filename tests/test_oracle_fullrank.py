@@ -109,3 +109,20 @@ def test_family_helpers():
     assert fam.var_param_dim == D + D * (D + 1) // 2
     with pytest.raises(ValueError, match='df must be greater than 2'):
         fo.FullRankT(3, 2)
+
+
+def test_fullrank_klvi_pd_vs_autograd():
+    D = 6
+    fam = fo.FullRankT(D, 100.0)
+    tgt = fo.target_fn('corr_gauss', D)
+    lam = _lam(D, 9)
+    draws = fam.draw(30, seed=5)
+    val, grad = fo.klvi_pd_value_grad(fam, tgt, lam, 30, draws=draws)
+    tl = torch.tensor(lam, requires_grad=True)
+    mu, L, Sig = t_unpack(tl, D)
+    s, z = (torch.tensor(a) for a in draws)
+    x = mu + (z @ t_sqrtm(Sig)) / s[:, None]
+    f = -(torch.mean(t_target('corr_gauss', x, tgt)) - torch.mean(t_mvt_logpdf(x, mu, Sig, 100.0)))
+    f.backward()
+    np.testing.assert_allclose(val, f.item(), rtol=1e-11)
+    np.testing.assert_allclose(grad, tl.grad.numpy(), rtol=1e-7, atol=1e-9)

@@ -114,6 +114,23 @@ def test_chivi_gradient_vs_torch_autograd(kind, df, target, D, alpha):
     np.testing.assert_allclose(grad, tgrad, rtol=1e-9, atol=1e-10)
 
 
+@pytest.mark.parametrize('kind,df,target,D', CASES)
+def test_klvi_pd_gradient_vs_torch_autograd(kind, df, target, D):
+    """black_box_klvi_pd (vb.py:268-278): autograd through samples AND lambda in log q."""
+    fam = vb_oracle.Family(kind, D, df)
+    lam = _lam(D, 5)
+    eps = fam.draw(40)
+    val, grad = vb_oracle.klvi_pd_value_grad(fam, target, lam, 40, eps=eps)
+    tl = torch.tensor(lam, requires_grad=True)
+    mu, ls = tl[:D], tl[D:]
+    te = torch.tensor(eps)
+    x = te * torch.exp(ls) + mu
+    tv = -(torch.mean(t_target(target, x)) - torch.mean(t_logq(kind, df, x, mu, ls)))
+    tv.backward()
+    np.testing.assert_allclose(val, tv.item(), rtol=1e-11)
+    np.testing.assert_allclose(grad, tl.grad.numpy(), rtol=1e-9, atol=1e-10)
+
+
 @pytest.mark.parametrize('target', ['isogauss', 'mixture', 'funnel', 'eight_schools_ncp'])
 def test_target_grad_finite_differences(target):
     D = 10 if target == 'eight_schools_ncp' else 4

@@ -17,7 +17,7 @@ VB_OK, VB_EINVAL, VB_EDEVICE, VB_ENOMEM, VB_EUNSUPPORTED = 0, -1, -2, -3, -4
 FAMILY_MF_GAUSSIAN, FAMILY_MF_T, FAMILY_FR_T = 0, 1, 2
 TARGET_ISOGAUSS, TARGET_MIXTURE, TARGET_FUNNEL, TARGET_EIGHT_SCHOOLS_NCP = 0, 1, 2, 3
 TARGET_CORR_GAUSS = 4
-OBJ_KLVI, OBJ_CHIVI = 0, 1
+OBJ_KLVI, OBJ_CHIVI, OBJ_KLVI_PD = 0, 1, 2
 OPT_ADAGRAD, OPT_RMSPROP_IA, OPT_ADAM_IA = 0, 1, 2
 NOISE_HOST, NOISE_PHILOX = 0, 1
 
@@ -88,6 +88,8 @@ _SIGNATURES = {
                              c_double_p, c_double_p], ctypes.c_int),
     'vb_covariance': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, c_double_p,
                        c_double_p], ctypes.c_int),
+    'vb_weighted_covariance': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,
+                                c_double_p, ctypes.c_int32, c_double_p, c_double_p], ctypes.c_int),
     'vb_psislw': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
                    c_double_p, c_double_p, c_int64_p, ctypes.c_int64, c_int64_p], ctypes.c_int),
     'vb_gpdfit': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, c_double_p, c_double_p,

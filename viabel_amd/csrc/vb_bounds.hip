@@ -341,6 +341,56 @@ hipError_t bounds_centered_moments(const double* x, long long n, long long d, do
   return hipGetLastError();
 }
 
+namespace {
+// mean_j = sum_n w_n x_nj / sw  (w null: plain mean); 4 waves split the rows
+__global__ __launch_bounds__(256) void wmean_kernel(const double* x, long long n, long long d,
+                                                    const double* w, double sw, double* mean) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long long j = (long long)blockIdx.x * 64 + lane;
+  double a = 0.0;
+  if (j < d)
+    for (long long r = wv; r < n; r += 4) a += (w ? w[r] : 1.0) * x[r * d + j];
+  part[wv][lane] = a;
+  __syncthreads();
+  if (wv == 0 && j < d) mean[j] = ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane])) / sw;
+}
+
+__global__ __launch_bounds__(256) void center_kernel(const double* x, long long n, long long d,
+                                                     const double* mean, double* xc) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx < n * d) xc[idx] = x[idx] - mean[idx % d];
+}
+}  // namespace
+
+// np.cov(x.T, aweights=w, ddof=ddof): mean [d], cov [d][d] = Xc^T diag(w) Xc / fact,
+// fact = sw - ddof * sw2 / sw (aweights) or n - ddof; the product on fp64 MFMA.
+hipError_t bounds_weighted_covariance(const double* x, long long n, long long d, const double* w,
+                                      double sw, double fact, double* xc_scratch, double* mean,
+                                      double* cov, hipStream_t s) {
+  hipLaunchKernelGGL(wmean_kernel, dim3((unsigned)((d + 63) / 64)), dim3(256), 0, s, x, n, d, w, sw,
+                     mean);
+  hipLaunchKernelGGL(center_kernel, dim3((unsigned)((n * d + 255) / 256)), dim3(256), 0, s, x, n, d,
+                     mean, xc_scratch);
+  GemmOp g{};
+  g.ta = true;
+  g.tb = false;
+  g.M = (int)d;
+  g.N = (int)d;
+  g.K = (int)n;
+  g.A = xc_scratch;
+  g.lda = d;
+  g.B = xc_scratch;
+  g.ldb = d;
+  g.C = cov;
+  g.ldc = d;
+  g.alpha = 1.0 / fact;
+  g.kscale = w;
+  hipError_t e = gemm(g, s);
+  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
 hipError_t bounds_covariance(const double* x, long long n, long long d, double* scratch,
                              double* mean, double* cov, hipStream_t s) {
   hipError_t e = means(x, n, d, scratch, mean, s);

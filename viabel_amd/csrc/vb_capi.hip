@@ -257,12 +257,22 @@ vbk::FrSpec fr_spec(const FamInfo& fi, const vb_target* tgt, const vb_objective*
   f.N = (int)obj->n_samples;
   f.tgt = tgt->kind;
   f.chivi = obj->kind == VB_OBJ_CHIVI;
+  f.pd = obj->kind == VB_OBJ_KLVI_PD;
   f.df = fi.df;
   f.t_const = fi.t_const;
   f.alpha = obj->alpha;
   f.tparams = tparams;
   f.tconst = tconst;
   return f;
+}
+
+// Constant of the column-pair kernel's value: KLVI -(c0 + sum log s + mean log p);
+// KLVI_PD adds -log q's per-coordinate constants instead (the kernel accumulates
+// 1/2 eps^2 or (df+1)/2 log1p(eps^2/df) with log p).
+double sep_c0(const FamInfo& fi, bool pd) {
+  const double D = (double)fi.D;
+  if (fi.kind == VB_FAMILY_MF_T) return pd ? -D * fi.t_const : 0.0;
+  return pd ? 0.5 * D * std::log(2 * M_PI) : 0.5 * D * (1.0 + std::log(2 * M_PI));
 }
 
 vbk::MfSpec mf_spec(const FamInfo& fi, const vb_target* tgt, const vb_objective* obj) {
@@ -272,6 +282,7 @@ vbk::MfSpec mf_spec(const FamInfo& fi, const vb_target* tgt, const vb_objective*
   f.N = obj ? (int)obj->n_samples : 0;
   f.tgt = tgt->kind;
   f.chivi = obj && obj->kind == VB_OBJ_CHIVI;
+  f.pd = obj && obj->kind == VB_OBJ_KLVI_PD;
   f.alpha = obj ? obj->alpha : 2.0;
   f.t_scale = fi.t_scale;
   f.shape = fi.shape;
@@ -514,6 +525,8 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
   if (!obj || !lam || !noise || !value || !grad) return fail(VB_EINVAL, "null argument");
   if (obj->n_samples < 1 || obj->n_samples > (1LL << 31))
     return fail(VB_EINVAL, "n_samples must be positive");
+  if (obj->kind < VB_OBJ_KLVI || obj->kind > VB_OBJ_KLVI_PD)
+    return fail(VB_EINVAL, "unknown objective %d", obj->kind);
   if (obj->kind == VB_OBJ_CHIVI && !(obj->alpha > 0))
     return fail(VB_EINVAL, "alpha must be positive");
   VB_TRY(require_fr(fi.kind, tgt->kind));
@@ -536,7 +549,8 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
   VB_TRY(c->slot[4].reserve(sizeof(double) * 2));
   dval = c->slot[4].d();
 
-  const bool sep = vbk::target_separable(tgt->kind) && obj->kind == VB_OBJ_KLVI;
+  const bool pd = obj->kind == VB_OBJ_KLVI_PD;
+  const bool sep = vbk::target_separable(tgt->kind) && obj->kind != VB_OBJ_CHIVI;
   if (sep && D > vbk::kBlockDMax) {
     vbk::SepArgs a{};
     a.D = D;
@@ -545,6 +559,7 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
     a.n_pairs = (D + 1) / 2;
     a.n_steps = 1;
     a.emit_grad = 1;
+    a.pd = pd ? (fi.kind == VB_FAMILY_MF_T ? 2 : 1) : 0;
     a.step0 = 0;
     a.hist_start = 1LL << 62;
     a.rng_step0 = (long long)noise->step;
@@ -560,8 +575,7 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
     a.k1 = k1;
     a.stream = noise->stream;
     VB_HIP(vbk::launch_sep(fi.kind, tgt->kind, host, a, c->stream));
-    const double c0 = fi.kind == VB_FAMILY_MF_T ? 0.0 : 0.5 * D * (1.0 + std::log(2 * M_PI));
-    VB_HIP(vbk::launch_sep_values(a.vpart, 1, a.n_waves, c0, dval, c->stream));
+    VB_HIP(vbk::launch_sep_values(a.vpart, 1, a.n_waves, sep_c0(fi, pd), dval, c->stream));
   } else if (D <= vbk::kBlockDMax) {
     vbk::BlockArgs a{};
     a.D = D;
@@ -571,6 +585,7 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
     a.n_steps = 1;
     a.emit_grad = 1;
     a.chivi = obj->kind == VB_OBJ_CHIVI;
+    a.pd = pd;
     a.step0 = 0;
     a.hist_start = 1LL << 62;
     a.n_iters = 1;
@@ -655,7 +670,9 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
     return fail(VB_EINVAL, "n_samples must be positive");
   const int D = fi.D;
   const bool fr = fi.kind == VB_FAMILY_FR_T;
-  const bool sep = !fr && vbk::target_separable(tgt->kind) && obj->kind == VB_OBJ_KLVI &&
+  if (obj->kind < VB_OBJ_KLVI || obj->kind > VB_OBJ_KLVI_PD)
+    return fail(VB_EINVAL, "unknown objective %d", obj->kind);
+  const bool sep = !fr && vbk::target_separable(tgt->kind) && obj->kind != VB_OBJ_CHIVI &&
                    (D > vbk::kBlockDMax);
   // D > kBlockDMax without the fused kernel (CHIVI, non-separable targets, IA
   // optimisers): the materialised mean-field path, one problem per run
@@ -813,6 +830,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
       a.n_pairs = r->n_waves;
       a.n_steps = cs;
       a.emit_grad = 0;
+      a.pd = r->obj == VB_OBJ_KLVI_PD ? (r->fi.kind == VB_FAMILY_MF_T ? 2 : 1) : 0;
       a.step0 = r->done + off;
       a.hist_start = r->hist_start;
       a.rng_step0 = (long long)noise->step + off;
@@ -831,8 +849,8 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
       a.k1 = k1;
       a.stream = noise->stream;
       VB_HIP(vbk::launch_sep(r->fi.kind, r->tgt, host, a, c->stream));
-      const double c0 = r->fi.kind == VB_FAMILY_MF_T ? 0.0 : 0.5 * D * (1.0 + std::log(2 * M_PI));
-      VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, c0, r->values.d() + a.step0, c->stream));
+      VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, sep_c0(r->fi, a.pd != 0), r->values.d() + a.step0,
+                                    c->stream));
       off += cs;
     }
   } else {
@@ -844,6 +862,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
     a.n_steps = (int)n_steps;
     a.emit_grad = 0;
     a.chivi = r->obj == VB_OBJ_CHIVI;
+    a.pd = r->obj == VB_OBJ_KLVI_PD;
     a.opt = r->opt;
     a.step0 = r->done;
     a.hist_start = r->hist_start;
@@ -1059,13 +1078,48 @@ int vb_centered_moments(vb_ctx* c, const double* x, int64_t n, int64_t d, double
   return VB_OK;
 }
 
+int vb_weighted_covariance(vb_ctx* c, const double* x, int64_t n, int64_t d, const double* w,
+                           int32_t ddof, double* mean_out, double* cov_out) {
+  VB_TRY(check_ctx(c));
+  if (!x || !cov_out || n < 1 || d < 1) return fail(VB_EINVAL, "invalid argument");
+  if (d > (1LL << 30) || n > (1LL << 31)) return fail(VB_EINVAL, "sizes out of range");
+  In dx, dw;
+  VB_TRY(dx.stage(c, 0, x, (size_t)n * d));
+  double sw = (double)n, fact = (double)(n - ddof);
+  if (w) {
+    // weight sums on the host copy (n values; the caller's vector)
+    std::vector<double> hw((size_t)n);
+    VB_HIP(hipMemcpyAsync(hw.data(), w, sizeof(double) * n, hipMemcpyDefault, c->stream));
+    VB_TRY(sync(c));
+    double s1 = 0.0, s2 = 0.0;
+    for (double v : hw) {
+      s1 += v;
+      s2 += v * v;
+    }
+    if (!(s1 > 0)) return fail(VB_EINVAL, "weights sum to zero");
+    sw = s1;
+    fact = ddof == 0 ? s1 : s1 - ddof * s2 / s1;   // numpy.cov with aweights
+    VB_TRY(dw.stage(c, 6, w, (size_t)n));
+  }
+  VB_TRY(c->slot[1].reserve(sizeof(double) * (size_t)n * d));
+  VB_TRY(c->slot[4].reserve(sizeof(double) * d));
+  double* mdev = c->slot[4].d();
+  Out dm, dc;
+  VB_TRY(dm.stage(c, 5, mean_out, mean_out ? (size_t)d : 0));
+  VB_TRY(dc.stage(c, 2, cov_out, (size_t)d * d));
+  VB_HIP(vbk::bounds_weighted_covariance(dx.d, n, d, w ? dw.d : nullptr, sw, fact, c->slot[1].d(),
+                                         mdev, dc.d, c->stream));
+  if (mean_out) VB_HIP(hipMemcpyAsync(dm.d, mdev, sizeof(double) * d, hipMemcpyDeviceToDevice, c->stream));
+  VB_TRY(dm.finish(c));
+  VB_TRY(dc.finish(c));
+  return sync(c);
+}
+
 int vb_covariance(vb_ctx* c, const double* x, int64_t n, int64_t d, double* mean_out,
                   double* cov_out) {
   VB_TRY(check_ctx(c));
   if (!x || !cov_out || n < 2 || d < 1) return fail(VB_EINVAL, "invalid argument");
-  if (d > vbk::kCovDMax)
-    return fail(VB_EUNSUPPORTED, "device covariance supports d <= %d (got %lld)", vbk::kCovDMax,
-                (long long)d);
+  if (d > vbk::kCovDMax) return vb_weighted_covariance(c, x, n, d, nullptr, 1, mean_out, cov_out);
   In dx;
   VB_TRY(dx.stage(c, 0, x, (size_t)n * d));
   VB_TRY(c->slot[1].reserve(sizeof(double) * vbk::bounds_scratch_doubles(n, d)));

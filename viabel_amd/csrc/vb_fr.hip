@@ -156,28 +156,34 @@ __global__ __launch_bounds__(256) void fr_rows_kernel(int D, long long n, const 
 // KLVI (vb.py:236-245):  value = -(entropy + mean logp), r_n = -1/N.
 // CHIVI (vb.py:248-266): lw = logp - logq, w = exp(lw - max)^alpha,
 //   value = log(mean w)/alpha + max, r_n = alpha w_n / N.
-__global__ __launch_bounds__(1024) void fr_weights_kernel(int N, int D, int chivi, double alpha,
+__global__ __launch_bounds__(1024) void fr_weights_kernel(int N, int D, int chivi, int pd,
+                                                          double alpha,
                                                           double df, double t_const,
                                                           const double* logp, const double* zz,
                                                           const double* s, double* scal,
                                                           double* r, double* rk, double* value) {
   __shared__ double red[16];
   const double hld = scal[0];
+  const double e = 0.5 * (df + D);
   if (!chivi) {
     double a = 0.0;
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
-      a += logp[k];
+      if (pd) {  // black_box_klvi_pd: log p - log q(x), the Mahalanobis invariant
+        const double maha = zz[k] / (s[k] * s[k]);
+        a += logp[k] - ((t_const - hld) - e * log(1.0 + maha / df));
+      } else {
+        a += logp[k];
+      }
       r[k] = -1.0 / N;
       rk[k] = (-1.0 / N) / s[k];
     }
     a = block_sum(a, red);
     if (threadIdx.x == 0) {
-      *value = -(hld + a / N);
+      *value = pd ? -(a / N) : -(hld + a / N);
       scal[1] = -0.5;
     }
     return;
   }
-  const double e = 0.5 * (df + D);
   double mx = -INFINITY;
   for (int k = threadIdx.x; k < N; k += blockDim.x) {
     const double maha = zz[k] / (s[k] * s[k]);
@@ -689,15 +695,15 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
   if (f.tgt == kTargetCorrGauss) {
     FR_HIP(gemm(mm(N, D, D, W->X.d(), false, f.tparams, false, W->G.d(), -1.0), st));
     hipLaunchKernelGGL(fr_rows_kernel, dim3(blocks(N, 4)), dim3(256), 0, st, D, (long long)N,
-                       f.chivi ? z : nullptr, W->X.d(), W->G.d(), f.tconst, 1, W->zz.d(),
+                       (f.chivi || f.pd) ? z : nullptr, W->X.d(), W->G.d(), f.tconst, 1, W->zz.d(),
                        W->logp.d());
   } else {
     FR_HIP(launch_target_logdensity(f.tgt, D, N, W->X.d(), W->logp.d(), W->G.d(), st));
-    if (f.chivi)
+    if (f.chivi || f.pd)
       hipLaunchKernelGGL(fr_rows_kernel, dim3(blocks(N, 4)), dim3(256), 0, st, D, (long long)N,
                          z, nullptr, nullptr, 0.0, 0, W->zz.d(), nullptr);
   }
-  hipLaunchKernelGGL(fr_weights_kernel, dim3(1), dim3(1024), 0, st, N, D, f.chivi, f.alpha, f.df,
+  hipLaunchKernelGGL(fr_weights_kernel, dim3(1), dim3(1024), 0, st, N, D, f.chivi, f.pd, f.alpha, f.df,
                      f.t_const, W->logp.d(), W->zz.d(), s, W->scal.d(), W->r.d(), W->rk.d(),
                      value);
   // cotangent of S: G_S = Z^T diag(r / s) G
@@ -787,7 +793,8 @@ namespace {
 // KLVI: value = -(entropy + mean logp), r_n = -1/N, rsum = -1 (the entropy's
 // d/dlog sigma).  CHIVI: lw = logp - logq, w = exp(lw - max)^alpha,
 // value = log(mean w)/alpha + max, r_n = alpha w_n / N, rsum = sum_n r_n.
-__global__ __launch_bounds__(1024) void mfw_weights_kernel(int N, int D, int chivi, double alpha,
+__global__ __launch_bounds__(1024) void mfw_weights_kernel(int N, int D, int chivi, int pd,
+                                                           double alpha,
                                                            double c0, const double* lam,
                                                            const double* logp,
                                                            const double* logq, double* r,
@@ -796,14 +803,14 @@ __global__ __launch_bounds__(1024) void mfw_weights_kernel(int N, int D, int chi
   if (!chivi) {
     double a = 0.0, e = 0.0;
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
-      a += logp[k];
+      a += pd ? logp[k] - logq[k] : logp[k];  // black_box_klvi_pd: sampled log q
       r[k] = -1.0 / N;
     }
     for (int d = threadIdx.x; d < D; d += blockDim.x) e += lam[D + d];
     a = block_sum(a, red);
     e = block_sum(e, red);
     if (threadIdx.x == 0) {
-      *value = -((c0 + e) + a / N);
+      *value = pd ? -(a / N) : -((c0 + e) + a / N);
       scal[1] = -1.0;
     }
     return;
@@ -870,10 +877,10 @@ int mf_wide_value_grad(FrWork* W, const MfSpec& f, const double* lam, const doub
   if (f.tgt == kTargetCorrGauss)
     return vb_set_error(-4, "corr_gauss is implemented for the full-rank family only");
   FR_HIP(launch_target_logdensity(f.tgt, D, N, W->X.d(), W->logp.d(), W->G.d(), st));
-  if (f.chivi)
+  if (f.chivi || f.pd)
     FR_HIP(launch_family_logdensity(f.fam, D, N, lam, f.df, f.t_const, W->X.d(), W->zz.d(), st));
   const double c0 = f.fam == 1 ? 0.0 : 0.5 * D * (1.0 + kLog2Pi);
-  hipLaunchKernelGGL(mfw_weights_kernel, dim3(1), dim3(1024), 0, st, N, D, f.chivi, f.alpha, c0,
+  hipLaunchKernelGGL(mfw_weights_kernel, dim3(1), dim3(1024), 0, st, N, D, f.chivi, f.pd, f.alpha, c0,
                      lam, W->logp.d(), W->zz.d(), W->r.d(), W->scal.d(), value);
   hipLaunchKernelGGL(mfw_grad_kernel, dim3(blocks(D, 64)), dim3(256), 0, st, N, D, lam, W->X.d(),
                      W->G.d(), W->r.d(), W->scal.d(), grad);

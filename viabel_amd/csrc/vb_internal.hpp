@@ -27,6 +27,7 @@ struct LrSched {
 // Arguments of the column-pair persistent KLVI kernel (separable targets).
 struct SepArgs {
   int D, N, W, n_pairs, n_steps, emit_grad;
+  int pd;  // value with the sampled log q (black_box_klvi_pd): 0 off, 1 Gaussian, 2 t family
   long long step0, hist_start;  // local step index of the first step; 3*n_iters//4
   long long rng_step0;          // Philox step counter of the first step
   int n_waves;
@@ -46,6 +47,7 @@ struct SepArgs {
 // Arguments of the block-per-problem kernel (any target, D <= kBlockDMax).
 struct BlockArgs {
   int D, N, W, P, n_steps, emit_grad, chivi;
+  int pd;   // KLVI value -(mean log p - mean log q(x)) (black_box_klvi_pd)
   int opt;  // 0 adagrad window (history: post-update, tail quarter); 1 RMSProp-IA, 2 Adam-IA
             // (state in ring rows 0/1, history: pre-update, last n_hist iterations)
   long long step0, hist_start, n_iters, n_hist, rng_step0;
@@ -112,6 +114,9 @@ hipError_t bounds_centered_moments(const double* x, long long n, long long d,
 hipError_t bounds_covariance(const double* x, long long n, long long d, double* dev_scratch,
                              double* mean_dev, double* cov_dev, hipStream_t s);
 size_t bounds_scratch_doubles(long long n, long long d);
+hipError_t bounds_weighted_covariance(const double* x, long long n, long long d, const double* w,
+                                      double sw, double fact, double* xc_scratch, double* mean,
+                                      double* cov, hipStream_t s);
 constexpr int kCovDMax = 64;
 
 // PSIS (vb_psis.hip)
@@ -142,7 +147,7 @@ FrWork* fr_work_create();
 void fr_work_destroy(FrWork* w);
 
 struct FrSpec {
-  int D, N, tgt, chivi;
+  int D, N, tgt, chivi, pd;
   double df, t_const, alpha;
   const double* tparams;  // device; corr_gauss: P*[D][D]
   double tconst;          // corr_gauss log normaliser
@@ -170,7 +175,7 @@ int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, 
 
 // Mean-field families on the materialised path (any D, any objective / target).
 struct MfSpec {
-  int fam, D, N, tgt, chivi;
+  int fam, D, N, tgt, chivi, pd;
   double alpha, t_scale, shape, df, t_const;
 };
 int mf_wide_value_grad(FrWork* W, const MfSpec& f, const double* lam, const double* host_eps,

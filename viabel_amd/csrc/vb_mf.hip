@@ -158,11 +158,24 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
       }
       double dg;
       const double xA = eA * sA + muA;
-      const double lpA = TGT::lp1(xA, dg);
+      double lpA = TGT::lp1(xA, dg);
       gA += dg;
       hA += dg * eA;
       const double xB = eB * sB + muB;
-      const double lpB = TGT::lp1(xB, dg);
+      double lpB = TGT::lp1(xB, dg);
+      if (a.pd) {
+        // -log q(x) without its per-pair constants: 1/2 eps^2 (Gaussian) or
+        // (df + 1)/2 log1p(eps^2 / df) (t, df = 2 shape)
+        // (the form is a run-time field: host-noise launches do not instantiate TFAM)
+        if (a.pd == 2) {
+          const double df = 2.0 * a.shape;
+          lpA += 0.5 * (df + 1.0) * log1p(eA * eA / df);
+          lpB += 0.5 * (df + 1.0) * log1p(eB * eB / df);
+        } else {
+          lpA += 0.5 * eA * eA;
+          lpB += 0.5 * eB * eB;
+        }
+      }
       v += hasB ? lpA + lpB : lpA;
       gB += dg;
       hB += dg * eB;
@@ -401,7 +414,20 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
         x[d] = e[d] * sg[d] + mu[d];
         g[d] = 0.0;
       }
-      const double lp = Row::template row<DMAX>(x, g, D);
+      double lp = Row::template row<DMAX>(x, g, D);
+      if (a.pd) {
+        // black_box_klvi_pd: accumulate log p - log q(x) (all constants)
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          if (d < D) {
+            const double z = (x[d] - mu[d]) / sg[d];
+            if constexpr (TFAM)
+              lp -= a.t_const - log1p(z * z / a.df) * (0.5 * (a.df + 1.0)) - lsg[d];
+            else
+              lp -= -0.5 * z * z - lsg[d] - 0.5 * kLog2Pi;
+          }
+        }
+      }
       if (!a.chivi) {
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) {
@@ -515,7 +541,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
         // entropy uses the pre-update lam: sum_d log sigma_d
         double sl = 0.0;
         for (int d = 0; d < D; ++d) sl += lsg[d];
-        val = -(c0 + sl + s_red[0][2 * DMAX] / dN);
+        val = a.pd ? -(s_red[0][2 * DMAX] / dN) : -(c0 + sl + s_red[0][2 * DMAX] / dN);
       } else {
         val = log(s_red[0][2 * DMAX] / dN) / a.alpha + M;
       }

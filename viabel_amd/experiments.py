@@ -1,7 +1,9 @@
 """Log-weight producer of the reference's experiment harness, on the device.
 
+  check_accuracy                notebooks/experiments.py:26-48 (host algebra on d x d)
   get_samples_and_log_weights   notebooks/experiments.py:60-63
   psis_correction               notebooks/experiments.py:66-70
+  improve_with_psis             notebooks/experiments.py:73-89
 
 Draws continue the family's stream (numpy mode: fam.rs, as the reference's
 ``var_family.sample(var_param, n_samples)``; philox mode: the family's
@@ -13,7 +15,8 @@ from . import _native as nat
 from .psis import psislw
 from .targets import Target
 
-__all__ = ['get_samples_and_log_weights', 'psis_correction', 'log_weights']
+__all__ = ['get_samples_and_log_weights', 'psis_correction', 'log_weights', 'check_accuracy',
+           'improve_with_psis', 'weighted_mean_and_cov']
 
 
 def log_weights(logdensity, var_family, var_param, n_samples, return_samples=True):
@@ -42,3 +45,61 @@ def psis_correction(logdensity, var_family, var_param, n_samples):
     samples, lw = get_samples_and_log_weights(logdensity, var_family, var_param, n_samples)
     smoothed_log_weights, khat = psislw(lw)
     return samples.T, smoothed_log_weights, khat
+
+
+def weighted_mean_and_cov(samples, weights=None, ddof=1):
+    """Device np.average(samples.T, axis=1, weights) and np.cov(samples.T,
+    aweights=weights, ddof=ddof) for samples [n, d]."""
+    x = nat.as_f64(np.atleast_2d(np.asarray(samples, dtype=float).T).T)
+    n, d = x.shape
+    w = None if weights is None else nat.as_f64(np.ravel(weights))
+    mean = np.empty(d)
+    cov = np.empty((d, d))
+    nat.check(nat.lib().vb_weighted_covariance(nat.context().handle, nat.dptr(x), n, d,
+                                               nat.dptr(w), int(ddof), nat.dptr(mean),
+                                               nat.dptr(cov)))
+    return mean, cov
+
+
+def check_accuracy(true_mean, true_cov, approx_mean, approx_cov, verbose=False, method=None):
+    """experiments.py:26-48: error summaries of an approximate mean / covariance."""
+    true_std = np.sqrt(np.diag(true_cov))
+    approx_std = np.sqrt(np.diag(approx_cov))
+    results = dict(mean_error=np.linalg.norm(true_mean - approx_mean),
+                   cov_error_2=np.linalg.norm(true_cov - approx_cov, ord=2),
+                   cov_norm_2=np.linalg.norm(true_cov, ord=2),
+                   cov_error_nuc=np.linalg.norm(true_cov - approx_cov, ord='nuc'),
+                   cov_norm_nuc=np.linalg.norm(true_cov, ord='nuc'),
+                   std_error=np.linalg.norm(true_std - approx_std),
+                   rel_std_error=np.linalg.norm(approx_std / true_std - 1))
+    if method is not None:
+        results['method'] = method
+    if verbose:
+        print('mean   =', approx_mean)
+        print('stdevs =', approx_std)
+        print()
+        print('mean error             = {:.3g}'.format(results['mean_error']))
+        print('stdev error            = {:.3g}'.format(results['std_error']))
+        print('||cov error||_2^{{1/2}}  = {:.3g}'.format(np.sqrt(results['cov_error_2'])))
+        print('||true cov||_2^{{1/2}}   = {:.3g}'.format(np.sqrt(results['cov_norm_2'])))
+    return results
+
+
+def improve_with_psis(logdensity, var_family, var_param, n_samples, true_mean, true_cov,
+                      transform=None, verbose=False):
+    """experiments.py:73-89: PSIS-reweighted mean and covariance (ddof 0) of
+    n_samples draws from q; the draws, log weights, PSIS and the weighted
+    moments run on the device (a user `transform` runs on the host)."""
+    samples, slw, khat = psis_correction(logdensity, var_family, var_param, n_samples)
+    if verbose:
+        print('khat = {:.3g}'.format(khat))
+        print()
+    if transform is not None:
+        samples = transform(samples)
+    slw = slw - np.max(slw)
+    wts = np.exp(slw)
+    wts /= np.sum(wts)
+    approx_mean, approx_cov = weighted_mean_and_cov(np.asarray(samples).T, wts, ddof=0)
+    res = check_accuracy(true_mean, true_cov, approx_mean, approx_cov, verbose)
+    res['khat'] = khat
+    return res, approx_mean, approx_cov

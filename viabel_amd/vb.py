@@ -8,6 +8,7 @@ error messages) for the hot path:
   t_variational_family (full rank)        vb.py:185-233, _distributions.py:8-38
   black_box_klvi                          vb.py:236-245
   black_box_chivi                         vb.py:248-266
+  black_box_klvi_pd / black_box_klvi_pd2  vb.py:268-295
   learning_rate_schedule                  vb.py:324-342
   adagrad_optimize                        vb.py:345-389
   rmsprop_IA_optimize_with_rhat           vb.py:392-553
@@ -43,6 +44,8 @@ __all__ = [
     't_variational_family',
     'black_box_klvi',
     'black_box_chivi',
+    'black_box_klvi_pd',
+    'black_box_klvi_pd2',
     'learning_rate_schedule',
     'adagrad_optimize',
     'rmsprop_IA_optimize_with_rhat',
@@ -288,8 +291,8 @@ class NativeObjective:
     def _eps_one_call(self):
         """Host draws for one call, in the reference's order (numpy mode)."""
         fam = self.family
-        if self.kind == nat.OBJ_KLVI:
-            return fam._draw(self.n_samples)                        # vb.py:239
+        if self.kind != nat.OBJ_CHIVI:
+            return fam._draw(self.n_samples)                        # vb.py:239, 271
         seed = np.random.randint(2 ** 32)                           # vb.py:258
         return fam._draw(self.n_samples, seed)                      # vb.py:251
 
@@ -322,6 +325,19 @@ def black_box_klvi(var_family, logdensity, n_samples):
 def black_box_chivi(alpha, var_family, logdensity, n_samples):
     """vb.py:248-266: returns objective_and_grad(var_param) -> (CUBO, grad)."""
     return NativeObjective(nat.OBJ_CHIVI, var_family, logdensity, n_samples, alpha)
+
+
+def black_box_klvi_pd(var_family, logdensity, n_samples):
+    """vb.py:268-278: value -(mean log p - mean log q(x)) on the family's draws;
+    autograd differentiates log q through x and lambda, whose total derivative
+    reduces to the entropy's, so the gradient is black_box_klvi's."""
+    return NativeObjective(nat.OBJ_KLVI_PD, var_family, logdensity, n_samples)
+
+
+def black_box_klvi_pd2(var_family, logdensity, n_samples):
+    """vb.py:281-295: the same objective written with a partial over var_param
+    (autograd still differentiates through it): identical value and gradient."""
+    return NativeObjective(nat.OBJ_KLVI_PD, var_family, logdensity, n_samples)
 
 
 def learning_rate_schedule(n_iters, learning_rate, learning_rate_end):
