@@ -71,9 +71,18 @@ enum vb_target_kind {
   VB_TARGET_MIXTURE = 1,        /* prod_d 0.5 N(-2,1) + 0.5 N(2,1)            (separable) */
   VB_TARGET_FUNNEL = 2,         /* Neal's funnel, x[1] = log sigma ~ N(0,1.35^2)           */
   VB_TARGET_EIGHT_SCHOOLS_NCP = 3, /* eight_schools_ncp.stan log_prob, D = 10              */
-  VB_TARGET_CORR_GAUSS = 4    /* N(0, Sigma*): params = [inv(Sigma*) (D x D row-major),
+  VB_TARGET_CORR_GAUSS = 4,   /* N(0, Sigma*): params = [inv(Sigma*) (D x D row-major),
                                  log normaliser]; full-rank family only (SURVEY §8d cfg 4) */
+  VB_TARGET_CALLBACK = 5      /* user model through vb_target.callback (make_stan_log_density,
+                                 vb.py:314-321): evaluated on the host once per step on the
+                                 batch of samples; everything else stays on the device */
 };
+
+/* User target: log p and d log p / dx of the n rows of x [n][d] (HOST memory,
+ * C order) into logp [n] and grad [n][d]; return 0, or non-zero to abort the
+ * call with VB_EDEVICE. */
+typedef int (*vb_target_callback)(void* user, const double* x, int64_t n, int64_t d,
+                                  double* logp, double* grad);
 
 enum vb_objective_kind {
   VB_OBJ_KLVI = 0,     /* value = -(entropy + mean log p)              vb.py:236-245 */
@@ -100,6 +109,8 @@ typedef struct vb_target {
   int64_t dim;    /* D (must equal the family's) */
   const double* params; /* target parameters (host or device), NULL if none */
   int64_t n_params;
+  vb_target_callback callback; /* VB_TARGET_CALLBACK only */
+  void* user;
 } vb_target;
 
 typedef struct vb_objective {

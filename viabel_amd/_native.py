@@ -17,6 +17,7 @@ VB_OK, VB_EINVAL, VB_EDEVICE, VB_ENOMEM, VB_EUNSUPPORTED = 0, -1, -2, -3, -4
 FAMILY_MF_GAUSSIAN, FAMILY_MF_T, FAMILY_FR_T = 0, 1, 2
 TARGET_ISOGAUSS, TARGET_MIXTURE, TARGET_FUNNEL, TARGET_EIGHT_SCHOOLS_NCP = 0, 1, 2, 3
 TARGET_CORR_GAUSS = 4
+TARGET_CALLBACK = 5
 OBJ_KLVI, OBJ_CHIVI, OBJ_KLVI_PD = 0, 1, 2
 OPT_ADAGRAD, OPT_RMSPROP_IA, OPT_ADAM_IA = 0, 1, 2
 NOISE_HOST, NOISE_PHILOX = 0, 1
@@ -30,9 +31,15 @@ class Family(ctypes.Structure):
                 ('dim', ctypes.c_int64), ('df', ctypes.c_double)]
 
 
+# vb_target_callback: (user, x, n, d, logp, grad) -> int, host pointers
+TARGET_CALLBACK_T = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, c_double_p, ctypes.c_int64,
+                                     ctypes.c_int64, c_double_p, c_double_p)
+
+
 class Target(ctypes.Structure):
     _fields_ = [('kind', ctypes.c_int32), ('reserved', ctypes.c_int32), ('dim', ctypes.c_int64),
-                ('params', c_double_p), ('n_params', ctypes.c_int64)]
+                ('params', c_double_p), ('n_params', ctypes.c_int64),
+                ('callback', TARGET_CALLBACK_T), ('user', ctypes.c_void_p)]
 
 
 class Objective(ctypes.Structure):
@@ -127,7 +134,15 @@ def lib():
     return _lib
 
 
+# exceptions raised inside a Python target callback, re-raised after the call
+PENDING_CALLBACK_ERRORS = []
+
+
 def check(rc):
+    if PENDING_CALLBACK_ERRORS:
+        err = PENDING_CALLBACK_ERRORS.pop()
+        PENDING_CALLBACK_ERRORS.clear()
+        raise err
     if rc == VB_OK:
         return
     msg = lib().vb_last_error().decode('utf-8', 'replace')

@@ -204,8 +204,10 @@ int check_family(const vb_family* f, FamInfo* o) {
 
 int check_target(const vb_target* t, int D) {
   if (!t) return fail(VB_EINVAL, "null vb_target");
-  if (t->kind < VB_TARGET_ISOGAUSS || t->kind > VB_TARGET_CORR_GAUSS)
+  if (t->kind < VB_TARGET_ISOGAUSS || t->kind > VB_TARGET_CALLBACK)
     return fail(VB_EUNSUPPORTED, "target kind %d is not implemented on the device", t->kind);
+  if (t->kind == VB_TARGET_CALLBACK && !t->callback)
+    return fail(VB_EINVAL, "callback target needs a callback");
   if (t->kind == VB_TARGET_CORR_GAUSS &&
       (!t->params || t->n_params != (int64_t)t->dim * t->dim + 1))
     return fail(VB_EINVAL, "corr_gauss target needs D*D + 1 parameters (precision, log normaliser)");
@@ -250,9 +252,19 @@ int require_fr(int fam_kind, int tgt_kind) {
   return VB_OK;
 }
 
+vbk::HostTarget host_of(const vb_target* t) {
+  vbk::HostTarget h{};
+  if (t && t->kind == VB_TARGET_CALLBACK) {
+    h.fn = t->callback;
+    h.user = t->user;
+  }
+  return h;
+}
+
 vbk::FrSpec fr_spec(const FamInfo& fi, const vb_target* tgt, const vb_objective* obj,
                     const double* tparams, double tconst) {
   vbk::FrSpec f{};
+  f.host = host_of(tgt);
   f.D = fi.D;
   f.N = (int)obj->n_samples;
   f.tgt = tgt->kind;
@@ -277,6 +289,7 @@ double sep_c0(const FamInfo& fi, bool pd) {
 
 vbk::MfSpec mf_spec(const FamInfo& fi, const vb_target* tgt, const vb_objective* obj) {
   vbk::MfSpec f{};
+  f.host = host_of(tgt);
   f.fam = fi.kind;
   f.D = fi.D;
   f.N = obj ? (int)obj->n_samples : 0;
@@ -498,7 +511,12 @@ int vb_target_logdensity(vb_ctx* c, const vb_target* tgt, const double* x, int64
   VB_TRY(dxx.stage(c, 0, x, (size_t)n * D));
   VB_TRY(dout.stage(c, 1, out, (size_t)n));
   VB_TRY(dg.stage(c, 2, grad_out, grad_out ? (size_t)n * D : 0));
-  if (tgt->kind == VB_TARGET_CORR_GAUSS) {
+  if (tgt->kind == VB_TARGET_CALLBACK) {
+    if (n == 0) return VB_OK;
+    vbk::FrWork* W;
+    VB_TRY(fr_work(c, &W));
+    VB_TRY(vbk::host_target_eval(W, host_of(tgt), D, n, dxx.d, dout.d, dg.d, c->stream));
+  } else if (tgt->kind == VB_TARGET_CORR_GAUSS) {
     if (n == 0) return VB_OK;
     const double* tp;
     double tc;
@@ -551,6 +569,7 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
 
   const bool pd = obj->kind == VB_OBJ_KLVI_PD;
   const bool sep = vbk::target_separable(tgt->kind) && obj->kind != VB_OBJ_CHIVI;
+  const bool cb = tgt->kind == VB_TARGET_CALLBACK;
   if (sep && D > vbk::kBlockDMax) {
     vbk::SepArgs a{};
     a.D = D;
@@ -576,7 +595,7 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
     a.stream = noise->stream;
     VB_HIP(vbk::launch_sep(fi.kind, tgt->kind, host, a, c->stream));
     VB_HIP(vbk::launch_sep_values(a.vpart, 1, a.n_waves, sep_c0(fi, pd), dval, c->stream));
-  } else if (D <= vbk::kBlockDMax) {
+  } else if (D <= vbk::kBlockDMax && !cb) {
     vbk::BlockArgs a{};
     a.D = D;
     a.N = N;
@@ -676,7 +695,8 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
                    (D > vbk::kBlockDMax);
   // D > kBlockDMax without the fused kernel (CHIVI, non-separable targets, IA
   // optimisers): the materialised mean-field path, one problem per run
-  const bool wide = !fr && D > vbk::kBlockDMax && (!sep || ia);
+  const bool wide = !fr && ((D > vbk::kBlockDMax && (!sep || ia)) ||
+                            tgt->kind == VB_TARGET_CALLBACK);
   if (wide && n_problems != 1)
     return fail(VB_EUNSUPPORTED, "wide (D > %d) runs hold one problem per vb_run", vbk::kBlockDMax);
   if (sep && n_problems != 1)
@@ -985,6 +1005,7 @@ int vb_log_weights(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const 
     double tc;
     VB_TRY(target_params(c, 4, tgt, &tp, &tc));
     vbk::FrSpec f{};
+    f.host = host_of(tgt);
     f.D = fi.D;
     f.tgt = tgt->kind;
     f.df = fi.df;
@@ -1001,7 +1022,8 @@ int vb_log_weights(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const 
     VB_TRY(dxs.finish(c));
     return sync(c);
   }
-  if (!vbk::target_separable(tgt->kind) && fi.D > vbk::kBlockDMax) {
+  if ((!vbk::target_separable(tgt->kind) && fi.D > vbk::kBlockDMax) ||
+      tgt->kind == VB_TARGET_CALLBACK) {
     const bool host = noise->kind == VB_NOISE_HOST;
     if (host && !noise->eps) return fail(VB_EINVAL, "host noise requires eps");
     if (m == 0) return VB_OK;

@@ -417,9 +417,14 @@ struct FrWork {
   double c = 0.0;              // its scaling (~1.25 lambda_max)
   // N x D / N
   Buf Z, X, G, s, logp, zz, r, rk;
+  // pinned host staging for host-callback targets
+  double *hx = nullptr, *hlp = nullptr, *hg = nullptr;
+  size_t hcap = 0;
   ~FrWork() {
     if (blas) rocblas_destroy_handle(blas);
     if (host_res) (void)hipHostFree(host_res);
+    for (double* p : {hx, hlp, hg})
+      if (p) (void)hipHostFree(p);
   }
 };
 
@@ -477,6 +482,39 @@ int reserve_n(FrWork* W, int D, long long n) {
   return 0;
 }
 
+}  // namespace
+
+int host_target_eval(FrWork* W, const HostTarget& t, int D, long long n, const double* x,
+                     double* logp, double* grad, hipStream_t st) {
+  if (!t.fn) return vb_set_error(-1, "callback target without a callback");
+  const size_t nd = (size_t)n * D;
+  if (nd > W->hcap || (size_t)n > W->hcap) {
+    for (double** p : {&W->hx, &W->hlp, &W->hg}) {
+      if (*p) (void)hipHostFree(*p);
+      *p = nullptr;
+    }
+    W->hcap = 0;
+    const size_t cap = std::max(nd, (size_t)n);
+    for (double** p : {&W->hx, &W->hlp, &W->hg}) FR_HIP(hipHostMalloc(p, sizeof(double) * cap));
+    W->hcap = cap;
+  }
+  FR_HIP(hipMemcpyAsync(W->hx, x, sizeof(double) * nd, hipMemcpyDefault, st));
+  FR_HIP(hipStreamSynchronize(st));
+  const int rc = t.fn(t.user, W->hx, (int64_t)n, (int64_t)D, W->hlp, W->hg);
+  if (rc != 0) return vb_set_error(-2, "target callback returned %d", rc);
+  FR_HIP(hipMemcpyAsync(logp, W->hlp, sizeof(double) * n, hipMemcpyDefault, st));
+  if (grad) FR_HIP(hipMemcpyAsync(grad, W->hg, sizeof(double) * nd, hipMemcpyDefault, st));
+  // the staging buffers are reused by the next call, which synchronises first
+  return 0;
+}
+
+namespace {
+int eval_target(FrWork* W, int tgt, const HostTarget& host, int D, long long n, const double* x,
+                double* logp, double* grad, hipStream_t st) {
+  if (tgt == kTargetCallback) return host_target_eval(W, host, D, n, x, logp, grad, st);
+  FR_HIP(launch_target_logdensity(tgt, D, n, x, logp, grad, st));
+  return 0;
+}
 }  // namespace
 
 // L, eigh(L L^T) -> (w ascending, Vt rows = eigenvectors), half log det from the
@@ -698,7 +736,7 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
                        (f.chivi || f.pd) ? z : nullptr, W->X.d(), W->G.d(), f.tconst, 1, W->zz.d(),
                        W->logp.d());
   } else {
-    FR_HIP(launch_target_logdensity(f.tgt, D, N, W->X.d(), W->logp.d(), W->G.d(), st));
+    if (int rc = eval_target(W, f.tgt, f.host, D, N, W->X.d(), W->logp.d(), W->G.d(), st)) return rc;
     if (f.chivi || f.pd)
       hipLaunchKernelGGL(fr_rows_kernel, dim3(blocks(N, 4)), dim3(256), 0, st, D, (long long)N,
                          z, nullptr, nullptr, 0.0, 0, W->zz.d(), nullptr);
@@ -753,7 +791,7 @@ int fr_log_weights(FrWork* W, const FrSpec& f, const double* lam, long long m,
     hipLaunchKernelGGL(fr_rows_kernel, dim3(blocks(m, 4)), dim3(256), 0, st, D, m, z, x, W->G.d(),
                        f.tconst, 1, W->zz.d(), W->logp.d());
   } else {
-    FR_HIP(launch_target_logdensity(f.tgt, D, m, x, W->logp.d(), nullptr, st));
+    if (int rc = eval_target(W, f.tgt, f.host, D, m, x, W->logp.d(), nullptr, st)) return rc;
     hipLaunchKernelGGL(fr_rows_kernel, dim3(blocks(m, 4)), dim3(256), 0, st, D, m, z, nullptr,
                        nullptr, 0.0, 0, W->zz.d(), nullptr);
   }
@@ -876,7 +914,7 @@ int mf_wide_value_grad(FrWork* W, const MfSpec& f, const double* lam, const doub
                        W->X.d(), st));
   if (f.tgt == kTargetCorrGauss)
     return vb_set_error(-4, "corr_gauss is implemented for the full-rank family only");
-  FR_HIP(launch_target_logdensity(f.tgt, D, N, W->X.d(), W->logp.d(), W->G.d(), st));
+  if (int rc = eval_target(W, f.tgt, f.host, D, N, W->X.d(), W->logp.d(), W->G.d(), st)) return rc;
   if (f.chivi || f.pd)
     FR_HIP(launch_family_logdensity(f.fam, D, N, lam, f.df, f.t_const, W->X.d(), W->zz.d(), st));
   const double c0 = f.fam == 1 ? 0.0 : 0.5 * D * (1.0 + kLog2Pi);
@@ -905,7 +943,7 @@ int mf_wide_log_weights(FrWork* W, const MfSpec& f, const double* lam, long long
   if (int rc = reserve_n(W, D, m)) return rc;
   double* x = xs ? xs : W->X.d();
   FR_HIP(launch_sample(f.fam, D, m, lam, f.t_scale, f.shape, host_eps, k0, k1, stream, step, x, st));
-  FR_HIP(launch_target_logdensity(f.tgt, D, m, x, W->logp.d(), nullptr, st));
+  if (int rc = eval_target(W, f.tgt, f.host, D, m, x, W->logp.d(), nullptr, st)) return rc;
   FR_HIP(launch_family_logdensity(f.fam, D, m, lam, f.df, f.t_const, x, W->zz.d(), st));
   hipLaunchKernelGGL(sub_kernel, dim3(blocks(m)), dim3(256), 0, st, m, W->logp.d(), W->zz.d(), lw);
   FR_HIP(hipGetLastError());

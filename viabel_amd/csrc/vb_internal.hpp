@@ -140,6 +140,17 @@ int vb_set_error(int code, const char* fmt, ...);  // defined in vb_capi.hip
 
 constexpr int kFamilyFrT = 2;
 constexpr int kTargetCorrGauss = 4;
+constexpr int kTargetCallback = 5;
+// host model callback (vb_target_callback) + its user pointer
+struct HostTarget {
+  int (*fn)(void* user, const double* x, int64_t n, int64_t d, double* logp, double* grad);
+  void* user;
+};
+struct FrWork;
+// Evaluate a host target on device x [n][D] into device logp [n] / grad [n][D]
+// (grad nullable): staged through pinned buffers of the workspace; synchronises.
+int host_target_eval(FrWork* W, const HostTarget& t, int D, long long n, const double* x,
+                     double* logp, double* grad, hipStream_t st);
 
 
 struct FrWork;  // per-context workspace + rocBLAS handle
@@ -151,6 +162,7 @@ struct FrSpec {
   double df, t_const, alpha;
   const double* tparams;  // device; corr_gauss: P*[D][D]
   double tconst;          // corr_gauss log normaliser
+  HostTarget host;        // tgt == kTargetCallback
 };
 
 // All return 0 or a VB_E* code (message via vb_set_error).
@@ -177,6 +189,7 @@ int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, 
 struct MfSpec {
   int fam, D, N, tgt, chivi, pd;
   double alpha, t_scale, shape, df, t_const;
+  HostTarget host;  // tgt == kTargetCallback
 };
 int mf_wide_value_grad(FrWork* W, const MfSpec& f, const double* lam, const double* host_eps,
                        uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,

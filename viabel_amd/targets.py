@@ -14,12 +14,20 @@ Targets:
   eight_schools_ncp()    eight_schools_ncp.stan log_prob (D = 10)   eight-schools.ipynb
   corr_gauss(D)          N(0, A A^T / D + I), A = RandomState(512).randn(D, D)
                          (full-rank family)
+
+User models (the reference's make_stan_log_density, vb.py:314-321, and autograd
+callables): callback(fn, D), from_stan(fit, D) and torch_target(f, D) evaluate
+the model on the HOST once per optimisation step on the whole batch of samples
+(VB_TARGET_CALLBACK); sampling, weights, gradient reductions and the optimiser
+stay on the device.  This is the model boundary, not a fallback of the VI
+computation: the model is the user's code and runs where that code runs.
 """
 import numpy as np
 
 from . import _native as nat
 
-__all__ = ['Target', 'isogauss', 'mixture', 'funnel', 'eight_schools_ncp', 'corr_gauss']
+__all__ = ['Target', 'isogauss', 'mixture', 'funnel', 'eight_schools_ncp', 'corr_gauss',
+           'callback', 'from_stan', 'torch_target']
 
 
 class Target:
@@ -27,14 +35,17 @@ class Target:
         self.kind, self.dim, self.name = int(kind), int(dim), name
         self.params = None if params is None else nat.as_f64(params)
 
+    _cfunc = None   # ctypes callback of a host target (kept alive with the target)
+
     @property
     def separable(self):
         return self.kind in (nat.TARGET_ISOGAUSS, nat.TARGET_MIXTURE)
 
     def _struct(self):
+        cb = self._cfunc if self._cfunc is not None else nat.TARGET_CALLBACK_T()
         if self.params is None:
-            return nat.Target(self.kind, 0, self.dim, None, 0)
-        return nat.Target(self.kind, 0, self.dim, nat.dptr(self.params), self.params.size)
+            return nat.Target(self.kind, 0, self.dim, None, 0, cb, None)
+        return nat.Target(self.kind, 0, self.dim, nat.dptr(self.params), self.params.size, cb, None)
 
     def logdensity_and_grad(self, x):
         x = nat.as_f64(np.atleast_2d(x))
@@ -86,3 +97,49 @@ def corr_gauss(dim, seed=512):
     t = Target(nat.TARGET_CORR_GAUSS, dim, 'corr_gauss', np.concatenate([prec.ravel(), [const]]))
     t.sigma = sigma
     return t
+
+
+def callback(logdensity_and_grad, dim, name='callback'):
+    """A user model: logdensity_and_grad(x) -> (log p (n,), d log p / dx (n, d)) for
+    x of shape (n, dim) (numpy, host)."""
+    dim = int(dim)
+
+    def _cb(user, xp, n, d, lpp, gp):
+        try:
+            x = np.ctypeslib.as_array(xp, shape=(n, d)).copy()
+            lp, g = logdensity_and_grad(x)
+            np.ctypeslib.as_array(lpp, shape=(n,))[:] = np.asarray(lp, dtype=float).reshape(n)
+            np.ctypeslib.as_array(gp, shape=(n, d))[:] = np.asarray(g, dtype=float).reshape(n, d)
+            return 0
+        except BaseException as e:          # re-raised by _native.check after the call
+            nat.PENDING_CALLBACK_ERRORS.append(e)
+            return 1
+
+    t = Target(nat.TARGET_CALLBACK, dim, name)
+    t._cfunc = nat.TARGET_CALLBACK_T(_cb)
+    t.fn = logdensity_and_grad
+    return t
+
+
+def from_stan(fitobj, dim):
+    """make_stan_log_density (vb.py:314-321): log_prob / grad_log_prob of a fitted
+    Stan model (pystan 2 fit object), applied row by row on the host."""
+    def f(x):
+        lp = np.array([fitobj.log_prob(row) for row in x])
+        g = np.array([fitobj.grad_log_prob(row) for row in x])
+        return lp, g
+    return callback(f, dim, 'stan')
+
+
+def torch_target(logdensity, dim, device=None):
+    """A model written in torch: logdensity(x: tensor (n, dim)) -> (n,); the
+    gradient comes from torch.autograd (on `device`, default the GPU when present)."""
+    import torch
+    dev = torch.device(device if device is not None else ('cuda' if torch.cuda.is_available() else 'cpu'))
+
+    def f(x):
+        xt = torch.tensor(x, dtype=torch.float64, device=dev, requires_grad=True)
+        lp = logdensity(xt)
+        g, = torch.autograd.grad(lp.sum(), xt)
+        return lp.detach().cpu().numpy(), g.cpu().numpy()
+    return callback(f, dim, 'torch')

@@ -275,8 +275,10 @@ class NativeObjective:
             raise TypeError('var_family must come from viabel_amd.vb')
         if not isinstance(logdensity, Target):
             raise TypeError(
-                'the device estimator needs a viabel_amd.targets target as logdensity '
-                '(arbitrary Python callables cannot run in a HIP kernel); got %r' % (logdensity,))
+                'the device estimator needs a viabel_amd.targets target as logdensity: a '
+                'built-in device target, or a user model wrapped with targets.callback / '
+                'targets.from_stan / targets.torch_target (an autograd callable cannot be '
+                'differentiated here); got %r' % (logdensity,))
         if logdensity.dim != var_family.dim:
             raise ValueError('target dimension %d != family dimension %d'
                              % (logdensity.dim, var_family.dim))
