@@ -552,7 +552,7 @@ int frob2(FrWork* W, int n, const double* X, double shift, double* out, hipStrea
 //   T_k = 3I - Z_k Y_k,  Y_{k+1} = Y_k T_k / 2,  Z_{k+1} = T_k Z_k / 2
 //   Y_k -> (Sigma / c)^{1/2},  Z_k -> (Sigma / c)^{-1/2}.
 // The iterates are kept for the tangent (Sylvester) pass.  Converged when
-// ||I - Z_k Y_k||_F <= 1e-12 sqrt(D) or has stalled at rounding level; the host
+// ||I - Z_k Y_k||_F <= 1e-10 sqrt(D) or has stalled at rounding level; the host
 // reads the residuals at most once per iteration after the previous root's count.
 // Also: L, Sigma = L L^T, scal[0] = 0.5 log det Sigma = sum log L_ii.
 int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st) {
@@ -565,12 +565,12 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st) {
   double* res = W->res.d();
   const int KM = FrWork::kNSMax;
   if (int rc = frob2(W, D, W->Sig.d(), 0.0, res + KM, st)) return rc;
-  // lambda_max estimate: 8 power steps (vectors in the sq / offd / w scratch)
+  // lambda_max estimate: 6 power steps (vectors in the sq / offd / w scratch)
   {
     const unsigned nb = (unsigned)((D + 7) / 8);
     double *xa = W->sq.d(), *xb = W->offd.d();
     hipLaunchKernelGGL(fr_power_kernel, dim3(nb), dim3(256), 0, st, D, W->Sig.d(), nullptr, xa);
-    for (int p = 1; p < 8; ++p) {
+    for (int p = 1; p < 5; ++p) {
       hipLaunchKernelGGL(fr_power_kernel, dim3(nb), dim3(256), 0, st, D, W->Sig.d(), xa, xb);
       std::swap(xa, xb);
     }
@@ -582,7 +582,9 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st) {
   hipLaunchKernelGGL(fr_ns_init_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, W->Sig.d(), res + KM,
                      W->nsY[0].d(), W->nsZ[0].d(), res + KM + 2);
   const int kmin = std::max(2, W->K_prev);
-  const double tol = 1e-12 * std::sqrt((double)D), stall = 1e-8 * std::sqrt((double)D);
+  // ||I - Z Y||_F <= 1e-10 sqrt(D): S = sqrt(c) Y_K to ~1e-10 relative (the parity bar is
+  // 1e-5; the tests hold gradients to 1e-8 of the scipy sqrtm / solve_sylvester oracle)
+  const double tol = 1e-10 * std::sqrt((double)D), stall = 1e-8 * std::sqrt((double)D);
   int K = -1;
   for (int k = 0; k < KM; ++k) {
     FR_HIP(W->nsT[k].reserve(bytes));
@@ -604,8 +606,9 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st) {
     if (k + 1 >= KM) break;
     FR_HIP(W->nsY[k + 1].reserve(bytes));
     FR_HIP(W->nsZ[k + 1].reserve(bytes));
-    FR_HIP(gemm(mm(D, D, D, W->nsY[k].d(), false, W->nsT[k].d(), false, W->nsY[k + 1].d(), 0.5), st));
-    FR_HIP(gemm(mm(D, D, D, W->nsT[k].d(), false, W->nsZ[k].d(), false, W->nsZ[k + 1].d(), 0.5), st));
+    const GemmOp yz[2] = {mm(D, D, D, W->nsY[k].d(), false, W->nsT[k].d(), false, W->nsY[k + 1].d(), 0.5),
+                          mm(D, D, D, W->nsT[k].d(), false, W->nsZ[k].d(), false, W->nsZ[k + 1].d(), 0.5)};
+    FR_HIP(gemm_group(yz, 2, st));
   }
   if (K < 0)
     return vb_set_error(-2, "Newton-Schulz square root of Sigma did not converge in %d iterations "
@@ -631,11 +634,19 @@ int fr_sylvester(FrWork* W, int D, double* H, hipStream_t st) {
   hipLaunchKernelGGL(fr_symscale_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, W->GS.d(), cdev,
                      W->dY.d());
   double *dY = W->dY.d(), *dZ = W->dZ.d(), *dYn = W->dYn.d(), *dZn = W->dZn.d(), *dT = W->dT.d();
+  // a dual product: alpha (A B + A2 B2), accumulated in one pass over K
+  auto dual = [&](const double* A, const double* B, const double* A2, const double* B2, double* C,
+                  double alpha) {
+    GemmOp g = mm(D, D, D, A, false, B, false, C, alpha);
+    g.A2 = A2;
+    g.B2 = B2;
+    g.alpha2 = alpha;
+    return g;
+  };
   // k = 0: Z_0 = I, dZ_0 = 0, dT_0 = -dY_0
   {
-    FR_HIP(gemm(mm(D, D, D, dY, false, W->nsT[0].d(), false, dYn, 0.5), st));
-    GemmOp g = mm(D, D, D, W->nsY[0].d(), false, dY, false, dYn, -0.5);
-    g.beta = 1.0;
+    GemmOp g = dual(dY, W->nsT[0].d(), W->nsY[0].d(), dY, dYn, 0.5);
+    g.alpha2 = -0.5;
     FR_HIP(gemm(g, st));
     hipLaunchKernelGGL(fr_axpby_kernel, dim3(blocks(dd)), dim3(256), 0, st, dd, -0.5, dY, dZn);
     std::swap(dY, dYn);
@@ -643,20 +654,10 @@ int fr_sylvester(FrWork* W, int D, double* H, hipStream_t st) {
   }
   for (int k = 1; k <= K; ++k) {
     const double *Yk = W->nsY[k].d(), *Zk = W->nsZ[k].d(), *Tk = W->nsT[k].d();
-    FR_HIP(gemm(mm(D, D, D, dZ, false, Yk, false, dT, -1.0), st));
-    GemmOp g = mm(D, D, D, Zk, false, dY, false, dT, -1.0);
-    g.beta = 1.0;
-    FR_HIP(gemm(g, st));
-    FR_HIP(gemm(mm(D, D, D, dY, false, Tk, false, dYn, 0.5), st));
-    g = mm(D, D, D, Yk, false, dT, false, dYn, 0.5);
-    g.beta = 1.0;
-    FR_HIP(gemm(g, st));
-    if (k < K) {
-      FR_HIP(gemm(mm(D, D, D, dT, false, Zk, false, dZn, 0.5), st));
-      g = mm(D, D, D, Tk, false, dZ, false, dZn, 0.5);
-      g.beta = 1.0;
-      FR_HIP(gemm(g, st));
-    }
+    FR_HIP(gemm(dual(dZ, Yk, Zk, dY, dT, -1.0), st));                 // dT
+    const GemmOp yz[2] = {dual(dY, Tk, Yk, dT, dYn, 0.5),              // dY_{k+1}
+                          dual(dT, Zk, Tk, dZ, dZn, 0.5)};             // dZ_{k+1}
+    FR_HIP(gemm_group(yz, k < K ? 2 : 1, st));
     std::swap(dY, dYn);
     std::swap(dZ, dZn);
   }

@@ -34,6 +34,17 @@ struct GemmOp {
   const double* row_div;   // [M] or null
   const double* col_bias;  // [N] or null
   double diag;             // added to C[i][i] (after the bias)
+  // optional second product accumulated into the same C (same shapes, leading
+  // dimensions and transposes): C = alpha op(A) op(B) + alpha2 op(A2) op(B2) ...
+  const double* A2;
+  const double* B2;
+  double alpha2;
+};
+
+// Up to two independent GEMMs of equal shape / transposes in one launch
+// (blockIdx.z selects the problem).
+struct GemmGroup {
+  GemmOp op[2];
 };
 
 namespace gemm_detail {
@@ -87,8 +98,9 @@ __device__ __forceinline__ double frag(const double* s, int r, int k) {
   return KCONTIG ? s[r * SR + k] : s[k * SK + r];
 }
 
-template <bool TA, bool TB, bool KS>
-__global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmOp g) {
+template <bool TA, bool TB, bool KS, bool DUAL>
+__global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
+  const GemmOp& g = gg.op[blockIdx.z];
   // A is k-contiguous when not transposed; B is k-contiguous when transposed.
   constexpr bool AK = !TA, BK = TB;
   __shared__ double sA[2][BUF];
@@ -97,28 +109,45 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmOp g) {
   const int q = w & 3, h = w >> 2;           // output quadrant, k half of each tile
   const int wm = q >> 1, wn = q & 1;
   const int i0 = blockIdx.y * BT, j0 = blockIdx.x * BT;
-  const int nt = (g.K + KT - 1) / KT;
+  const int nt1 = (g.K + KT - 1) / KT;
+  const int nt = DUAL ? 2 * nt1 : nt1;   // the second product's tiles follow the first's
+  // tile `it` of the virtual k range: operands and k offset
+  auto src_a = [&](int it) { return (DUAL && it >= nt1) ? g.A2 : g.A; };
+  auto src_b = [&](int it) { return (DUAL && it >= nt1) ? g.B2 : g.B; };
+  auto koff = [&](int it) { return (DUAL && it >= nt1 ? it - nt1 : it) * KT; };
   // two register stages: tile it+2 is loaded while tile it feeds the MFMAs
   // and tile it+1 (loaded one iteration earlier) moves to LDS
   Tile<AK, KS> ta0, ta1;
   Tile<BK, false> tb0, tb1;
-  ta0.load(g.A, g.lda, i0, 0, g.M, g.K, g.kscale, t);
-  tb0.load(g.B, g.ldb, j0, 0, g.N, g.K, nullptr, t);
+  ta0.load(src_a(0), g.lda, i0, koff(0), g.M, g.K, g.kscale, t);
+  tb0.load(src_b(0), g.ldb, j0, koff(0), g.N, g.K, nullptr, t);
   if (nt > 1) {
-    ta1.load(g.A, g.lda, i0, KT, g.M, g.K, g.kscale, t);
-    tb1.load(g.B, g.ldb, j0, KT, g.N, g.K, nullptr, t);
+    ta1.load(src_a(1), g.lda, i0, koff(1), g.M, g.K, g.kscale, t);
+    tb1.load(src_b(1), g.ldb, j0, koff(1), g.N, g.K, nullptr, t);
   }
   ta0.store(sA[0], t);
   tb0.store(sB[0], t);
   __syncthreads();
   // four independent accumulator chains (interleaved k4 steps): one dependent
   // f64 MFMA chain per wave is latency-bound on gfx950
-  d4 acc[4];
+  d4 acc[4], acc2[DUAL ? 4 : 1];
 #pragma unroll
   for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < (DUAL ? 4 : 1); ++c) acc2[c] = d4{0.0, 0.0, 0.0, 0.0};
   const int ra = wm * 16 + (lane & 15), cb = wn * 16 + (lane & 15), kq = lane >> 4;
   const int kb = h * (KT / 2);
-  auto mma = [&](const double* a_s, const double* b_s) {
+  auto mma = [&](const double* a_s, const double* b_s, int it) {
+    if (DUAL && it >= nt1) {
+#pragma unroll
+      for (int s = 0; s < KT / 8; ++s) {
+        const int kk = kb + 4 * s;
+        const double a = frag<AK>(a_s, ra, kk + kq);
+        const double b = frag<BK>(b_s, cb, kk + kq);
+        acc2[s & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc2[s & 3], 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < KT / 8; ++s) {
       const int kk = kb + 4 * s;
@@ -129,10 +158,10 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmOp g) {
   };
   for (int it = 0; it < nt; it += 2) {
     if (it + 2 < nt) {
-      ta0.load(g.A, g.lda, i0, (it + 2) * KT, g.M, g.K, g.kscale, t);
-      tb0.load(g.B, g.ldb, j0, (it + 2) * KT, g.N, g.K, nullptr, t);
+      ta0.load(src_a(it + 2), g.lda, i0, koff(it + 2), g.M, g.K, g.kscale, t);
+      tb0.load(src_b(it + 2), g.ldb, j0, koff(it + 2), g.N, g.K, nullptr, t);
     }
-    mma(sA[0], sB[0]);
+    mma(sA[0], sB[0], it);
     if (it + 1 < nt) {
       ta1.store(sA[1], t);
       tb1.store(sB[1], t);
@@ -140,10 +169,10 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmOp g) {
     __syncthreads();
     if (it + 1 >= nt) break;
     if (it + 3 < nt) {
-      ta1.load(g.A, g.lda, i0, (it + 3) * KT, g.M, g.K, g.kscale, t);
-      tb1.load(g.B, g.ldb, j0, (it + 3) * KT, g.N, g.K, nullptr, t);
+      ta1.load(src_a(it + 3), g.lda, i0, koff(it + 3), g.M, g.K, g.kscale, t);
+      tb1.load(src_b(it + 3), g.ldb, j0, koff(it + 3), g.N, g.K, nullptr, t);
     }
-    mma(sA[1], sB[1]);
+    mma(sA[1], sB[1], it + 1);
     if (it + 2 < nt) {
       ta0.store(sA[0], t);
       tb0.store(sB[0], t);
@@ -151,6 +180,11 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmOp g) {
     __syncthreads();
   }
   d4 r4 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  if constexpr (DUAL) {
+    const d4 r2 = (acc2[0] + acc2[1]) + (acc2[2] + acc2[3]);
+    // combine here so the epilogue's alpha applies to both: alpha r + alpha2 r2
+    r4 = r4 + (g.alpha2 / g.alpha) * r2;
+  }
   // k-half 1 hands its partial tile to k-half 0 through LDS
   double* red = sA[0];
   if (h == 1) {
@@ -177,19 +211,34 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmOp g) {
 
 }  // namespace gemm_detail
 
-inline hipError_t gemm(const GemmOp& g, hipStream_t s) {
+// Launch n (1 or 2) GEMMs of equal shape and transposes; dual products (A2/B2)
+// must not use kscale.
+inline hipError_t gemm_group(const GemmOp* ops, int n, hipStream_t s) {
   using namespace gemm_detail;
-  if (g.M <= 0 || g.N <= 0) return hipSuccess;
-  const dim3 grid((unsigned)((g.N + BT - 1) / BT), (unsigned)((g.M + BT - 1) / BT));
-  const bool ks = g.kscale != nullptr;
-#define VB_GEMM(TA, TB, KS) \
-  hipLaunchKernelGGL((gemm_f64_kernel<TA, TB, KS>), grid, dim3(NTH), 0, s, g)
-  if (!g.ta && !g.tb) { if (ks) VB_GEMM(false, false, true); else VB_GEMM(false, false, false); }
-  else if (!g.ta && g.tb) { if (ks) VB_GEMM(false, true, true); else VB_GEMM(false, true, false); }
-  else if (g.ta && !g.tb) { if (ks) VB_GEMM(true, false, true); else VB_GEMM(true, false, false); }
-  else { if (ks) VB_GEMM(true, true, true); else VB_GEMM(true, true, false); }
+  const GemmOp& g = ops[0];
+  if (g.M <= 0 || g.N <= 0 || n < 1 || n > 2) return n < 1 ? hipSuccess : hipErrorInvalidValue;
+  GemmGroup gg{};
+  for (int i = 0; i < n; ++i) gg.op[i] = ops[i];
+  const dim3 grid((unsigned)((g.N + BT - 1) / BT), (unsigned)((g.M + BT - 1) / BT), (unsigned)n);
+  const bool ks = g.kscale != nullptr, dual = g.A2 != nullptr;
+  if (ks && dual) return hipErrorInvalidValue;
+#define VB_GEMM(TA, TB)                                                                 \
+  do {                                                                                  \
+    if (dual)                                                                           \
+      hipLaunchKernelGGL((gemm_f64_kernel<TA, TB, false, true>), grid, dim3(NTH), 0, s, gg); \
+    else if (ks)                                                                        \
+      hipLaunchKernelGGL((gemm_f64_kernel<TA, TB, true, false>), grid, dim3(NTH), 0, s, gg); \
+    else                                                                                \
+      hipLaunchKernelGGL((gemm_f64_kernel<TA, TB, false, false>), grid, dim3(NTH), 0, s, gg); \
+  } while (0)
+  if (!g.ta && !g.tb) VB_GEMM(false, false);
+  else if (!g.ta && g.tb) VB_GEMM(false, true);
+  else if (g.ta && !g.tb) VB_GEMM(true, false);
+  else VB_GEMM(true, true);
 #undef VB_GEMM
   return hipGetLastError();
 }
+
+inline hipError_t gemm(const GemmOp& g, hipStream_t s) { return gemm_group(&g, 1, s); }
 
 }  // namespace vbk
