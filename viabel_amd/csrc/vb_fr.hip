@@ -410,7 +410,8 @@ struct FrWork {
   Buf nsY[kNSMax], nsZ[kNSMax], nsT[kNSMax];
   // D
   Buf w, sq, offd, scal;
-  Buf info, part, ticket, res;
+  Buf info, part, ticket, res, tpart;
+  double* host_tpart = nullptr;  // pinned copy of the T_k residual partials
   double* host_res = nullptr;  // pinned copy of res
   int K = 0, K_prev = 0;       // Newton-Schulz iterations of the current / previous root
   bool eig_pending = false;    // a dsyevd ran since the last fr_info
@@ -423,6 +424,7 @@ struct FrWork {
   ~FrWork() {
     if (blas) rocblas_destroy_handle(blas);
     if (host_res) (void)hipHostFree(host_res);
+    if (host_tpart) (void)hipHostFree(host_tpart);
     for (double* p : {hx, hlp, hg})
       if (p) (void)hipHostFree(p);
   }
@@ -468,6 +470,14 @@ int reserve_d(FrWork* W, int D, hipStream_t st) {
   }
   FR_HIP(W->part.reserve(sizeof(double) * kNormBlocks));
   FR_HIP(W->res.reserve(sizeof(double) * (FrWork::kNSMax + 3)));
+  {
+    // residual partials of T_k: 4 per 32 x 32 block, kept per iteration
+    const size_t nblk = (size_t)((D + 31) / 32) * ((D + 31) / 32) * 4;
+    FR_HIP(W->tpart.reserve(sizeof(double) * nblk * FrWork::kNSMax));
+    if (W->host_tpart) (void)hipHostFree(W->host_tpart);
+    W->host_tpart = nullptr;
+    FR_HIP(hipHostMalloc(&W->host_tpart, sizeof(double) * 2 * nblk));
+  }
   if (!W->host_res) FR_HIP(hipHostMalloc(&W->host_res, sizeof(double) * (FrWork::kNSMax + 3)));
   W->D = D;
   return 0;
@@ -588,13 +598,23 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st) {
   int K = -1;
   for (int k = 0; k < KM; ++k) {
     FR_HIP(W->nsT[k].reserve(bytes));
+    const size_t nblk = (size_t)((D + 31) / 32) * ((D + 31) / 32) * 4;
     GemmOp g = mm(D, D, D, W->nsZ[k].d(), false, W->nsY[k].d(), false, W->nsT[k].d(), -1.0);
     g.diag = 3.0;
+    g.sq_part = W->tpart.d() + nblk * k;   // ||T_k - 2I||_F^2 partials from the epilogue
+    g.sq_shift = 2.0;
     FR_HIP(gemm(g, st));
-    if (int rc = frob2(W, D, W->nsT[k].d(), 2.0, res + k, st)) return rc;
     if (k >= kmin) {
-      FR_HIP(hipMemcpyAsync(W->host_res, res, sizeof(double) * (KM + 3), hipMemcpyDeviceToHost, st));
+      // partials of T_{k-1} and T_k (contiguous) and the scale c, one synchronisation
+      FR_HIP(hipMemcpyAsync(W->host_tpart, W->tpart.d() + nblk * (k - 1), sizeof(double) * 2 * nblk,
+                            hipMemcpyDeviceToHost, st));
+      FR_HIP(hipMemcpyAsync(W->host_res + KM + 2, res + KM + 2, sizeof(double), hipMemcpyDeviceToHost, st));
       FR_HIP(hipStreamSynchronize(st));
+      for (int kk = 0; kk < 2; ++kk) {
+        double t = 0.0;
+        for (size_t b = 0; b < nblk; ++b) t += W->host_tpart[kk * nblk + b];   // fixed order
+        W->host_res[k - 1 + kk] = t;
+      }
       const double rk = std::sqrt(W->host_res[k]), rp = std::sqrt(W->host_res[k - 1]);
       if (!(rk < 1e30))
         return vb_set_error(-2, "Newton-Schulz square root of Sigma diverged (residual %g)", rk);

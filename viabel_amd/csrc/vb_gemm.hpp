@@ -39,6 +39,10 @@ struct GemmOp {
   const double* A2;
   const double* B2;
   double alpha2;
+  // optional: per-wave partial sums of (C_ij - sq_shift [i == j])^2 over the
+  // written outputs, 4 per block at sq_part[4 (by gridDim.x + bx) + wave]
+  double* sq_part;
+  double sq_shift;
 };
 
 // Up to two independent GEMMs of equal shape / transposes in one launch
@@ -194,6 +198,7 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   __syncthreads();
   if (h == 1) return;
   const int col = j0 + wn * 16 + (lane & 15);
+  double sq = 0.0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = i0 + wm * 16 + kq + 4 * r;
@@ -205,7 +210,14 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
       double* c = g.C + (long long)row * g.ldc + col;
       if (g.beta != 0.0) v += g.beta * *c;
       *c = v;
+      const double e = row == col ? v - g.sq_shift : v;
+      sq += e * e;
     }
+  }
+  if (g.sq_part) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off, 64);
+    if (lane == 0) g.sq_part[4 * (blockIdx.y * gridDim.x + blockIdx.x) + q] = sq;
   }
 }
 
