@@ -158,6 +158,34 @@ class TestPsis:
         assert abs(np.log(np.sum(np.exp(out))) ) < 1e-10
 
 
+@pytest.mark.parametrize('n,reff', [(200_000, 0.01), (10_000_000, 1.0)])
+def test_psislw_large_tail(n, reff):
+    """Tails beyond one workgroup's LDS sort (M_t > 8192) take the device radix
+    sort: same k, tail order and smoothed weights as the oracle."""
+    from viabel_amd import psis
+    from oracle import psis_oracle
+    rs = np.random.RandomState(7)
+    lw = rs.standard_t(4, n) * 1.1
+    out, k, tails = psis.psislw_with_tail(lw, Reff=reff)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        oout, ok, otails = psis_oracle.psislw(lw.copy(), Reff=reff, return_tail=True)
+    assert len(otails[0]) > 8192
+    _close(k, ok, rtol=1e-9)
+    np.testing.assert_array_equal(tails[0], otails[0])
+    _close(out[:, 0], oout, rtol=1e-11, atol=1e-11)
+
+
+def test_gpdfit_large():
+    from viabel_amd import psis
+    from oracle import psis_oracle
+    x = np.random.RandomState(3).pareto(3.0, 20000)
+    k, sigma = psis.gpdfitnew(x)
+    ok, osigma = psis_oracle.gpdfit(x)[:2]
+    _close(k, ok, rtol=1e-10)
+    _close(sigma, osigma, rtol=1e-10)
+
+
 # ---- covariance at any d, PSIS-weighted moments (experiments.py:73-89) -------
 @pytest.mark.parametrize('n,d', [(500, 3), (2000, 100), (700, 300)])
 @pytest.mark.parametrize('weighted', [False, True])

@@ -1179,7 +1179,7 @@ int vb_psislw(vb_ctx* c, const double* lw, int64_t n, int64_t m, double reff, do
   Out dout, dk;
   VB_TRY(dout.stage(c, 1, lw_out, (size_t)n * m));
   VB_TRY(dk.stage(c, 2, k_out, (size_t)m));
-  VB_TRY(c->slot[3].reserve(vbk::psis_scratch_bytes()));
+  VB_TRY(c->slot[3].reserve(vbk::psis_scratch_bytes(Mt)));
   OutT<long long> dti, dnt;
   VB_TRY(dti.stage(c, 4, reinterpret_cast<long long*>(tail_idx_out),
                    tail_idx_out ? (size_t)tail_cap * m : 0));
@@ -1207,7 +1207,7 @@ int vb_gpdfit(vb_ctx* c, const double* x, int64_t n, double* k, double* sigma, d
   const int m = 30 + (int)std::sqrt((double)n);
   In dx;
   VB_TRY(dx.stage(c, 0, x, (size_t)n));
-  VB_TRY(c->slot[3].reserve(vbk::psis_scratch_bytes()));
+  VB_TRY(c->slot[3].reserve(vbk::psis_scratch_bytes(n)));
   Out dks, dw;
   VB_TRY(dks.stage(c, 1, ks_out, ks_out ? (size_t)m : 0));
   VB_TRY(dw.stage(c, 2, w_out, w_out ? (size_t)m : 0));
@@ -1290,7 +1290,7 @@ int vb_sumlogs(vb_ctx* c, const double* x, int64_t n, double* out) {
   if (!x || !out || n < 1) return fail(VB_EINVAL, "invalid argument");
   In dx;
   VB_TRY(dx.stage(c, 0, x, (size_t)n));
-  VB_TRY(c->slot[3].reserve(vbk::psis_scratch_bytes()));
+  VB_TRY(c->slot[3].reserve(vbk::psis_scratch_bytes(0)));
   VB_TRY(c->slot[4].reserve(sizeof(double)));
   VB_HIP(vbk::psis_sumlogs(dx.d, n, c->slot[3].p, c->slot[4].d(), c->stream));
   VB_HIP(hipMemcpyAsync(out, c->slot[4].p, sizeof(double), hipMemcpyDeviceToHost, c->stream));

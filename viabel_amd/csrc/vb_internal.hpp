@@ -120,7 +120,7 @@ hipError_t bounds_weighted_covariance(const double* x, long long n, long long d,
 constexpr int kCovDMax = 64;
 
 // PSIS (vb_psis.hip)
-size_t psis_scratch_bytes();
+size_t psis_scratch_bytes(long long tail_cap);  // scratch for tails / gpdfit inputs <= tail_cap
 long long psis_tail_max();
 hipError_t psis_column(const double* lw, double* out, long long n, long long st, long long Mt,
                        void* scratch, double* k_dev, long long* tail_idx_dev,

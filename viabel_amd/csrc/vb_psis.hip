@@ -21,6 +21,8 @@
 #include "vb_device.hpp"
 #include "vb_internal.hpp"
 
+#include <hipcub/hipcub.hpp>
+
 #include <cfloat>
 #include <cmath>
 
@@ -28,7 +30,8 @@ using namespace vbd;
 
 namespace vbk {
 
-constexpr int kTailMax = 8192;  // tail sorted in one workgroup's LDS
+constexpr int kTailMax = 8192;  // tails up to this size: one workgroup's LDS bitonic sort;
+                                // larger tails: stable device radix sort (hipcub)
 constexpr int kPsisBlocks = 512;
 
 // device scratch layout for one column (see psis_scratch_doubles)
@@ -226,6 +229,7 @@ __global__ __launch_bounds__(1024) void tail_sort_kernel(const double* tv, const
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long* key = reinterpret_cast<unsigned long long*>(smem);
   unsigned* pos = reinterpret_cast<unsigned*>(smem + sizeof(unsigned long long) * kTailMax);
+  if (cap > kTailMax) cap = kTailMax;
   long long n2 = ps->n2;
   if (n2 > cap) n2 = cap;
   int np2 = 1;
@@ -471,11 +475,23 @@ static int psis_grid(long long n) {
   return (int)g;
 }
 
-size_t psis_scratch_bytes() {
-  // state + partials + radix hist + tail (value, index) x2 + y + grid arrays
+static size_t radix_temp_bytes(long long cap) {
+  if (cap <= kTailMax) return 0;
+  size_t bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const double*)nullptr, (double*)nullptr,
+                                           (const long long*)nullptr, (long long*)nullptr,
+                                           (int)cap);
+  return (bytes + 255) / 256 * 256;
+}
+
+static long long cap_of(long long cap) { return cap < kTailMax ? kTailMax : cap; }
+
+size_t psis_scratch_bytes(long long tail_cap) {
+  const long long cap = cap_of(tail_cap);
+  // state + partials + radix hist + tail (value, index) x2 + y + grid arrays + sort temp
   return 256 + sizeof(double) * kPsisBlocks * 2 + sizeof(unsigned) * 256 +
-         sizeof(unsigned) * kPsisBlocks + 2 * kTailMax * (sizeof(double) + sizeof(long long)) +
-         sizeof(double) * kTailMax + sizeof(double) * 8 * 256;
+         sizeof(unsigned) * kPsisBlocks + 2 * cap * (sizeof(double) + sizeof(long long)) +
+         sizeof(double) * cap + sizeof(double) * 8 * 256 + radix_temp_bytes(tail_cap) + 256;
 }
 
 struct PsisScratch {
@@ -491,9 +507,12 @@ struct PsisScratch {
   double* bs;
   double* ks;
   double* Lw;
+  void* sort_tmp;
+  size_t sort_bytes;
 };
 
-static PsisScratch carve(void* base) {
+static PsisScratch carve(void* base, long long tail_cap) {
+  const long long kTailMax = cap_of(tail_cap);   // array capacity of this carve
   unsigned char* p = static_cast<unsigned char*>(base);
   PsisScratch s;
   s.ps = reinterpret_cast<PsisState*>(p);
@@ -517,16 +536,42 @@ static PsisScratch carve(void* base) {
   s.bs = reinterpret_cast<double*>(p);
   s.ks = s.bs + 256;
   s.Lw = s.ks + 256;
+  p += sizeof(double) * 8 * 256;
+  p = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(p) + 255) & ~uintptr_t(255));
+  s.sort_tmp = p;
+  s.sort_bytes = radix_temp_bytes(tail_cap);
   return s;
 }
 
-long long psis_tail_max() { return kTailMax; }
+long long psis_tail_max() { return 1LL << 30; }
+
+namespace {
+__global__ __launch_bounds__(256) void fill_inf_kernel(double* v, long long n) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) v[i] = INFINITY;
+}
+
+// tail values tv / indices ti (n2 <= cap valid entries, the rest +inf when cap >
+// kTailMax) -> ascending sv / si, stable on position
+hipError_t sort_tail(const PsisScratch& S, long long cap, hipStream_t s) {
+  if (cap <= kTailMax) {
+    const size_t lds = (sizeof(unsigned long long) + sizeof(unsigned)) * kTailMax;
+    hipLaunchKernelGGL(tail_sort_kernel, dim3(1), dim3(1024), lds, s, S.tv, S.ti, S.ps, S.sv, S.si,
+                       cap);
+    return hipGetLastError();
+  }
+  size_t bytes = S.sort_bytes;
+  return hipcub::DeviceRadixSort::SortPairs(S.sort_tmp, bytes, S.tv, S.sv, S.ti, S.si, (int)cap, 0,
+                                            64, s);
+}
+}  // namespace
 
 // One column of psislw.  lw/out are device pointers with stride st.
 hipError_t psis_column(const double* lw, double* out, long long n, long long st, long long Mt,
                        void* scratch, double* k_dev, long long* tail_idx_dev,
                        long long* n_tail_dev, hipStream_t s) {
-  PsisScratch S = carve(scratch);
+  const long long cap = Mt < 1 ? 1 : Mt;   // the tail holds at most M_t draws
+  PsisScratch S = carve(scratch, cap);
   const int g = psis_grid(n);
   // 1. max
   hipLaunchKernelGGL(col_max_kernel, dim3(g), dim3(256), 0, s, lw, n, st, S.part);
@@ -548,21 +593,23 @@ hipError_t psis_column(const double* lw, double* out, long long n, long long st,
   hipLaunchKernelGGL(shift_kernel, dim3(g), dim3(256), 0, s, lw, out, n, st, S.ps);
   hipLaunchKernelGGL(tail_count_kernel, dim3(gc), dim3(256), 0, s, out, n, st, chunk, S.ps, S.cnt);
   hipLaunchKernelGGL(tail_scan_kernel, dim3(1), dim3(64), 0, s, S.cnt, gc, S.ps);
+  if (cap > kTailMax)
+    hipLaunchKernelGGL(fill_inf_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, S.tv,
+                       cap);
   hipLaunchKernelGGL(tail_compact_kernel, dim3(gc), dim3(256), 0, s, out, n, st, chunk, S.ps, S.cnt,
-                     (long long)kTailMax, S.tv, S.ti);
+                     cap, S.tv, S.ti);
   // 4. sort the tail
-  const size_t lds = (sizeof(unsigned long long) + sizeof(unsigned)) * kTailMax;
-  hipLaunchKernelGGL(tail_sort_kernel, dim3(1), dim3(1024), lds, s, S.tv, S.ti, S.ps, S.sv, S.si,
-                     (long long)kTailMax);
+  e = sort_tail(S, cap, s);
+  if (e != hipSuccess) return e;
   // 5. GPD fit (skipped on device when n2 <= 4)
-  hipLaunchKernelGGL(gpd_prep_kernel, dim3(32), dim3(256), 0, s, S.sv, S.ps, S.y, (long long)kTailMax);
+  hipLaunchKernelGGL(gpd_prep_kernel, dim3(32), dim3(256), 0, s, S.sv, S.ps, S.y, cap);
   const int mmax = 30 + (int)std::sqrt((double)Mt) + 1;
   hipLaunchKernelGGL(gpd_grid_kernel, dim3(mmax), dim3(256), 0, s, S.y, S.ps, 0LL, S.bs, S.ks);
   hipLaunchKernelGGL(gpd_final_kernel, dim3(1), dim3(256), 0, s, S.y, S.ps, 0LL, S.bs, S.ks, S.Lw,
                      nullptr, nullptr);
   hipLaunchKernelGGL(k_inf_kernel, dim3(1), dim3(64), 0, s, S.ps);
   // 6. smoothing
-  hipLaunchKernelGGL(smooth_kernel, dim3(32), dim3(256), 0, s, out, st, S.ps, S.si, (long long)kTailMax);
+  hipLaunchKernelGGL(smooth_kernel, dim3(32), dim3(256), 0, s, out, st, S.ps, S.si, cap);
   // 7. renormalise: x -= sumlogs(x)
   hipLaunchKernelGGL(col_max_kernel, dim3(g), dim3(256), 0, s, out, n, st, S.part);
   hipLaunchKernelGGL(max_final_kernel, dim3(1), dim3(256), 0, s, S.part, g, &S.ps->b);
@@ -585,12 +632,11 @@ hipError_t psis_column(const double* lw, double* out, long long n, long long st,
 // gpdfitnew on a caller array x[n] (device), any order.  out4 = {k, sigma, m, nkeep}
 hipError_t psis_gpdfit(const double* x, long long n, void* scratch, double* out4,
                        double* ks_out, double* w_out, hipStream_t s) {
-  PsisScratch S = carve(scratch);
+  PsisScratch S = carve(scratch, n);
   hipLaunchKernelGGL(iota_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n,
                      S.tv, S.ti, S.ps);
-  const size_t lds = (sizeof(unsigned long long) + sizeof(unsigned)) * kTailMax;
-  hipLaunchKernelGGL(tail_sort_kernel, dim3(1), dim3(1024), lds, s, S.tv, S.ti, S.ps, S.sv, S.si,
-                     (long long)kTailMax);
+  hipError_t e0 = sort_tail(S, n, s);
+  if (e0 != hipSuccess) return e0;
   const int m = 30 + (int)std::sqrt((double)n);
   hipLaunchKernelGGL(gpd_grid_kernel, dim3(m), dim3(256), 0, s, S.sv, S.ps, n, S.bs, S.ks);
   hipLaunchKernelGGL(gpd_final_kernel, dim3(1), dim3(256), 0, s, S.sv, S.ps, n, S.bs, S.ks, S.Lw,
@@ -611,7 +657,7 @@ hipError_t psis_gpinv(const double* p, long long n, double k, double sigma, doub
 }
 
 hipError_t psis_sumlogs(const double* x, long long n, void* scratch, double* out, hipStream_t s) {
-  PsisScratch S = carve(scratch);
+  PsisScratch S = carve(scratch, 0);
   const int g = psis_grid(n);
   hipLaunchKernelGGL(col_max_kernel, dim3(g), dim3(256), 0, s, x, n, 1LL, S.part);
   hipLaunchKernelGGL(max_final_kernel, dim3(1), dim3(256), 0, s, S.part, g, &S.ps->b);
