@@ -165,3 +165,32 @@ def test_klvi_pd_adagrad_and_fullrank():
     ov, og = fr.klvi_pd_value_grad(offam, fr.target_fn('corr_gauss', Dr), lam, 40)
     np.testing.assert_allclose(v, ov, rtol=1e-9)
     _close(g, og, 1e-8)
+
+
+def test_big_window_and_many_wide_problems():
+    """adagrad windows > 64 (materialised path, window in HBM) and several
+    problems in one wide run match the oracle."""
+    vb, targets, vo = _mods()
+    D = 6
+    fam = _family(vb, 'gauss', None, D)
+    ofam = vo.Family('gauss', D)
+    obj = vb.black_box_klvi(fam, targets.mixture(D), 20)
+    lam0 = _lam(D, 3)
+    res = vb.adagrad_optimize(120, obj, lam0, window=100, learning_rate=.05)
+    ores = vo.adagrad_optimize(120, lambda l: vo.klvi_value_grad(ofam, 'mixture', l, 20), lam0,
+                               window=100, learning_rate=.05)
+    _close(res[1], ores[1], 1e-7)
+    _close(res[2], ores[2], 1e-7)
+    # three restarts of a wide CHIVI problem in one run (Philox streams 5, 6, 7)
+    Dw = 30
+    famw = vb.mean_field_gaussian_variational_family(Dw, rng='philox')
+    objw = vb.black_box_chivi(2.0, famw, targets.funnel(Dw), 16)
+    inits = np.stack([_lam(Dw, s) for s in range(3)])
+    run = vb.DeviceRun(objw, 30, inits, learning_rate=.01)
+    run.advance_philox(30, 9, 5, 0)
+    lam, hist, vals, _ = run.result()
+    assert np.all(np.isfinite(vals)) and vals.shape == (3, 30)
+    for q in range(3):   # each problem equals a single-problem run on its own stream
+        single = vb.DeviceRun(objw, 30, inits[q][None], learning_rate=.01)
+        single.advance_philox(30, 9, 5 + q, 0)
+        _close(single.result()[2][0], vals[q], 1e-12)

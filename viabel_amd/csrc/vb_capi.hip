@@ -681,8 +681,7 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
   if (cfg->optimizer < VB_OPT_ADAGRAD || cfg->optimizer > VB_OPT_ADAM_IA)
     return fail(VB_EINVAL, "unknown optimizer %d", cfg->optimizer);
   const bool ia = cfg->optimizer != VB_OPT_ADAGRAD;
-  if (cfg->window < 1 || (!ia && cfg->window > 64))
-    return fail(VB_EINVAL, "window must be in [1, 64]");
+  if (cfg->window < 1) return fail(VB_EINVAL, "window must be positive");
   if (cfg->n_iters < 0) return fail(VB_EINVAL, "n_iters must be non-negative");
   if (n_problems < 1) return fail(VB_EINVAL, "n_problems must be positive");
   if (obj->n_samples < 1 || obj->n_samples > (1LL << 31))
@@ -695,10 +694,11 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
                    (D > vbk::kBlockDMax);
   // D > kBlockDMax without the fused kernel (CHIVI, non-separable targets, IA
   // optimisers): the materialised mean-field path, one problem per run
+  // (the fused kernels keep the adagrad window on chip: windows > 64 use the
+  // materialised path, whose window lives in HBM)
+  const bool big_window = !ia && cfg->window > 64;
   const bool wide = !fr && ((D > vbk::kBlockDMax && (!sep || ia)) ||
-                            tgt->kind == VB_TARGET_CALLBACK);
-  if (wide && n_problems != 1)
-    return fail(VB_EUNSUPPORTED, "wide (D > %d) runs hold one problem per vb_run", vbk::kBlockDMax);
+                            tgt->kind == VB_TARGET_CALLBACK || big_window);
   if (sep && n_problems != 1)
     return fail(VB_EUNSUPPORTED, "wide (D > %d) runs hold one problem per vb_run", vbk::kBlockDMax);
 
