@@ -179,7 +179,7 @@ def main():
                 line['roofline']['traffic_source'] = tr.get('source')
             except Exception:
                 pass
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # rank 0 at N = 1 only
             line['cpu_baseline'] = cpu_baseline(args.cpu_seconds)
             line['speedup_vs_cpu_baseline'] = value / line['cpu_baseline']['value']
         print(json.dumps(line), flush=True)
