@@ -11,7 +11,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libviabel_amd.so')
+# VIABEL_AMD_LIB selects another in-tree build (e.g. an instrumented one)
+LIB_PATH = os.environ.get('VIABEL_AMD_LIB') or os.path.join(_HERE, 'libviabel_amd.so')
 
 VB_OK, VB_EINVAL, VB_EDEVICE, VB_ENOMEM, VB_EUNSUPPORTED = 0, -1, -2, -3, -4
 FAMILY_MF_GAUSSIAN, FAMILY_MF_T, FAMILY_FR_T = 0, 1, 2

@@ -307,38 +307,98 @@ __global__ __launch_bounds__(256) void row_mean_kernel(const double* hist, long 
 template <class TGT>
 using RowOf = std::conditional_t<TGT::kSeparable, SepRow<TGT>, TGT>;
 
-template <int K>
-__device__ __forceinline__ void block_sum(double (&v)[K], double (*red)[K + 1], int nwave) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const double t = wave_sum_dpp(v[k]);
-    if (lane == 0) red[wid][k] = t;
-  }
-  __syncthreads();
-  if (threadIdx.x < K) {
-    double acc = red[0][threadIdx.x];
-    for (int q = 1; q < nwave; ++q) acc += red[q][threadIdx.x];
-    red[0][threadIdx.x] = acc;  // each thread only touches its own column
-  }
-  __syncthreads();
+// Wave-level reduce-scatter of K per-lane values: two permlane swap levels fold
+// four values into each register (halves, then rows), a 4-step DPP row sum
+// finishes them, and lane 0 of each row writes its value's wave total to
+// out[k].  ~3x fewer instructions than K full-wave sums.
+__device__ __forceinline__ double swap32_pair(double a, double b) {
+  const auto l = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(a),
+                                                  (unsigned)__double2loint(b), false, false);
+  const auto h = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(a),
+                                                  (unsigned)__double2hiint(b), false, false);
+  return __hiloint2double((int)h[0], (int)l[0]) + __hiloint2double((int)h[1], (int)l[1]);
 }
 
-// Philox mode splits a step into a draw phase (every thread takes (sample, pair)
-// items: normal pair [+ gamma pair] -> LDS) and a row phase (one thread per
-// sample: reparameterise, target, accumulate), so one problem's draws spread
-// over up to 8 waves instead of one thread per sample.
+__device__ __forceinline__ double swap16_pair(double a, double b) {
+  const auto l = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(a),
+                                                  (unsigned)__double2loint(b), false, false);
+  const auto h = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(a),
+                                                  (unsigned)__double2hiint(b), false, false);
+  return __hiloint2double((int)h[0], (int)l[0]) + __hiloint2double((int)h[1], (int)l[1]);
+}
+
+template <int K>
+__device__ __forceinline__ void wave_reduce_scatter(const double (&v)[K], double* out) {
+  constexpr int H1 = (K + 1) / 2, H2 = (H1 + 1) / 2;
+  double r1[H1], r2[H2];
+#pragma unroll
+  for (int i = 0; i < H1; ++i) r1[i] = swap32_pair(v[i], i + H1 < K ? v[i + H1] : 0.0);
+#pragma unroll
+  for (int j = 0; j < H2; ++j) {
+    double t = swap16_pair(r1[j], j + H2 < H1 ? r1[j + H2] : 0.0);
+    t += dpp_f64<0xB1>(t);   // quad_perm [1,0,3,2]
+    t += dpp_f64<0x4E>(t);   // quad_perm [2,3,0,1]
+    t += dpp_f64<0x141>(t);  // row_half_mirror
+    t += dpp_f64<0x140>(t);  // row_mirror
+    r2[j] = t;
+  }
+  const int lane = threadIdx.x & 63, q = lane >> 4;
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < H2; ++j) {
+      const int i = j + (q & 1) * H2;  // row q of register j holds v[i + (q >> 1) * H1]
+      const int k = i + (q >> 1) * H1;
+      if (i < H1 && k < K) out[k] = r2[j];
+    }
+  }
+}
+
+// Philox mode runs the block as row waves (reparameterise, target, accumulate:
+// one thread per sample) and draw waves (normal pair [+ gamma pair] and the
+// pair's log q partial per (sample, pair) item, into LDS).  When one step's
+// draws fit half of the draw buffer the two roles overlap: draw waves produce
+// step s+1 into the other half while row waves consume step s.  Otherwise
+// (large N) all waves draw a chunk, then the row waves consume it.
 constexpr int kBlockMaxThreads = 512;
-constexpr int kBlockDrawLds = 4096;  // doubles of LDS for one chunk of draws
+constexpr int kBlockDrawLds = 4096;  // doubles of LDS for the draw records
+constexpr int kBlockMaxRowWaves = 4;
+
+struct BlockLayout {
+  int nt, rw, pipe, rec;  // threads, row waves, overlapped draws, doubles per sample record
+};
+
+__host__ __device__ inline BlockLayout block_layout(int N, int D, bool host, bool need_lq) {
+  const int NP = (D + 1) / 2;
+  const int rw = std::min(kBlockMaxRowWaves, std::max(1, (N + 63) / 64));
+  BlockLayout L{};
+  L.rw = rw;
+  L.rec = 2 * NP + (need_lq ? NP : 0);
+  if (host) {
+    L.nt = 64 * rw;
+    L.pipe = 0;
+    return L;
+  }
+  const long long iw = ((long long)N * NP + 63) / 64;  // waves of draw items
+  const int maxw = kBlockMaxThreads / 64;
+  if ((long long)N * L.rec <= kBlockDrawLds / 2) {
+    L.pipe = 1;
+    L.nt = 64 * (rw + (int)std::min<long long>(maxw - rw, std::max<long long>(1, iw)));
+  } else {
+    L.pipe = 0;
+    L.nt = 64 * (int)std::min<long long>(maxw, std::max<long long>(rw, iw));
+  }
+  return L;
+}
 
 template <class TGT, bool TFAM, bool HOST, int DMAX>
 __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   constexpr int K = 2 * DMAX + 2;   // G[DMAX], H[DMAX], V/S, spare
   constexpr int WMAX = 64;
   __shared__ double s_lam[2 * DMAX];
+  __shared__ double s_sg[DMAX];     // exp(log sigma) of the current lam
   __shared__ double s_ring[WMAX * 2 * DMAX];
-  __shared__ double s_red[8][K + 1];
-  __shared__ double s_max[8];
+  __shared__ double s_red[kBlockMaxRowWaves][K];
+  __shared__ double s_max[kBlockMaxRowWaves];
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN];
   __shared__ double s_e[HOST ? 1 : kBlockDrawLds];
@@ -346,9 +406,14 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
 
   using Row = RowOf<TGT>;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int NT = blockDim.x, NW = NT >> 6;  // 64..512 threads (sized by the launcher)
+  const int NT = blockDim.x;
   const int prob = blockIdx.x;
   const int D = a.D, N = a.N, W = a.W, P = a.P;
+  const bool need_lq = a.chivi || a.pd;
+  const BlockLayout L = block_layout(N, D, HOST, need_lq);
+  const int RW = L.rw, RT = 64 * RW, R = L.rec;
+  const bool row_wave = wid < RW;
+  const int val_tid = NT > 64 ? NT - 64 : 0;  // value on another wave than the update
   const double dN = (double)N;
   double* lam_g = a.lam + (long long)prob * P;
   double* ring_g = a.ring ? a.ring + (long long)prob * W * P : nullptr;
@@ -356,78 +421,86 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   for (int p = tid; p < P; p += NT) s_lam[p] = lam_g[p];
   if (!a.emit_grad)
     for (int q = tid; q < W * P; q += NT) s_ring[q] = ring_g[q];
-  __syncthreads();
+  for (int d = tid; d < D; d += NT) s_sg[d] = exp(lam_g[D + d]);
 
   const Rng rng{a.k0, a.k1, (uint32_t)(a.stream + (uint32_t)prob * a.stream_stride)};
   const double c0 = TFAM ? 0.0 : 0.5 * D * (1.0 + kLog2Pi);
+  const int NP = (D + 1) / 2;
+  const double lq_half = 0.5 * (a.df + 1.0);
 
+  // one (sample, pair) draw item: e pair [+ log q partial of the pair, sans -log sigma]
+  auto draw_item = [&](int it0, int it_step, int n_items, int nbase, long long ri, double* buf) {
+    for (int it = it0; it < n_items; it += it_step) {
+      const int nl = it / NP, j = it - nl * NP;
+      const uint32_t n = (uint32_t)(nbase + nl);
+      double ea, eb;
+      normal_pair_tab(rng.draw((uint32_t)j, n, (uint32_t)ri, 0u), ea, eb, s_sct, s_lt);
+      if constexpr (TFAM) {
+        double ga, gb;
+        gamma_pair<true>(rng, (uint32_t)j, n, (uint32_t)ri, a.shape, ga, gb, s_sct, s_lt);
+        ea = a.t_scale * ea / sqrt(ga);
+        eb = a.t_scale * eb / sqrt(gb);
+      }
+      double* rec = buf + nl * R;
+      rec[2 * j] = ea;
+      rec[2 * j + 1] = eb;
+      if (need_lq) {
+        const bool hasb = 2 * j + 1 < D;
+        double lqp;
+        if constexpr (TFAM) {
+          lqp = a.t_const - log1p(ea * ea / a.df) * lq_half;
+          if (hasb) lqp += a.t_const - log1p(eb * eb / a.df) * lq_half;
+        } else {
+          lqp = -0.5 * ea * ea - 0.5 * kLog2Pi;
+          if (hasb) lqp += -0.5 * eb * eb - 0.5 * kLog2Pi;
+        }
+        rec[2 * NP + j] = lqp;
+      }
+    }
+  };
+
+  if constexpr (!HOST) {
+    if (L.pipe && a.n_steps > 0) draw_item(tid, NT, N * NP, 0, a.rng_step0, s_e);
+  }
+  __syncthreads();
+
+#ifdef VB_BLOCK_PROF
+  unsigned long long ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tw0 = wall_clock64(), tc0 = clock64(), tp = clock64();
+#define VB_PH(k) do { __builtin_amdgcn_s_waitcnt(0xC07F); const unsigned long long t_ = clock64(); ph[k] += t_ - tp; tp = t_; } while (0)
+#else
+#define VB_PH(k) do {} while (0)
+#endif
+
+  int slot = W > 0 ? (int)(a.step0 % W) : 0;  // window ring slot of step i (i % W)
   for (int s = 0; s < a.n_steps; ++s) {
     const long long i = a.step0 + s;
     const long long ri = a.rng_step0 + s;
-    double mu[DMAX], sg[DMAX], lsg[DMAX];
+    double mu[DMAX], sg[DMAX];
+    double sl = 0.0;  // sum_d log sigma_d of the pre-update lam
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
       mu[d] = d < D ? s_lam[d] : 0.0;
-      lsg[d] = d < D ? s_lam[D + d] : 0.0;
-      sg[d] = exp(lsg[d]);
+      sg[d] = d < D ? s_sg[d] : 0.0;
+      if (d < D) sl += s_lam[D + d];
     }
     double acc[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
     double mloc = -INFINITY;  // CHIVI: running max of this thread's log weights
+    VB_PH(0);
 
-    const int NP = (D + 1) / 2;
-    const int CH = HOST ? N : kBlockDrawLds / (2 * NP);  // samples per draw chunk
-    for (int c0n = 0; c0n < N; c0n += CH) {
-    const int nc = min(CH, N - c0n);
-    if constexpr (!HOST) {
-      // draw phase: items (sample, pair) over all threads
-      for (int it = tid; it < nc * NP; it += NT) {
-        const int nl = it / NP, j = it - nl * NP;
-        const uint32_t n = (uint32_t)(c0n + nl);
-        double ea, eb;
-        normal_pair_tab(rng.draw((uint32_t)j, n, (uint32_t)ri, 0u), ea, eb, s_sct, s_lt);
-        if constexpr (TFAM) {
-          double ga, gb;
-          gamma_pair<true>(rng, (uint32_t)j, n, (uint32_t)ri, a.shape, ga, gb, s_sct, s_lt);
-          ea = a.t_scale * ea / sqrt(ga);
-          eb = a.t_scale * eb / sqrt(gb);
-        }
-        s_e[nl * 2 * NP + 2 * j] = ea;
-        s_e[nl * 2 * NP + 2 * j + 1] = eb;
-      }
-      __syncthreads();
-    }
-    for (int n = c0n + tid; n < c0n + nc; n += NT) {
-      double e[DMAX], x[DMAX], g[DMAX];
-      if constexpr (HOST) {
-        const double* row = a.noise + (((long long)prob * a.n_steps + s) * N + n) * D;
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) e[d] = d < D ? row[d] : 0.0;
-      } else {
-        const double* row = s_e + (n - c0n) * 2 * NP;
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) e[d] = d < D ? row[d] : 0.0;
-      }
+    auto row_of = [&](const double* e, double lqs) {
+      double x[DMAX], g[DMAX];
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
         x[d] = e[d] * sg[d] + mu[d];
         g[d] = 0.0;
       }
       double lp = Row::template row<DMAX>(x, g, D);
-      if (a.pd) {
-        // black_box_klvi_pd: accumulate log p - log q(x) (all constants)
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) {
-          if (d < D) {
-            const double z = (x[d] - mu[d]) / sg[d];
-            if constexpr (TFAM)
-              lp -= a.t_const - log1p(z * z / a.df) * (0.5 * (a.df + 1.0)) - lsg[d];
-            else
-              lp -= -0.5 * z * z - lsg[d] - 0.5 * kLog2Pi;
-          }
-        }
-      }
+      // log q(x; lam) with all constants (mvn.logpdf / t.logpdf), z = eps
+      const double lq = lqs - sl;
+      if (a.pd) lp -= lq;
       if (!a.chivi) {
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) {
@@ -436,18 +509,6 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
         }
         acc[2 * DMAX] += lp;
       } else {
-        // log q(x; lam) with all constants (mvn.logpdf / t.logpdf)
-        double lq = 0.0;
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) {
-          if (d < D) {
-            const double z = (x[d] - mu[d]) / sg[d];
-            if constexpr (TFAM)
-              lq += a.t_const - log1p(z * z / a.df) * (0.5 * (a.df + 1.0)) - lsg[d];
-            else
-              lq += -0.5 * z * z - lsg[d] - 0.5 * kLog2Pi;
-          }
-        }
         const double lw = lp - lq;
         if (lw > mloc) {
           const double f = (mloc == -INFINITY) ? 0.0 : exp(a.alpha * (mloc - lw));
@@ -463,92 +524,164 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
         }
         acc[2 * DMAX] += wgt;
       }
-    }
-    if constexpr (!HOST) __syncthreads();  // s_e is refilled by the next chunk
+    };
+
+    if constexpr (HOST) {
+      for (int n = tid; n < N; n += RT) {
+        const double* row = a.noise + (((long long)prob * a.n_steps + s) * N + n) * D;
+        double e[DMAX];
+        double lqs = 0.0;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          e[d] = d < D ? row[d] : 0.0;
+          if (need_lq && d < D) {
+            if constexpr (TFAM)
+              lqs += a.t_const - log1p(e[d] * e[d] / a.df) * lq_half;
+            else
+              lqs += -0.5 * e[d] * e[d] - 0.5 * kLog2Pi;
+          }
+        }
+        row_of(e, lqs);
+      }
+    } else {
+      auto consume = [&](const double* buf, int nbase, int nc) {
+        for (int n = tid; n < nc; n += RT) {
+          const double* rec = buf + n * R;
+          double e[DMAX];
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) e[d] = d < D ? rec[d] : 0.0;
+          double lqs = 0.0;
+          if (need_lq)
+            for (int j = 0; j < NP; ++j) lqs += rec[2 * NP + j];
+          row_of(e, lqs);
+        }
+        (void)nbase;
+      };
+      if (L.pipe) {
+        double* cur = s_e + (s & 1) * (kBlockDrawLds / 2);
+        double* nxt = s_e + ((s + 1) & 1) * (kBlockDrawLds / 2);
+        if (row_wave)
+          consume(cur, 0, N);
+        else if (s + 1 < a.n_steps)
+          draw_item(tid - RT, NT - RT, N * NP, 0, ri + 1, nxt);
+        VB_PH(2);
+      } else {
+        const int CH = kBlockDrawLds / R;  // samples per draw chunk
+        for (int c0n = 0; c0n < N; c0n += CH) {
+          const int nc = min(CH, N - c0n);
+          draw_item(tid, NT, nc * NP, c0n, ri, s_e);
+          VB_PH(1);
+          __syncthreads();
+          if (row_wave) consume(s_e, c0n, nc);
+          VB_PH(2);
+          if (c0n + CH < N) __syncthreads();  // s_e is refilled by the next chunk
+        }
+      }
     }
 
     double M = 0.0;
     if (a.chivi) {
-      const double wm = wave_max_dpp(mloc);
-      if (lane == 0) s_max[wid] = wm;
+      if (row_wave) {
+        const double wm = wave_max_dpp(mloc);
+        if (lane == 0) s_max[wid] = wm;
+      }
       __syncthreads();
       M = s_max[0];
-      for (int q = 1; q < NW; ++q) M = fmax(M, s_max[q]);
+      for (int q = 1; q < RW; ++q) M = fmax(M, s_max[q]);
       const double f = (mloc == -INFINITY) ? 0.0 : exp(a.alpha * (mloc - M));
 #pragma unroll
       for (int k = 0; k <= 2 * DMAX; ++k) acc[k] *= f;
     }
-    block_sum<K>(acc, s_red, NW);
+    VB_PH(3);
+    if (row_wave) wave_reduce_scatter<K>(acc, s_red[wid]);
+    __syncthreads();
+    if (tid < K) {
+      double t = s_red[0][tid];
+      for (int q = 1; q < RW; ++q) t += s_red[q][tid];
+      s_red[0][tid] = t;  // each thread only touches its own column
+    }
+    __syncthreads();
+    VB_PH(4);
 
-    // gradient + adagrad update: thread p owns parameter p
+    // gradient + update: thread p owns parameter p
     if (tid < P) {
       const int p = tid;
       double gp;
       if (!a.chivi) {
         gp = p < D ? -(s_red[0][p] / dN)
-                   : -(1.0 + exp(s_lam[p]) * (s_red[0][DMAX + (p - D)] / dN));
+                   : -(1.0 + s_sg[p - D] * (s_red[0][DMAX + (p - D)] / dN));
       } else {
         const double Ssum = s_red[0][2 * DMAX];
         gp = p < D ? a.alpha * s_red[0][p] / dN
-                   : a.alpha * (exp(s_lam[p]) * s_red[0][DMAX + (p - D)] + Ssum) / dN;
+                   : a.alpha * (s_sg[p - D] * s_red[0][DMAX + (p - D)] + Ssum) / dN;
       }
       if (a.emit_grad) {
         a.grad[(long long)prob * P + p] = gp;
-      } else if (a.opt != 0) {
-        // RMSProp-IA (vb.py:436-453) / Adam-IA (vb.py:606-617): state in
-        // s_ring[0..P) (second moment) and s_ring[P..2P) (first moment); the
-        // history keeps the PRE-update parameters of the last n_hist iterations.
-        const double old = s_lam[p];
-        if (i >= a.hist_start) a.hist[((long long)prob * a.n_hist + (i - a.hist_start)) * P + p] = old;
-        const double g2 = __dmul_rn(gp, gp);
-        double nl;
-        if (a.opt == 1) {
-          const double sgs = i == 0 ? g2 : __dadd_rn(__dmul_rn(s_ring[p], 0.9), __dmul_rn(1.0 - 0.9, g2));
-          s_ring[p] = sgs;
-          nl = __dsub_rn(old, __dmul_rn(a.lr.at(i), gp) / sqrt(__dadd_rn(a.eps, sgs)));
-        } else {
-          const double v = i == 0 ? __dmul_rn(0.9, g2)
-                                  : __dadd_rn(__dmul_rn(s_ring[p], 0.999), __dmul_rn(1.0 - 0.999, g2));
-          const double m = i == 0 ? __dmul_rn(0.9, gp)
-                                  : __dadd_rn(__dmul_rn(s_ring[P + p], 0.9), __dmul_rn(1.0 - 0.9, gp));
-          s_ring[p] = v;
-          s_ring[P + p] = m;
-          const double mh = m / (1.0 - pow(0.9, (double)(i + 2)));
-          const double vh = v / (1.0 - pow(0.999, (double)(i + 2)));
-          nl = __dsub_rn(old, __dmul_rn(a.lr.at(i), mh) / sqrt(__dadd_rn(a.eps, vh)));
-        }
-        s_lam[p] = nl;
       } else {
-        const int slot = (int)(i % W);
-        s_ring[slot * P + p] = gp;
-        const int cnt = (i + 1 < W) ? (int)(i + 1) : W;
-        const int oldest = (cnt < W) ? 0 : (int)((i + 1) % W);
-        double q = 0.0;
-        for (int k = 0; k < cnt; ++k) {
-          int L = oldest + k;
-          if (L >= W) L -= W;
-          const double t = s_ring[L * P + p];
-          q = __dadd_rn(q, __dmul_rn(t, t));
+        double nl;
+        if (a.opt != 0) {
+          // RMSProp-IA (vb.py:436-453) / Adam-IA (vb.py:606-617): state in
+          // s_ring[0..P) (second moment) and s_ring[P..2P) (first moment); the
+          // history keeps the PRE-update parameters of the last n_hist iterations.
+          const double old = s_lam[p];
+          if (i >= a.hist_start) a.hist[((long long)prob * a.n_hist + (i - a.hist_start)) * P + p] = old;
+          const double g2 = __dmul_rn(gp, gp);
+          if (a.opt == 1) {
+            const double sgs = i == 0 ? g2 : __dadd_rn(__dmul_rn(s_ring[p], 0.9), __dmul_rn(1.0 - 0.9, g2));
+            s_ring[p] = sgs;
+            nl = __dsub_rn(old, __dmul_rn(a.lr.at(i), gp) / sqrt(__dadd_rn(a.eps, sgs)));
+          } else {
+            const double v = i == 0 ? __dmul_rn(0.9, g2)
+                                    : __dadd_rn(__dmul_rn(s_ring[p], 0.999), __dmul_rn(1.0 - 0.999, g2));
+            const double m = i == 0 ? __dmul_rn(0.9, gp)
+                                    : __dadd_rn(__dmul_rn(s_ring[P + p], 0.9), __dmul_rn(1.0 - 0.9, gp));
+            s_ring[p] = v;
+            s_ring[P + p] = m;
+            const double mh = m / (1.0 - pow(0.9, (double)(i + 2)));
+            const double vh = v / (1.0 - pow(0.999, (double)(i + 2)));
+            nl = __dsub_rn(old, __dmul_rn(a.lr.at(i), mh) / sqrt(__dadd_rn(a.eps, vh)));
+          }
+        } else {
+          s_ring[slot * P + p] = gp;
+          const int cnt = (i + 1 < W) ? (int)(i + 1) : W;
+          const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;  // (i + 1) % W
+          double q = 0.0;
+          for (int k = 0; k < cnt; ++k) {
+            int Lk = oldest + k;
+            if (Lk >= W) Lk -= W;
+            const double t = s_ring[Lk * P + p];
+            q = __dadd_rn(q, __dmul_rn(t, t));
+          }
+          nl = __dsub_rn(s_lam[p], __dmul_rn(a.lr.at(i), gp) / sqrt(__dadd_rn(a.eps, q)));
+          if (i >= a.hist_start) a.hist[((long long)prob * a.n_hist + (i - a.hist_start)) * P + p] = nl;
         }
-        const double nl = __dsub_rn(s_lam[p], __dmul_rn(a.lr.at(i), gp) / sqrt(__dadd_rn(a.eps, q)));
-        s_lam[p] = nl;  // only thread p reads/writes s_lam[p] until the barrier below
-        if (i >= a.hist_start) a.hist[((long long)prob * a.n_hist + (i - a.hist_start)) * P + p] = nl;
+        s_lam[p] = nl;  // only thread p reads/writes s_lam[p] / s_sg[p - D] until the barrier
+        if (p >= D) s_sg[p - D] = exp(nl);
       }
     }
-    if (tid == 0) {
+    if (tid == val_tid) {
       double val;
       if (!a.chivi) {
         // entropy uses the pre-update lam: sum_d log sigma_d
-        double sl = 0.0;
-        for (int d = 0; d < D; ++d) sl += lsg[d];
         val = a.pd ? -(s_red[0][2 * DMAX] / dN) : -(c0 + sl + s_red[0][2 * DMAX] / dN);
       } else {
         val = log(s_red[0][2 * DMAX] / dN) / a.alpha + M;
       }
       a.values[(long long)prob * a.n_iters + (a.emit_grad ? 0 : i)] = val;
     }
+    VB_PH(5);
+    slot = slot + 1 == W ? 0 : slot + 1;
     __syncthreads();
+    VB_PH(6);
   }
+#ifdef VB_BLOCK_PROF
+  if (prob == 0 && tid == 0) {
+    const unsigned long long tw = wall_clock64() - tw0, tc = clock64() - tc0;
+    printf("BLOCKPROF D=%d N=%d NT=%d RW=%d pipe=%d steps=%d wall_ticks=%llu cycles=%llu | exp %llu draw %llu row %llu chivi %llu bsum %llu upd %llu bar %llu\n",
+           D, N, NT, RW, L.pipe, a.n_steps, tw, tc, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6]);
+  }
+#endif
+#undef VB_PH
 
   if (!a.emit_grad) {
     for (int p = tid; p < P; p += NT) lam_g[p] = s_lam[p];
@@ -884,16 +1017,14 @@ hipError_t launch_sep(int fam, int tgt, bool host, const SepArgs& a, hipStream_t
 // Threads per problem: the draws of one step spread over ceil(N/64) waves (<= 4).
 // Threads per problem: host noise -> one thread per sample (<= 4 waves); Philox ->
 // enough waves for the (sample, pair) draw items of a step (<= 8 waves).
-inline unsigned block_threads(int N, int D, bool host) {
-  const long long items = host ? N : (long long)N * ((D + 1) / 2);
-  const int cap = host ? 4 : kBlockMaxThreads / 64;
-  return 64u * (unsigned)std::min<long long>(cap, std::max<long long>(1, (items + 63) / 64));
+inline unsigned block_threads(const BlockArgs& a, bool host) {
+  return (unsigned)block_layout(a.N, a.D, host, a.chivi || a.pd).nt;
 }
 
 template <class TGT, int DM>
 static hipError_t block_dispatch_dm(int fam, bool host, const BlockArgs& a, int nprob,
                                     hipStream_t s) {
-  const dim3 grid(nprob), block(block_threads(a.N, a.D, host));
+  const dim3 grid(nprob), block(block_threads(a, host));
   if (host && fam == 1) {
     hipLaunchKernelGGL((block_kernel<TGT, true, true, DM>), grid, block, 0, s, a);
   } else if (host) {
