@@ -49,7 +49,8 @@ def config1(cpu_s):
     lam0 = np.array([0., 0., 1., 1.])
     fam = vb.mean_field_gaussian_variational_family(D, rng='philox')
     obj = vb.black_box_klvi(fam, targets.mixture(D), N)
-    vb.adagrad_optimize(50, obj, lam0)           # warm-up (module load, kernels)
+    vb.adagrad_optimize(iters, obj, lam0)        # warm-up (module load, kernels, first
+                                                 # pageable-copy staging of this size)
     _sync()
     t0 = time.perf_counter()
     sm = vb.adagrad_optimize(iters, obj, lam0)[0]

@@ -459,10 +459,13 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
     }
   };
 
+  __syncthreads();  // Box-Muller tables, lam, ring and sigma are in LDS
   if constexpr (!HOST) {
-    if (L.pipe && a.n_steps > 0) draw_item(tid, NT, N * NP, 0, a.rng_step0, s_e);
+    if (L.pipe && a.n_steps > 0) {
+      draw_item(tid, NT, N * NP, 0, a.rng_step0, s_e);
+      __syncthreads();
+    }
   }
-  __syncthreads();
 
 #ifdef VB_BLOCK_PROF
   unsigned long long ph[7] = {0, 0, 0, 0, 0, 0, 0};
