@@ -213,6 +213,32 @@ def test_many_problems_one_launch():
         np.testing.assert_allclose(smooth[r], ores[0], rtol=1e-7, atol=1e-9)
 
 
+@pytest.mark.parametrize('kind,df,objective,N', [('gauss', None, 'klvi', 100), ('t', 40.0, 'klvi', 100),
+                                                 ('t', 40.0, 'chivi', 128), ('gauss', None, 'klvi', 600)])
+def test_many_problems_first_steps(kind, df, objective, N):
+    """96 problems x 3 steps in one launch: every workgroup's first draws (the
+    pipelined prologue reads the LDS Box-Muller tables) and the draw/row
+    overlap of the next steps match the oracle.  N = 600 takes the chunked
+    (non-overlapped) layout."""
+    vb, targets, vo, ro = _mods()
+    D, n_iters, R = 10, 3, 96
+    fam = _family(vb, kind, df, D, 'philox')
+    tgt = targets.funnel(D)
+    obj = (vb.black_box_klvi(fam, tgt, N) if objective == 'klvi'
+           else vb.black_box_chivi(2.0, fam, tgt, N))
+    inits = np.random.RandomState(5).randn(R, 2 * D) * 0.3
+    run = vb.DeviceRun(obj, n_iters, inits, learning_rate=0.05)
+    run.advance_philox(n_iters, seed=3, stream=7, step=0)
+    lam, hist, vals, smooth = run.result()
+    ofam = vo.Family(kind, D, df)
+    for r in range(R):
+        eps_fn = lambda i, r=r: ro.noise(3, 7 + r, i, N, D, kind, df or 0.0)
+        ores = _oracle_run(vo, ofam, objective, 'funnel', n_iters, inits[r], N,
+                           eps_fn=eps_fn, learning_rate=0.05)
+        np.testing.assert_allclose(vals[r], ores[2], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(lam[r], ores[1][-1], rtol=1e-9, atol=1e-11)
+
+
 def test_foreign_objective_device_update():
     """A plain Python objective runs with the device adagrad update kernel."""
     vb, targets, vo, _ = _mods()
