@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 D, N, WINDOW, LR, EPS = 10_000, 128, 10, 0.01, 0.1
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+VALU_PEAK_GINSTR = 256 * 4 * 2.4 / 4  # wave64 fp64 VALU issue: 4 cycles/instr/SIMD (profiles/r01/ubench_instr_costs.txt)
 CHUNK = 256                    # steps per sep_kernel launch (vb_capi.hip max_chunk)
 
 
@@ -177,6 +178,17 @@ def main():
                 tr = json.load(open(prof))
                 line['roofline']['traffic'] = tr.get('bytes_per_launch')
                 line['roofline']['traffic_source'] = tr.get('source')
+                if tr.get('valu_instr_per_launch'):
+                    # the kernel's real ceiling: fp64 VALU issue
+                    ins = float(tr['valu_instr_per_launch'])
+                    rate = ins / launch_s / 1e9
+                    line['valu'] = {'instr_per_launch': ins, 'achieved': rate,
+                                    'peak': VALU_PEAK_GINSTR, 'unit': 'G wave-instr/s',
+                                    'frac': rate / VALU_PEAK_GINSTR,
+                                    'source': 'SQ_INSTS_VALU (rocprofv3 --pmc, '
+                                              'profiles/r01/bench_pmc_summary.json) / live '
+                                              'launch time; peak = 256 CUs x 4 SIMDs x 2.4 GHz '
+                                              '/ 4 cycles per wave64 fp64 instruction'}
             except Exception:
                 pass
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N = 1 only

@@ -49,6 +49,8 @@ def main(rnd='r01', src=os.path.join(ROOT, 'gpurun_out', 'prof')):
                          '8-B accesses); per sep_kernel launch of 256 steps; kernel %s' % (rnd, k),
                'fetch_kb_raw': fetch, 'write_kb': write,
                'bytes_per_launch': int(round((2 * fetch + write) * 1024))}
+        if 'SQ_INSTS_VALU' in summary[k]:
+            out['valu_instr_per_launch'] = summary[k]['SQ_INSTS_VALU']['mean_per_dispatch']
         json.dump(out, open(os.path.join(ROOT, 'profiles', 'traffic.json'), 'w'), indent=1)
         print(json.dumps(out))
     if stats:
