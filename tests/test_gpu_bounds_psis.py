@@ -237,3 +237,58 @@ def test_improve_with_psis_vs_oracle():
     np.testing.assert_allclose(c, oc, rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(res['khat'], khat, rtol=1e-9)
     np.testing.assert_allclose(res['mean_error'], np.linalg.norm(true_mean - om), rtol=1e-8)
+
+
+def test_device_resident_chain_matches_host():
+    """log weights -> all_bounds -> psislw with the log weights kept in HBM (a
+    float64 device tensor) give bitwise the host-array results."""
+    import torch
+    from viabel_amd import vb, targets, experiments, bounds, psis
+    tgt = targets.eight_schools_ncp()
+    lam = np.random.RandomState(1).randn(20) * 0.3
+    M = 200_000
+    fams = [vb.mean_field_t_variational_family(10, 40.0, rng='philox') for _ in range(2)]
+    for f in fams:
+        f.stream = 4242                      # identical draws for both paths
+    _, lw_h = experiments.log_weights(tgt, fams[0], lam, M, return_samples=False)
+    lw_d = torch.empty(M, dtype=torch.float64, device='cuda')
+    xs, out = experiments.log_weights(tgt, fams[1], lam, M, return_samples=False, lw_out=lw_d)
+    assert xs is None and out is lw_d
+    np.testing.assert_array_equal(lw_d.cpu().numpy(), lw_h)
+    kw = dict(q_var=fams[0].mean_and_cov(lam)[1], moment_bound_fn=lambda p: fams[0].pth_moment(p, lam))
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        bh = bounds.all_bounds(lw_h, **kw)
+        bd = bounds.all_bounds(lw_d, **kw)
+    assert bh == bd
+    oh, kh = psis.psislw(lw_h)
+    od, kd = psis.psislw(lw_d)
+    assert kd == kh and isinstance(od, torch.Tensor)
+    np.testing.assert_array_equal(od.cpu().numpy(), oh)
+    with pytest.raises(ValueError):
+        experiments.log_weights(tgt, fams[1], lam, M + 1, return_samples=False, lw_out=lw_d)
+
+
+def test_run_restarts_records_match_host_recomputation():
+    """restarts.run_restarts (device-resident bounds stage) == each restart's
+    record recomputed with host arrays from the same fitted parameters."""
+    from viabel_amd import vb, targets, restarts, experiments, bounds, psis
+    fac = lambda: vb.mean_field_t_variational_family(10, 40.0, rng='philox')
+    tgt = targets.eight_schools_ncp()
+    R, iters, M = 3, 40, 30_000
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        tab = restarts.run_restarts(fac, tgt, R, iters, n_samples=50, n_bounds=M)
+        assert tab.shape == (R, len(restarts.RECORD_HEAD) + 20)
+        for j in range(R):
+            r = int(tab[j, 0])
+            opt = tab[j, len(restarts.RECORD_HEAD):]
+            bfam = fac()
+            bfam.stream = (1 << 20) + r
+            _, lw = experiments.log_weights(tgt, bfam, opt, M, return_samples=False)
+            res = bounds.all_bounds(lw, q_var=bfam.mean_and_cov(opt)[1],
+                                    moment_bound_fn=lambda p: bfam.pth_moment(p, opt))
+            _, khat = psis.psislw(lw)
+            expect = [r, np.mean(lw), res['d2'], res['W1'], res['W2'], res['mean_error'],
+                      res['std_error'], res['cov_error'], khat]
+            np.testing.assert_allclose(tab[j, :9], expect, rtol=1e-12, atol=1e-14)

@@ -230,6 +230,18 @@ def dptr(a):
     return ctypes.cast(ctypes.c_void_p(a.data_ptr()), c_double_p)
 
 
+def device_tensor(a):
+    """`a` if it is a torch tensor in device memory (checked: contiguous
+    float64), else None.  Device tensors go to the C ABI as device pointers,
+    so chained calls (log weights -> bounds -> PSIS) stay in HBM."""
+    if not getattr(a, 'is_cuda', False) or not hasattr(a, 'data_ptr'):
+        return None
+    import torch
+    if a.dtype != torch.float64 or not a.is_contiguous():
+        raise TypeError('expected a contiguous float64 device tensor')
+    return a
+
+
 def i64ptr(a):
     if a is None:
         return None

@@ -32,10 +32,15 @@ def _mc_warning(m, s, quantity_name, atol=0.01, rtol=0.0):
 
 
 def _device_divergence(log_weights, alpha, log_norm_bound):
-    lw = nat.as_f64(np.ravel(np.asarray(log_weights)))
+    lw = nat.device_tensor(log_weights)   # HBM-resident log weights are read in place
+    if lw is None:
+        lw = nat.as_f64(np.ravel(np.asarray(log_weights)))
+    else:
+        lw = lw.reshape(-1)
     out = np.empty(7)
     has = log_norm_bound is not None
-    nat.check(nat.lib().vb_divergence_bound(nat.context().handle, nat.dptr(lw), lw.size,
+    nat.check(nat.lib().vb_divergence_bound(nat.context().handle, nat.dptr(lw), int(lw.numel()
+                                            if hasattr(lw, 'numel') else lw.size),
                                             float(alpha), int(has),
                                             float(log_norm_bound) if has else 0.0,
                                             nat.dptr(out)))

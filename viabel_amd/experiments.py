@@ -19,12 +19,21 @@ __all__ = ['get_samples_and_log_weights', 'psis_correction', 'log_weights', 'che
            'improve_with_psis', 'weighted_mean_and_cov']
 
 
-def log_weights(logdensity, var_family, var_param, n_samples, return_samples=True):
+def log_weights(logdensity, var_family, var_param, n_samples, return_samples=True,
+                lw_out=None):
+    """(samples [m, D] or None, lw [m]).  `lw_out`: a float64 device tensor of m
+    entries to write the log weights into (they stay in HBM for the bounds /
+    PSIS calls that follow)."""
     if not isinstance(logdensity, Target):
         raise TypeError('log weights on the device need a viabel_amd.targets target')
     lam = nat.as_f64(var_param)
     m = int(n_samples)
-    lw = np.empty(m)
+    if lw_out is not None:
+        lw = nat.device_tensor(lw_out)
+        if lw is None or lw.numel() != m:
+            raise ValueError('lw_out must be a float64 device tensor of n_samples entries')
+    else:
+        lw = np.empty(m)
     xs = np.empty((m, var_family.dim)) if return_samples else None
     if var_family.rng == 'numpy':
         eps = nat.as_f64(var_family._draw(m))

@@ -22,7 +22,12 @@ def _tail_cap(n, Reff):
 
 
 def psislw_with_tail(lw, Reff=1.0):
-    lw = np.asarray(lw, dtype=float)
+    """psislw plus the tail order of each column.  A float64 device tensor
+    input stays in HBM: the smoothed log weights come back as a device tensor
+    of shape (n, m); k and the tail orders are host arrays."""
+    dev = nat.device_tensor(lw)
+    if dev is None:
+        lw = np.asarray(lw, dtype=float)
     if lw.ndim == 2:
         n, m = lw.shape
     elif lw.ndim == 1:
@@ -31,8 +36,13 @@ def psislw_with_tail(lw, Reff=1.0):
         raise ValueError("Argument `lw` must be 1 or 2 dimensional.")
     if n <= 1:
         raise ValueError("More than one log-weight needed.")
-    src = nat.as_f64(lw.reshape(n, m))
-    out = np.empty((n, m))
+    if dev is None:
+        src = nat.as_f64(lw.reshape(n, m))
+        out = np.empty((n, m))
+    else:
+        import torch
+        src = dev.reshape(n, m)
+        out = torch.empty((n, m), dtype=torch.float64, device=dev.device)
     k = np.empty(m)
     cap = _tail_cap(n, Reff)
     tail = np.empty((m, max(cap, 1)), dtype=np.int64)
@@ -48,6 +58,8 @@ def psislw(lw, Reff=1.0, overwrite_lw=False):
     """Pareto smoothed importance sampling (PSIS).  Returns (lw_out, kss);
     kss is a scalar for 1-D input (psis.py:204-206)."""
     out, k, _ = psislw_with_tail(lw, Reff)
+    if nat.device_tensor(lw) is not None:   # device in, device out (no copy to the host)
+        return (out[:, 0], k[0]) if lw.ndim == 1 else (out, k)
     lw_arr = np.asarray(lw)
     if lw_arr.ndim == 1:
         res = out[:, 0]

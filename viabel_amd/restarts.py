@@ -48,15 +48,19 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
                        learning_rate_end=learning_rate_end)
     run.advance_philox(n_iters, seed, stream_base, 0, stream_stride=stride)
     _, _, vals, smooth = run.result()
+    # the M log weights of each restart stay in HBM from the draws through the
+    # bounds and PSIS (one device buffer, reused)
+    import torch
+    lw = torch.empty(int(n_bounds), dtype=torch.float64, device=torch.device('cuda', nat.context().device))
     recs = []
     for j, r in enumerate(ids):
         opt = smooth[j]
         bfam = family_factory()
         bfam.stream = (1 << 20) + r          # bound draws: a Philox stream of their own
-        _, lw = experiments.log_weights(target, bfam, opt, n_bounds, return_samples=False)
-        elbo = float(np.mean(lw))
+        experiments.log_weights(target, bfam, opt, n_bounds, return_samples=False, lw_out=lw)
         res = bounds.all_bounds(lw, q_var=bfam.mean_and_cov(opt)[1],
                                 moment_bound_fn=lambda p: bfam.pth_moment(p, opt))
+        elbo = float(res['log_norm_bound'])  # = mean log weight (bounds.py:170-172)
         _, khat = psis.psislw(lw)
         recs.append(np.concatenate([[r, elbo, res['d2'], res['W1'], res['W2'],
                                      res['mean_error'], res['std_error'], res['cov_error'],
