@@ -28,6 +28,9 @@
  *                          halfway drivers)
  *   vb_iterate_average     viabel/functions.py:68-77 (stochastic_iterate_averaging)
  *   vb_adagrad_update      viabel/vb.py:364-374 (one adagrad step for a foreign objective)
+ *   vb_adagrad_update_scaled  viabel/vb.py:364-374 with has_log_norm (grad_scale, :371-373)
+ *   vb_ia_update           viabel/vb.py:436-453, 606-617 (one RMSProp-IA / Adam-IA step for a
+ *                          foreign objective, or with avg_grad_norm)
  *   vb_log_weights         notebooks/experiments.py:60-63 (get_samples_and_log_weights)
  *   vb_divergence_bound    viabel/bounds.py:142-192 (divergence_bound, mean_and_check_mc_error)
  *   vb_centered_moments    viabel/bounds.py:127-135 (wasserstein_bounds sample moments)
@@ -141,7 +144,8 @@ typedef struct vb_noise {
 enum vb_optimizer_kind {
   VB_OPT_ADAGRAD = 0,      /* adagrad_optimize, vb.py:345-389 (window of W gradients) */
   VB_OPT_RMSPROP_IA = 1,   /* rmsprop_IA_optimize_with_rhat's update, vb.py:436-453 */
-  VB_OPT_ADAM_IA = 2       /* adam_IA_optimize_with_rhat's update, vb.py:606-617 */
+  VB_OPT_ADAM_IA = 2,      /* adam_IA_optimize_with_rhat's update, vb.py:606-617 */
+  VB_OPT_RMSPROP_IA_NORM = 3 /* rmsprop_IA with avg_grad_norm=True (vb_ia_update only) */
 };
 
 /* Optimiser settings, vb.py:345-347 defaults: window 10, lr .01, eps .1.
@@ -218,6 +222,23 @@ int vb_run_destroy(vb_run* run);
 int vb_adagrad_update(vb_ctx* ctx, int64_t P, double* lam, const double* grad,
                       double* ring, int32_t window, int64_t step, double lr,
                       double epsilon);
+/* vb_adagrad_update for objectives with log norms (has_log_norm=True,
+ * vb.py:371-373): window_scale [min(step + 1, window)] holds, oldest first, the
+ * reference's grad_scale = exp(min(log_norms) - log_norm_j) over the window;
+ * accum = sum_j (window_scale_j g_j)^2. */
+int vb_adagrad_update_scaled(vb_ctx* ctx, int64_t P, double* lam, const double* grad,
+                             double* ring, int32_t window, int64_t step, double lr,
+                             double epsilon, const double* window_scale);
+/* One RMSProp-IA (vb.py:436-453) or Adam-IA (vb.py:606-617) step for a
+ * caller-supplied gradient.  lam [P] and state [2][P] are DEVICE pointers
+ * (state row 0: second moment, row 1: first moment; zeros before step 0);
+ * old_out (nullable) receives the pre-update lam, which the reference's
+ * history keeps.  VB_OPT_RMSPROP_IA_NORM is avg_grad_norm=True: every
+ * coordinate is divided by sqrt(epsilon + norm2), with norm2 the reference's
+ * scalar sum_grad_squared (vb.py:443-451); norm2 is ignored otherwise. */
+int vb_ia_update(vb_ctx* ctx, int32_t optimizer, int64_t P, double* lam, const double* grad,
+                 double* state, int64_t step, double lr, double epsilon, double norm2,
+                 double* old_out);
 
 /* ---- convergence diagnostics (functions.py:8-77) ------------------------ */
 /* Split-chain R-hat (compute_R_hat) of chains [n_chains][n_iters][P] on n_jobs

@@ -69,11 +69,14 @@ def stochastic_iterate_averaging(estimate, start):
 def _ia_optimize(kind, n_iters, objective_and_grad, init_param, K, window=500,
                  learning_rate=.01, epsilon=.000001, rhat_window=500, n_optimisers=1,
                  r_mean_threshold=1.15, r_sigma_threshold=1.20, tail_avg_iters=2000,
-                 learning_rate_end=None, perturb=None):
-    """vb.py:392-553 (rmsprop, avg_grad_norm=False, has_log_norm=False) and
-    vb.py:556-712 (adam).  `perturb(o, P)` replaces the global-RNG init
-    perturbation draw (stats.norm.rvs after np.random.seed(o)) when given."""
+                 learning_rate_end=None, perturb=None, has_log_norm=False, avg_grad_norm=False):
+    """vb.py:392-553 (rmsprop; avg_grad_norm: the scalar sum of squares, or
+    exp(log_norm), normalises every coordinate, vb.py:443-451) and vb.py:556-712
+    (adam).  has_log_norm: the objective returns (value, grad, log_norm).
+    `perturb(o, P)` replaces the global-RNG init perturbation draw
+    (stats.norm.rvs after np.random.seed(o)) when given."""
     value_history = []
+    log_norm_history = []
     lam = init_param.copy()
     hist_list, final_list = [], []
     scale = 0.5 if kind == 'rmsprop' else 0.2
@@ -85,11 +88,20 @@ def _ia_optimize(kind, n_iters, objective_and_grad, init_param, K, window=500,
             lam = init_param + z * (o + 1) * scale
         sched = vb_oracle.learning_rate_schedule(n_iters, learning_rate, learning_rate_end)
         for i, lr in zip(range(n_iters), sched):
-            val, g = objective_and_grad(lam)
+            if has_log_norm:
+                val, g, ln = objective_and_grad(lam)
+            else:
+                val, g = objective_and_grad(lam)
+                ln = 0
             value_history.append(val)
+            log_norm_history.append(ln)
             old = lam.copy()
             if kind == 'rmsprop':
-                sgs = g ** 2 if i == 0 else sgs * 0.9 + (1. - 0.9) * g ** 2
+                if avg_grad_norm:
+                    gn = np.exp(ln) if has_log_norm else np.sum(g ** 2, axis=0)
+                    sgs = gn if i == 0 else gn * 0.9 + (1. - 0.9) * gn
+                else:
+                    sgs = g ** 2 if i == 0 else sgs * 0.9 + (1. - 0.9) * g ** 2
                 lam = lam - lr * g / np.sqrt(epsilon + sgs)
             else:
                 if i == 0:
@@ -127,7 +139,7 @@ def _ia_optimize(kind, n_iters, objective_and_grad, init_param, K, window=500,
            'r_hat_mean': rm, 'r_hat_sigma': rs,
            'r_hat_mean_halfway': rhats_halfway[:, :K], 'r_hat_sigma_halfway': rhats_halfway[:, K:]}
     return (lam, chains, means, sigmas, np.array(value_history),
-            np.zeros(len(value_history)), log)
+            np.array(log_norm_history, dtype=float), log)
 
 
 def rmsprop_IA_optimize_with_rhat(*args, **kw):

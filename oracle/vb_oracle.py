@@ -163,25 +163,39 @@ def learning_rate_schedule(n_iters, learning_rate, learning_rate_end):
 
 
 def adagrad_optimize(n_iters, objective_and_grad, init_param, window=10,
-                     learning_rate=.01, epsilon=.1, learning_rate_end=None):
-    """vb.py:345-389 with has_log_norm=False (grad_scale == 1)."""
+                     learning_rate=.01, epsilon=.1, learning_rate_end=None, has_log_norm=False):
+    """vb.py:345-389.  has_log_norm: the objective returns (value, grad, log_norm)
+    and the window's gradients are scaled by exp(min log_norm - log_norm_j)
+    (vb.py:365-373)."""
     grads = []
     values = []
+    log_norms, local_log_norms = [], []
     lam = init_param.copy()
     hist = []
     for i, lr in enumerate(learning_rate_schedule(n_iters, learning_rate, learning_rate_end)):
-        val, g = objective_and_grad(lam)
+        if has_log_norm:
+            val, g, ln = objective_and_grad(lam)
+        else:
+            val, g = objective_and_grad(lam)
+            ln = 0
         values.append(val)
+        log_norms.append(ln)
         grads.append(g)
+        local_log_norms.append(ln)
         if len(grads) > window:
             grads.pop(0)
-        acc = np.sum(np.array(grads) ** 2, axis=0)
+            local_log_norms.pop(0)
+        if has_log_norm:
+            scale = np.exp(np.min(local_log_norms) - np.array(local_log_norms))
+            acc = np.sum((scale[:, np.newaxis] * np.array(grads)) ** 2, axis=0)
+        else:
+            acc = np.sum(np.array(grads) ** 2, axis=0)
         lam = lam - lr * g / np.sqrt(epsilon + acc)
         if i >= 3 * n_iters // 4:
             hist.append(lam.copy())
     hist = np.array(hist)
     smoothed = np.mean(hist, axis=0) if len(hist) else np.full(lam.shape, np.nan)
-    return smoothed, hist, np.array(values), np.zeros(n_iters)
+    return smoothed, hist, np.array(values), np.array(log_norms, dtype=float)
 
 
 def log_weights(fam, target, lam, n_samples, eps=None):

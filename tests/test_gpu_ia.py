@@ -131,3 +131,77 @@ def test_ia_optimizer_philox_chains():
     assert np.all(np.isfinite(chains)) and np.all(np.isfinite(vals))
     assert log['r_hat_mean'].shape == (4, D)
     assert len(means) == 4 and means[0].shape[1] == D
+
+
+def _foreign(kind, D, N, log_norm=False):
+    """A caller-supplied (Python) objective over the oracle's own stream; with
+    log_norm it returns (value, grad, log_norm) like has_log_norm objectives."""
+    from oracle import vb_oracle as vo
+    ofam = vo.Family(kind, D, 40.0 if kind == 't' else None)
+    tgt = 'eight_schools_ncp' if kind == 't' else 'mixture'
+
+    def f(lam):
+        v, g = vo.klvi_value_grad(ofam, tgt, lam, N)
+        if log_norm:
+            return v, g, 0.05 * float(np.sum(lam ** 2)) - 0.3
+        return v, g
+    return f
+
+
+@pytest.mark.parametrize('which', ['rmsprop', 'adam'])
+@pytest.mark.parametrize('log_norm', [False, True])
+def test_ia_optimizer_foreign_objective(which, log_norm):
+    """A Python objective with the device IA update (vb_ia_update): same chains,
+    values, log norms and averages as the reference loop (vb.py:392-712)."""
+    from viabel_amd import vb
+    from oracle import functions_oracle as fo
+    D, N, n_iters = 10, 20, 500
+    init = np.zeros(2 * D)
+    kw = dict(window=3, learning_rate=.01, rhat_window=100, n_optimisers=2, tail_avg_iters=300,
+              learning_rate_end=.001, has_log_norm=log_norm)
+    res = getattr(vb, which + '_IA_optimize_with_rhat')(n_iters, _foreign('t', D, N, log_norm),
+                                                         init, D, **kw)
+    ores = getattr(fo, which + '_IA_optimize_with_rhat')(n_iters, _foreign('t', D, N, log_norm),
+                                                          init, D, **kw)
+    assert res[1].shape == (2, 300, 2 * D)
+    _check_ia(res, ores, 1e-10)
+    _close(res[5], ores[5], 1e-14)
+
+
+@pytest.mark.parametrize('native', [False, True])
+@pytest.mark.parametrize('log_norm', [False, True])
+def test_rmsprop_avg_grad_norm(native, log_norm):
+    """avg_grad_norm=True: every coordinate scaled by the scalar sum of squared
+    gradients (or exp(log_norm)), vb.py:443-451."""
+    from viabel_amd import vb, targets
+    from oracle import functions_oracle as fo
+    if native and log_norm:
+        pytest.skip('native objectives return (value, grad)')
+    D, N, n_iters = 3, 30, 400
+    if native:
+        fam = vb.mean_field_gaussian_variational_family(D, rng='numpy')
+        obj = vb.black_box_klvi(fam, targets.mixture(D), N)
+    else:
+        obj = _foreign('gauss', D, N, log_norm)
+    init = np.full(2 * D, 0.1)
+    kw = dict(window=5, learning_rate=.02, rhat_window=100, n_optimisers=2, tail_avg_iters=200,
+              has_log_norm=log_norm)
+    res = vb.rmsprop_IA_optimize_with_rhat(n_iters, obj, init, D, avg_grad_norm=True, **kw)
+    ores = fo.rmsprop_IA_optimize_with_rhat(n_iters, _foreign('gauss', D, N, log_norm), init, D,
+                                            avg_grad_norm=True, **kw)
+    _check_ia(res, ores, 1e-10)
+
+
+def test_adagrad_foreign_has_log_norm():
+    """adagrad_optimize(has_log_norm=True): window gradients scaled by
+    exp(min log_norm - log_norm_j) (vb.py:365-373) in vb_adagrad_update_scaled."""
+    from viabel_amd import vb
+    from oracle import vb_oracle as vo
+    D, N = 10, 25
+    init = np.zeros(2 * D)
+    res = vb.adagrad_optimize(200, _foreign('t', D, N, True), init, has_log_norm=True, window=7,
+                              learning_rate=.05, learning_rate_end=.01)
+    ores = vo.adagrad_optimize(200, _foreign('t', D, N, True), init, window=7, learning_rate=.05,
+                               learning_rate_end=.01, has_log_norm=True)
+    for a, b in zip(res, ores):
+        _close(a, b, 1e-12)

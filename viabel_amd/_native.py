@@ -20,7 +20,7 @@ TARGET_ISOGAUSS, TARGET_MIXTURE, TARGET_FUNNEL, TARGET_EIGHT_SCHOOLS_NCP = 0, 1,
 TARGET_CORR_GAUSS = 4
 TARGET_CALLBACK = 5
 OBJ_KLVI, OBJ_CHIVI, OBJ_KLVI_PD = 0, 1, 2
-OPT_ADAGRAD, OPT_RMSPROP_IA, OPT_ADAM_IA = 0, 1, 2
+OPT_ADAGRAD, OPT_RMSPROP_IA, OPT_ADAM_IA, OPT_RMSPROP_IA_NORM = 0, 1, 2, 3
 NOISE_HOST, NOISE_PHILOX = 0, 1
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
@@ -88,6 +88,12 @@ _SIGNATURES = {
     'vb_adagrad_update': ([ctypes.c_void_p, ctypes.c_int64, c_double_p, c_double_p, c_double_p,
                            ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_double],
                           ctypes.c_int),
+    'vb_adagrad_update_scaled': ([ctypes.c_void_p, ctypes.c_int64, c_double_p, c_double_p,
+                                  c_double_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double,
+                                  ctypes.c_double, c_double_p], ctypes.c_int),
+    'vb_ia_update': ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, c_double_p, c_double_p,
+                      c_double_p, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                      ctypes.c_double, c_double_p], ctypes.c_int),
     'vb_log_weights': ([ctypes.c_void_p, P(Family), P(Target), c_double_p, ctypes.c_int64,
                         P(Noise), c_double_p, c_double_p], ctypes.c_int),
     'vb_divergence_bound': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_double,

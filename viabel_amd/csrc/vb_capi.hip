@@ -827,12 +827,12 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
                            : nullptr;
         if (r->opt != VB_OPT_ADAGRAD) {
           VB_HIP(vbk::launch_ia_update(r->opt, (long long)P, lam, r->grad.d(),
-                                       r->ring.d() + q * P * r->W, step, lr, r->eps, hrow,
+                                       r->ring.d() + q * P * r->W, step, lr, r->eps, 0.0, hrow,
                                        c->stream));
         } else {
           VB_HIP(vbk::launch_adagrad_update((long long)P, lam, r->grad.d(),
                                             r->ring.d() + q * P * r->W, r->W, step, lr, r->eps,
-                                            c->stream));
+                                            nullptr, c->stream));
           if (hrow)
             VB_HIP(hipMemcpyAsync(hrow, lam, sizeof(double) * P, hipMemcpyDeviceToDevice,
                                   c->stream));
@@ -978,7 +978,45 @@ int vb_adagrad_update(vb_ctx* c, int64_t P, double* lam, const double* grad, dou
     return fail(VB_EINVAL, "vb_adagrad_update keeps lam and ring on the device: pass device pointers");
   In dg;
   VB_TRY(dg.stage(c, 0, grad, (size_t)P));
-  VB_HIP(vbk::launch_adagrad_update(P, lam, dg.d, ring, window, step, lr, epsilon, c->stream));
+  VB_HIP(vbk::launch_adagrad_update(P, lam, dg.d, ring, window, step, lr, epsilon, nullptr,
+                                    c->stream));
+  return sync(c);
+}
+
+int vb_adagrad_update_scaled(vb_ctx* c, int64_t P, double* lam, const double* grad, double* ring,
+                             int32_t window, int64_t step, double lr, double epsilon,
+                             const double* window_scale) {
+  VB_TRY(check_ctx(c));
+  if (!lam || !grad || !ring || !window_scale || P < 1 || window < 1 || step < 0)
+    return fail(VB_EINVAL, "invalid argument");
+  if (!is_device_ptr(lam) || !is_device_ptr(ring))
+    return fail(VB_EINVAL, "vb_adagrad_update_scaled keeps lam and ring on the device: pass device pointers");
+  const int64_t cnt = step + 1 < window ? step + 1 : window;
+  In dg, dsc;
+  VB_TRY(dg.stage(c, 0, grad, (size_t)P));
+  VB_TRY(dsc.stage(c, 1, window_scale, (size_t)cnt));
+  VB_HIP(vbk::launch_adagrad_update(P, lam, dg.d, ring, window, step, lr, epsilon, dsc.d,
+                                    c->stream));
+  return sync(c);
+}
+
+int vb_ia_update(vb_ctx* c, int32_t optimizer, int64_t P, double* lam, const double* grad,
+                 double* state, int64_t step, double lr, double epsilon, double norm2,
+                 double* old_out) {
+  VB_TRY(check_ctx(c));
+  if (!lam || !grad || !state || P < 1 || step < 0) return fail(VB_EINVAL, "invalid argument");
+  if (optimizer != VB_OPT_RMSPROP_IA && optimizer != VB_OPT_ADAM_IA &&
+      optimizer != VB_OPT_RMSPROP_IA_NORM)
+    return fail(VB_EINVAL, "unknown optimizer %d", optimizer);
+  if (!is_device_ptr(lam) || !is_device_ptr(state))
+    return fail(VB_EINVAL, "vb_ia_update keeps lam and state on the device: pass device pointers");
+  In dg;
+  Out dold;
+  VB_TRY(dg.stage(c, 0, grad, (size_t)P));
+  VB_TRY(dold.stage(c, 1, old_out, old_out ? (size_t)P : 0));
+  VB_HIP(vbk::launch_ia_update(optimizer, P, lam, dg.d, state, step, lr, epsilon, norm2, dold.d,
+                               c->stream));
+  VB_TRY(dold.finish(c));
   return sync(c);
 }
 

@@ -89,13 +89,16 @@ hipError_t launch_log_weights(int fam, int tgt, int D, long long m, const double
                               double t_scale, double shape, double df, double t_const,
                               const double* noise, uint32_t k0, uint32_t k1, uint32_t stream,
                               uint32_t step, double* lw, double* xs, hipStream_t s);
+// scale (nullable): [min(step + 1, W)] window scales, oldest first
 hipError_t launch_adagrad_update(long long P, double* lam, const double* g, double* ring, int W,
-                                 long long step, double lr, double eps, hipStream_t s);
-// RMSProp-IA / Adam-IA step (opt 1 / 2) on device state [2][P]; old_out (nullable)
-// receives the pre-update parameters.
+                                 long long step, double lr, double eps, const double* scale,
+                                 hipStream_t s);
+// RMSProp-IA / Adam-IA step (opt 1 / 2) on device state [2][P], or (opt 3)
+// RMSProp-IA with avg_grad_norm: every coordinate divided by sqrt(eps + norm2);
+// old_out (nullable) receives the pre-update parameters.
 hipError_t launch_ia_update(int opt, long long P, double* lam, const double* g, double* state,
-                            long long step, double lr, double eps, double* old_out,
-                            hipStream_t s);
+                            long long step, double lr, double eps, double norm2,
+                            double* old_out, hipStream_t s);
 // R-hat (functions.py:8-31) of chains [nc][n][P] (row stride P) over n_jobs
 // iteration segments [start, start + len) (len even): out [n_jobs][P] (var_hat
 // in var_out when non-null).

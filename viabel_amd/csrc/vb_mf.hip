@@ -804,10 +804,13 @@ __global__ __launch_bounds__(256) void target_row_kernel(int D, long long n, con
     for (int d = 0; d < D; ++d) grad[r * D + d] = g[d];
 }
 
+// scale (nullable): per window position, oldest first, the reference's
+// grad_scale = exp(min(log_norms) - log_norm_j) of has_log_norm objectives
+// (vb.py:371-373): accum = sum_j (scale_j g_j)^2.
 __global__ __launch_bounds__(256) void adagrad_update_kernel(long long P, double* lam,
                                                              const double* g, double* ring,
                                                              int W, long long step, double lr,
-                                                             double eps) {
+                                                             double eps, const double* scale) {
   const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
   if (p >= P) return;
   const int slot = (int)(step % W);
@@ -818,7 +821,8 @@ __global__ __launch_bounds__(256) void adagrad_update_kernel(long long P, double
   for (int k = 0; k < cnt; ++k) {
     int L = oldest + k;
     if (L >= W) L -= W;
-    const double t = ring[(long long)L * P + p];
+    double t = ring[(long long)L * P + p];
+    if (scale) t = __dmul_rn(scale[k], t);
     q = __dadd_rn(q, __dmul_rn(t, t));
   }
   lam[p] = __dsub_rn(lam[p], __dmul_rn(lr, g[p]) / sqrt(__dadd_rn(eps, q)));
@@ -827,13 +831,17 @@ __global__ __launch_bounds__(256) void adagrad_update_kernel(long long P, double
 __global__ __launch_bounds__(256) void ia_update_kernel(int opt, long long P, double* lam,
                                                        const double* g, double* state,
                                                        long long i, double lr, double eps,
-                                                       double* old_out) {
+                                                       double norm2, double* old_out) {
   const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
   if (p >= P) return;
   const double old = lam[p], gp = g[p], g2 = __dmul_rn(gp, gp);
   if (old_out) old_out[p] = old;
   double nl;
-  if (opt == 1) {
+  if (opt == 3) {
+    // RMSProp-IA with avg_grad_norm (vb.py:443-451): one host-computed scalar
+    // normaliser for every coordinate
+    nl = __dsub_rn(old, __dmul_rn(lr, gp) / sqrt(__dadd_rn(eps, norm2)));
+  } else if (opt == 1) {
     const double sgs = i == 0 ? g2 : __dadd_rn(__dmul_rn(state[p], 0.9), __dmul_rn(1.0 - 0.9, g2));
     state[p] = sgs;
     nl = __dsub_rn(old, __dmul_rn(lr, gp) / sqrt(__dadd_rn(eps, sgs)));
@@ -1197,17 +1205,18 @@ hipError_t launch_log_weights(int fam, int tgt, int D, long long m, const double
 }
 
 hipError_t launch_adagrad_update(long long P, double* lam, const double* g, double* ring, int W,
-                                 long long step, double lr, double eps, hipStream_t s) {
+                                 long long step, double lr, double eps, const double* scale,
+                                 hipStream_t s) {
   hipLaunchKernelGGL(adagrad_update_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P,
-                     lam, g, ring, W, step, lr, eps);
+                     lam, g, ring, W, step, lr, eps, scale);
   return hipGetLastError();
 }
 
 hipError_t launch_ia_update(int opt, long long P, double* lam, const double* g, double* state,
-                            long long step, double lr, double eps, double* old_out,
-                            hipStream_t s) {
+                            long long step, double lr, double eps, double norm2,
+                            double* old_out, hipStream_t s) {
   hipLaunchKernelGGL(ia_update_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, opt, P,
-                     lam, g, state, step, lr, eps, old_out);
+                     lam, g, state, step, lr, eps, norm2, old_out);
   return hipGetLastError();
 }
 

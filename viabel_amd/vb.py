@@ -456,26 +456,39 @@ def _foreign_adagrad(n_iters, objective_and_grad, init_param, has_log_norm, wind
     import torch
     if not torch.cuda.is_available():
         raise RuntimeError('viabel_amd.adagrad_optimize needs a GPU')
-    if has_log_norm:
-        raise NotImplementedError('has_log_norm=True is not supported by the device optimiser')
     dev = torch.device('cuda', nat.context().device)
     lam = torch.tensor(np.asarray(init_param, dtype=float), dtype=torch.float64, device=dev)
     ring = torch.zeros((window, lam.numel()), dtype=torch.float64, device=dev)
-    values, hist = [], []
+    values, hist, log_norms, local_log_norms = [], [], [], []
     sched = learning_rate_schedule(n_iters, learning_rate, learning_rate_end)
     for i, lr in zip(range(n_iters), sched):
         torch.cuda.synchronize(dev)
-        val, g = objective_and_grad(lam.cpu().numpy())
+        if has_log_norm:
+            val, g, log_norm = objective_and_grad(lam.cpu().numpy())
+        else:
+            val, g = objective_and_grad(lam.cpu().numpy())
+            log_norm = 0
         values.append(val)
+        log_norms.append(log_norm)
         g = nat.as_f64(g)
-        nat.check(nat.lib().vb_adagrad_update(nat.context().handle, lam.numel(), nat.dptr(lam),
-                                              nat.dptr(g), nat.dptr(ring), window, i, lr,
-                                              epsilon))
+        if has_log_norm:
+            # vb.py:365-373: the window's gradients scaled by exp(min - log_norm_j)
+            local_log_norms.append(log_norm)
+            if len(local_log_norms) > window:
+                local_log_norms.pop(0)
+            scale = nat.as_f64(np.exp(np.min(local_log_norms) - np.array(local_log_norms)))
+            nat.check(nat.lib().vb_adagrad_update_scaled(
+                nat.context().handle, lam.numel(), nat.dptr(lam), nat.dptr(g), nat.dptr(ring),
+                window, i, lr, epsilon, nat.dptr(scale)))
+        else:
+            nat.check(nat.lib().vb_adagrad_update(nat.context().handle, lam.numel(),
+                                                  nat.dptr(lam), nat.dptr(g), nat.dptr(ring),
+                                                  window, i, lr, epsilon))
         if i >= 3 * n_iters // 4:
             hist.append(lam.cpu().numpy().copy())
     hist = np.array(hist)
     smooth = np.mean(hist, axis=0) if len(hist) else np.full(lam.numel(), np.nan)
-    return smooth, hist, np.array(values), np.zeros(n_iters)
+    return smooth, hist, np.array(values), np.array(log_norms, dtype=float)
 
 
 def adagrad_optimize(n_iters, objective_and_grad, init_param,
@@ -501,17 +514,22 @@ def adagrad_optimize(n_iters, objective_and_grad, init_param,
 
 def _ia_optimize(opt, n_iters, objective_and_grad, init_param, K, has_log_norm, window,
                  learning_rate, epsilon, rhat_window, n_optimisers, r_mean_threshold,
-                 r_sigma_threshold, tail_avg_iters, learning_rate_end, perturb_scale):
-    from . import functions
-    if not isinstance(objective_and_grad, NativeObjective):
-        raise NotImplementedError('the device IA optimisers need a native objective '
-                                  '(viabel_amd.vb.black_box_klvi / black_box_chivi)')
-    if has_log_norm:
+                 r_sigma_threshold, tail_avg_iters, learning_rate_end, perturb_scale,
+                 avg_grad_norm):
+    native = isinstance(objective_and_grad, NativeObjective)
+    if native and has_log_norm:
         raise ValueError('not enough values to unpack (expected 3, got 2)')
     if learning_rate <= 0:
         raise ValueError('learning rate must be positive')
     if learning_rate_end is not None and learning_rate <= learning_rate_end:
         raise ValueError('initial learning rate must be greater than final learning rate')
+    if not native or avg_grad_norm:
+        lams, hists, values, log_norms = _ia_host_chains(
+            opt, int(n_iters), objective_and_grad, np.asarray(init_param, dtype=float),
+            has_log_norm, window, learning_rate, epsilon, learning_rate_end, n_optimisers,
+            perturb_scale, avg_grad_norm)
+        return _ia_finish(lams, hists, values, log_norms, int(n_iters), K, rhat_window,
+                          r_mean_threshold, r_sigma_threshold, tail_avg_iters, n_optimisers)
     obj = objective_and_grad
     fam = obj.family
     init_param = np.asarray(init_param, dtype=float)
@@ -549,6 +567,64 @@ def _ia_optimize(opt, n_iters, objective_and_grad, init_param, K, has_log_norm, 
         fam.step += n_iters
         lam, hist, vals, _ = run.result()
         lams, hists, valss = list(lam), list(hist), list(vals)
+    values = np.concatenate(valss)
+    return _ia_finish(lams, hists, values, np.zeros(len(values)), n_iters, K, rhat_window,
+                      r_mean_threshold, r_sigma_threshold, tail_avg_iters, n_optimisers)
+
+
+def _ia_host_chains(opt, n_iters, objective_and_grad, init_param, has_log_norm, window,
+                    learning_rate, epsilon, learning_rate_end, n_optimisers, perturb_scale,
+                    avg_grad_norm):
+    """RMSProp-IA / Adam-IA chains for a caller-supplied objective (or with
+    avg_grad_norm): the objective runs where the caller's code runs, each
+    update in the device kernel vb_ia_update on device-resident state
+    (vb.py:417-468, 583-631).  Returns the final parameters and pre-update
+    histories per chain plus the value / log-norm histories of all chains."""
+    import collections
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError('viabel_amd IA optimisers need a GPU')
+    dev = torch.device('cuda', nat.context().device)
+    P = init_param.size
+    lams, hists, values, log_norms = [], [], [], []
+    alpha = 0.9
+    for o in range(n_optimisers):
+        np.random.seed(seed=o)                                        # vb.py:418 / 584
+        init = init_param.copy() if o == 0 else (
+            init_param + np.random.randn(P) * (o + 1) * perturb_scale)
+        lam = torch.tensor(init, dtype=torch.float64, device=dev)
+        state = torch.zeros((2, P), dtype=torch.float64, device=dev)
+        hist = collections.deque(maxlen=100 * window)                 # vb.py:465-466
+        sched = learning_rate_schedule(n_iters, learning_rate, learning_rate_end)
+        for i, lr in zip(range(n_iters), sched):
+            cur = lam.cpu().numpy()
+            if has_log_norm:
+                val, g, log_norm = objective_and_grad(cur)
+            else:
+                val, g = objective_and_grad(cur)
+                log_norm = 0
+            values.append(val)
+            log_norms.append(log_norm)
+            g = nat.as_f64(g)
+            kind, norm2 = opt, 0.0
+            if avg_grad_norm:
+                # vb.py:443-451 (the reference's own arithmetic, on the host scalar)
+                grad_norm = np.exp(log_norm) if has_log_norm else np.sum(g ** 2, axis=0)
+                norm2 = grad_norm if i == 0 else grad_norm * alpha + (1. - alpha) * grad_norm
+                kind = nat.OPT_RMSPROP_IA_NORM
+            nat.check(nat.lib().vb_ia_update(nat.context().handle, kind, P, nat.dptr(lam),
+                                             nat.dptr(g), nat.dptr(state), i, lr, epsilon,
+                                             float(norm2), None))
+            hist.append(cur.copy())
+        lams.append(lam.cpu().numpy())
+        hists.append(np.array(hist))
+    return lams, hists, np.array(values), np.array(log_norms, dtype=float)
+
+
+def _ia_finish(lams, hists, values, log_norms, n_iters, K, rhat_window, r_mean_threshold,
+               r_sigma_threshold, tail_avg_iters, n_optimisers):
+    """R-hat windows and iterate averaging of the chains (vb.py:486-553)."""
+    from . import functions
     chains = np.stack(hists, axis=0)
     rhats = functions.compute_R_hat_adaptive_numpy(chains, window_size=rhat_window)
     rhats_halfway = functions.compute_R_hat_halfway(chains, interval=100, start=200)
@@ -569,8 +645,7 @@ def _ia_optimize(opt, n_iters, objective_and_grad, init_param, K, has_log_norm, 
     log = {'start_avg_mean_iters': start_m, 'start_avg_sigma_iters': start_s,
            'r_hat_mean': rm, 'r_hat_sigma': rs,
            'r_hat_mean_halfway': rhats_halfway[:, :K], 'r_hat_sigma_halfway': rhats_halfway[:, K:]}
-    values = np.concatenate(valss)
-    return (lams[-1], chains, means, sigmas, values, np.zeros(len(values)), log)
+    return (lams[-1], chains, means, sigmas, values, log_norms, log)
 
 
 def rmsprop_IA_optimize_with_rhat(n_iters, objective_and_grad, init_param, K,
@@ -586,12 +661,10 @@ def rmsprop_IA_optimize_with_rhat(n_iters, objective_and_grad, init_param, K,
     chain, values, log norms, log dict).  The updates run on the device
     (vb_run, optimizer RMSPROP_IA); R-hat and averaging too (vb_rhat,
     vb_iterate_average)."""
-    if avg_grad_norm:
-        raise NotImplementedError('avg_grad_norm=True is not supported by the device optimiser')
     return _ia_optimize(nat.OPT_RMSPROP_IA, n_iters, objective_and_grad, init_param, K,
                         has_log_norm, window, learning_rate, epsilon, rhat_window, n_optimisers,
                         r_mean_threshold, r_sigma_threshold, tail_avg_iters, learning_rate_end,
-                        0.5)
+                        0.5, avg_grad_norm)
 
 
 def adam_IA_optimize_with_rhat(n_iters, objective_and_grad, init_param, K,
@@ -604,4 +677,4 @@ def adam_IA_optimize_with_rhat(n_iters, objective_and_grad, init_param, K,
     return _ia_optimize(nat.OPT_ADAM_IA, n_iters, objective_and_grad, init_param, K,
                         has_log_norm, window, learning_rate, epsilon, rhat_window, n_optimisers,
                         r_mean_threshold, r_sigma_threshold, tail_avg_iters, learning_rate_end,
-                        0.2)
+                        0.2, False)
