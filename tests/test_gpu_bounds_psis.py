@@ -292,3 +292,20 @@ def test_run_restarts_records_match_host_recomputation():
             expect = [r, np.mean(lw), res['d2'], res['W1'], res['W2'], res['mean_error'],
                       res['std_error'], res['cov_error'], khat]
             np.testing.assert_allclose(tab[j, :9], expect, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.parametrize('scale', [0.001, 1.0])
+def test_mean_and_check_mc_error(scale):
+    """bounds.py:183-192 on the device: the mean, and the warning exactly when
+    the oracle warns."""
+    from viabel_amd import bounds
+    from oracle import bounds_oracle
+    a = np.random.RandomState(4).randn(5000) * scale + 2.0
+    with warnings.catch_warnings(record=True) as w1:
+        warnings.simplefilter('always')
+        m = bounds.mean_and_check_mc_error(a, quantity_name='X')
+    with warnings.catch_warnings(record=True) as w2:
+        warnings.simplefilter('always')
+        om = bounds_oracle.mc_mean(a, 'X')
+    _close(m, om, rtol=1e-13)
+    assert len(w1) == len(w2) == (1 if scale == 1.0 else 0)

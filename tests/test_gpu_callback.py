@@ -102,3 +102,21 @@ def test_callback_exception_propagates():
     obj = vb.black_box_klvi(fam, targets.callback(bad, 4), 10)
     with pytest.raises(ValueError, match='model failed'):
         obj(np.zeros(8))
+
+
+def test_make_stan_log_density_dimension_from_family():
+    """vb.make_stan_log_density(fit) (vb.py:314-321, no dimension argument): the
+    target takes the family's dimension, here through adagrad and log weights."""
+    from viabel_amd import vb, targets, experiments
+    f1 = vb.mean_field_t_variational_family(10, 40.0, rng='numpy')
+    f2 = vb.mean_field_t_variational_family(10, 40.0, rng='numpy')
+    stan = vb.make_stan_log_density(_MockStanFit())
+    assert stan.dim is None
+    r1 = vb.adagrad_optimize(30, vb.black_box_klvi(f1, targets.eight_schools_ncp(), 20), np.zeros(20))
+    r2 = vb.adagrad_optimize(30, vb.black_box_klvi(f2, stan, 20), np.zeros(20))
+    _close(r2[1], r1[1], 1e-10)
+    _, lw1 = experiments.log_weights(targets.eight_schools_ncp(), f1, r1[0], 500)
+    _, lw2 = experiments.log_weights(stan, f2, r1[0], 500)
+    _close(lw2, lw1, 1e-11)
+    lp, g = stan.logdensity_and_grad(np.zeros((3, 10)))
+    assert lp.shape == (3,) and g.shape == (3, 10)

@@ -18,7 +18,7 @@ __all__ = [
     'error_bounds',
     'wasserstein_bounds',
     'divergence_bound'
-]
+]   # bounds.py:5-10 (mean_and_check_mc_error and the *_bound helpers are module-level, as there)
 
 
 def _mc_warning(m, s, quantity_name, atol=0.01, rtol=0.0):
@@ -29,6 +29,16 @@ def _mc_warning(m, s, quantity_name, atol=0.01, rtol=0.0):
             msg += ' when computing ' + quantity_name
         msg += ' (mean = {}, standard deviation = {})'.format(m, s)
         warn(msg)
+
+
+def mean_and_check_mc_error(a, atol=0.01, rtol=0.0, quantity_name=None):
+    """bounds.py:183-192: mean of `a` with a warning when its Monte Carlo
+    standard error std(a) / sqrt(n) exceeds rtol |mean| + atol (the mean and
+    standard error come from the device reduction of vb_divergence_bound)."""
+    out = _device_divergence(a, 2.0, None)
+    m, s = out[4], out[5]
+    _mc_warning(m, s, quantity_name, atol=atol, rtol=rtol)
+    return m
 
 
 def _device_divergence(log_weights, alpha, log_norm_bound):

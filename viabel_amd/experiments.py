@@ -26,6 +26,7 @@ def log_weights(logdensity, var_family, var_param, n_samples, return_samples=Tru
     PSIS calls that follow)."""
     if not isinstance(logdensity, Target):
         raise TypeError('log weights on the device need a viabel_amd.targets target')
+    logdensity = logdensity.bind(var_family.dim)
     lam = nat.as_f64(var_param)
     m = int(n_samples)
     if lw_out is not None:

@@ -32,8 +32,19 @@ __all__ = ['Target', 'isogauss', 'mixture', 'funnel', 'eight_schools_ncp', 'corr
 
 class Target:
     def __init__(self, kind, dim, name, params=None):
-        self.kind, self.dim, self.name = int(kind), int(dim), name
+        # dim None: a user model whose dimension is taken from the variational
+        # family it is used with (like the reference's make_stan_log_density)
+        self.kind, self.dim, self.name = int(kind), None if dim is None else int(dim), name
         self.params = None if params is None else nat.as_f64(params)
+
+    def bind(self, dim):
+        """This target for dimension `dim` (a copy when the dimension was left open)."""
+        if self.dim is None:
+            import copy
+            t = copy.copy(self)
+            t.dim = int(dim)
+            return t
+        return self
 
     _cfunc = None   # ctypes callback of a host target (kept alive with the target)
 
@@ -49,6 +60,8 @@ class Target:
 
     def logdensity_and_grad(self, x):
         x = nat.as_f64(np.atleast_2d(x))
+        if self.dim is None:
+            return self.bind(x.shape[1]).logdensity_and_grad(x)
         if x.shape[1] != self.dim:
             raise ValueError('expected x with %d columns, got %s' % (self.dim, x.shape))
         n = x.shape[0]
@@ -99,10 +112,10 @@ def corr_gauss(dim, seed=512):
     return t
 
 
-def callback(logdensity_and_grad, dim, name='callback'):
+def callback(logdensity_and_grad, dim=None, name='callback'):
     """A user model: logdensity_and_grad(x) -> (log p (n,), d log p / dx (n, d)) for
-    x of shape (n, dim) (numpy, host)."""
-    dim = int(dim)
+    x of shape (n, dim) (numpy, host).  dim None: the dimension of the family
+    the target is used with."""
 
     def _cb(user, xp, n, d, lpp, gp):
         try:
@@ -121,7 +134,7 @@ def callback(logdensity_and_grad, dim, name='callback'):
     return t
 
 
-def from_stan(fitobj, dim):
+def from_stan(fitobj, dim=None):
     """make_stan_log_density (vb.py:314-321): log_prob / grad_log_prob of a fitted
     Stan model (pystan 2 fit object), applied row by row on the host."""
     def f(x):
@@ -131,7 +144,7 @@ def from_stan(fitobj, dim):
     return callback(f, dim, 'stan')
 
 
-def torch_target(logdensity, dim, device=None):
+def torch_target(logdensity, dim=None, device=None):
     """A model written in torch: logdensity(x: tensor (n, dim)) -> (n,); the
     gradient comes from torch.autograd (on `device`, default the GPU when present)."""
     import torch

@@ -39,6 +39,7 @@ from . import _native as nat
 from .targets import Target
 
 __all__ = [
+    'make_stan_log_density',
     'mean_field_gaussian_variational_family',
     'mean_field_t_variational_family',
     't_variational_family',
@@ -279,6 +280,7 @@ class NativeObjective:
                 'built-in device target, or a user model wrapped with targets.callback / '
                 'targets.from_stan / targets.torch_target (an autograd callable cannot be '
                 'differentiated here); got %r' % (logdensity,))
+        logdensity = logdensity.bind(var_family.dim)
         if logdensity.dim != var_family.dim:
             raise ValueError('target dimension %d != family dimension %d'
                              % (logdensity.dim, var_family.dim))
@@ -340,6 +342,14 @@ def black_box_klvi_pd2(var_family, logdensity, n_samples):
     """vb.py:281-295: the same objective written with a partial over var_param
     (autograd still differentiates through it): identical value and gradient."""
     return NativeObjective(nat.OBJ_KLVI_PD, var_family, logdensity, n_samples)
+
+
+def make_stan_log_density(fitobj):
+    """vb.py:314-321: a fitted Stan model's log_prob / grad_log_prob as the
+    target (evaluated on the host per sample row; its dimension is the
+    family's, as in the reference)."""
+    from .targets import from_stan
+    return from_stan(fitobj)
 
 
 def learning_rate_schedule(n_iters, learning_rate, learning_rate_end):
