@@ -959,9 +959,10 @@ bool target_separable(int tgt) { return tgt == 0 || tgt == 1; }
 // Split of the column pairs between multi-pair (PPW_BIG) and 1-pair waves.
 // VB_SEP_MODE: "1" all single; "2" / "4" all 2- / 4-pair; "mix": per SIMD
 // (1024 of them) two 2-pair waves, then 1-pair waves for the rest; "q"
-// (default, measured fastest: profiles/r01/ab_layouts_q.json): one 4-pair wave
-// per SIMD, then 1-pair waves.  Blocks of big waves come first so round-robin
-// dispatch deals the same mix to every CU.
+// (default below 8 192 pairs, measured fastest at D = 1e4:
+// profiles/r01/ab_layouts_q.json): one 4-pair wave per SIMD, then 1-pair waves;
+// larger D generalises it (see the default branch).  Blocks of big waves come
+// first so round-robin dispatch deals the same mix to every CU.
 static int sep_split(SepArgs& a, int& big) {
   const char* e = getenv("VB_SEP_MODE");
   const int np = a.n_pairs;
@@ -977,9 +978,17 @@ static int sep_split(SepArgs& a, int& big) {
   } else if (e && e[0] == 'm') {  // "mix": two 2-pair waves + 1-pair waves per SIMD
     const int cap2 = 1024 * 2 * 2;
     pairs2 = np >= cap2 + 1024 ? cap2 : (np > 4096 ? np - 1024 : 0);
-  } else {                         // default "q": one 4-pair wave + 1-pair waves per SIMD
+  } else if (np < 2 * 4096) {      // default "q": one 4-pair wave + 1-pair waves per SIMD
     big = 4;
     pairs2 = np > 4096 + 1024 ? 4096 : (np > 1024 ? np - 1024 : 0);
+  } else {
+    // larger D: L layers of one 4-pair wave per SIMD and the rest in 1-pair
+    // waves while that stays within ~4 resident waves per SIMD; beyond, all
+    // 4-pair waves (their fixed per-step cost per pair is ~4x lower:
+    // profiles/r01_sweep_layouts.json)
+    big = 4;
+    const int layers = np / 4096, rest = np - 4096 * layers;
+    pairs2 = layers + (rest + 1023) / 1024 <= 4 ? 4096 * layers : np;
   }
   pairs2 -= pairs2 % (4 * big);   // whole blocks of 4 big waves
   a.pairs2 = pairs2;
