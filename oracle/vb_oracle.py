@@ -88,6 +88,11 @@ class Family:
         return c ** 2 * (2 * (self.df - 1) / (self.df - 4) * np.sum(s ** 4) + np.sum(s ** 2) ** 2)
 
 
+def _target(target):
+    """A target name of targets_oracle.TARGETS, or a callable x -> (log p, grad)."""
+    return target if callable(target) else targets_oracle.TARGETS[target]
+
+
 def klvi_value_grad(fam, target, lam, n_samples, eps=None):
     """black_box_klvi (vb.py:236-245): value = -(H + mean log p), analytic grad.
 
@@ -95,7 +100,7 @@ def klvi_value_grad(fam, target, lam, n_samples, eps=None):
     if eps is None:
         eps = fam.draw(n_samples)
     x = fam.transform(lam, eps)
-    lp, g = targets_oracle.TARGETS[target](x)
+    lp, g = _target(target)(x)
     value = -(fam.entropy(lam) + np.mean(lp))
     _, ls = fam.split(lam)
     gmu = -np.mean(g, axis=0)
@@ -111,7 +116,7 @@ def klvi_pd_value_grad(fam, target, lam, n_samples, eps=None):
     if eps is None:
         eps = fam.draw(n_samples)
     x = fam.transform(lam, eps)
-    lp, g = targets_oracle.TARGETS[target](x)
+    lp, g = _target(target)(x)
     value = -(np.mean(lp) - np.mean(fam.logdensity(x, lam)))
     _, ls = fam.split(lam)
     gmu = -np.mean(g, axis=0)
@@ -130,7 +135,7 @@ def chivi_value_grad(fam, target, lam, n_samples, alpha, eps=None):
         seed = np.random.randint(2 ** 32)
         eps = fam.draw(n_samples, seed)
     x = fam.transform(lam, eps)
-    lp, g = targets_oracle.TARGETS[target](x)
+    lp, g = _target(target)(x)
     lw = lp - fam.logdensity(x, lam)
     log_norm = np.max(lw)
     w = np.exp(lw - log_norm) ** alpha
@@ -203,5 +208,5 @@ def log_weights(fam, target, lam, n_samples, eps=None):
     if eps is None:
         eps = fam.draw(n_samples)
     x = fam.transform(lam, eps)
-    lp, _ = targets_oracle.TARGETS[target](x)
+    lp, _ = _target(target)(x)
     return x, lp - fam.logdensity(x, lam)
