@@ -31,41 +31,97 @@ namespace vbk {
 // -------------------------------------------------------------------------
 // column-pair persistent KLVI kernel
 // -------------------------------------------------------------------------
-// Reduce-scatter of the four per-lane partial sums (gA, gB, hA, hB) over the
-// LPP = 64 / PPW lanes of one column pair: lane l ends with the group total of
-// quantity (l & 3).  Two DPP exchange steps hand each lane one quantity; two
-// row rotations (16 lanes) and, for groups wider than a row, permlane swaps
-// finish the sum: about a third of the instructions of four all-reduces.
-template <int PPW>
-__device__ __forceinline__ double reduce_scatter4(int lane, double gA, double gB, double hA,
-                                                  double hB) {
-  const bool b0 = lane & 1, b1 = lane & 2;
-  double kg = b0 ? gB : gA, kh = b0 ? hB : hA;
-  kg += dpp_f64<0xB1>(b0 ? gA : gB);  // quad_perm [1,0,3,2]: partner keeps the other column
-  kh += dpp_f64<0xB1>(b0 ? hA : hB);
-  double k = b1 ? kh : kg;
-  k += dpp_f64<0x4E>(b1 ? kg : kh);   // quad_perm [2,3,0,1]
-  return stride4_sum<PPW>(k);
+// DPP move with an undefined "old" operand.  Every control used by the
+// column-pair kernel (quad_perm, row_ror, row_newbcast) reads a lane of the same
+// row, and the kernel reduces with all 64 lanes active, so "old" is never
+// selected: leaving it undefined spares the v_mov that would initialise it.
+template <int CTRL>
+__device__ __forceinline__ double dppu_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
 }
 
-// Sum over the lanes of one column-pair group (all lanes get their group's total).
-template <int PPW>
-__device__ __forceinline__ double group_sum(double v) {
-  v += dpp_f64<0xB1>(v);
-  v += dpp_f64<0x4E>(v);
-  return stride4_sum<PPW>(v);
+// Sum over the 16 lanes of each DPP row.  Pairwise symmetric steps (xor 1,
+// xor 2, half mirror, mirror): every lane of the row gets the bitwise-identical
+// total, so the owner lanes of a parameter evolve it identically.
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dppu_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dppu_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dppu_f64<0x141>(v);  // row_half_mirror
+  return v + dppu_f64<0x140>(v);  // row_mirror
 }
 
-// Value of lane (group base + K) for every lane of the group.  4 pairs per
-// wave: a group is one DPP row, so row_newbcast:K (dpp_ctrl 0x150 + K) does it;
-// 2 pairs: newbcast, then permlane16_swap copies each even row into the odd
-// row above it; 1 pair: readlane (the value is wave-uniform).
+// Sum over lanes l = c (mod 4) of a group of 64/PPW lanes (PPW >= 2).
+template <int PPW>
+__device__ __forceinline__ double stride4_sumu(double k) {
+  k += dppu_f64<0x124>(k);  // row_ror:4
+  k += dppu_f64<0x128>(k);  // row_ror:8
+  if constexpr (PPW == 2) k = swap_sum16(k);  // rows 0+1, 2+3
+  return k;
+}
+
+// Permlane swaps of two different quantities x, y (no copies needed): the sum
+// of the swapped registers is a reduce-scatter over row pairs (swap16: rows
+// 0+1 of x land in row 0, of y in row 1, ...) or wave halves (swap32).
+__device__ __forceinline__ double swap16_rs(double x, double y) {
+  const auto a = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(x),
+                                                  (unsigned)__double2loint(y), false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(x),
+                                                  (unsigned)__double2hiint(y), false, false);
+  return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+}
+__device__ __forceinline__ double swap32_rs(double x, double y) {
+  const auto a = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(x),
+                                                  (unsigned)__double2loint(y), false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(x),
+                                                  (unsigned)__double2hiint(y), false, false);
+  return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+}
+
+// Reduce-scatter of four per-lane partial sums (q0..q3) over the LPP = 64 / PPW
+// lanes of one column pair; the lane's "owner" quantity total is returned
+// (sep_owner below says which lane owns which quantity).
+//  * PPW >= 2: lane l owns quantity l & 3.  Two DPP exchange steps hand each
+//    lane one quantity; two row rotations and, for 2-row groups, a permlane
+//    swap finish the sum.
+//  * PPW == 1: row r owns quantity r.  Two permlane16 swaps of (q0, q1) and
+//    (q2, q3) and one permlane32 swap scatter the quantities over the rows (no
+//    register copies: the swapped operands are different quantities), then a
+//    16-lane row sum.
+template <int PPW>
+__device__ __forceinline__ double reduce4(int lane, double q0, double q1, double q2, double q3) {
+  if constexpr (PPW == 1) {
+    return row_sum16(swap32_rs(swap16_rs(q0, q1), swap16_rs(q2, q3)));
+  } else {
+    const bool b0 = lane & 1, b1 = lane & 2;
+    double kg = b0 ? q1 : q0, kh = b0 ? q3 : q2;
+    kg += dppu_f64<0xB1>(b0 ? q0 : q1);  // quad_perm [1,0,3,2]: partner keeps the other column
+    kh += dppu_f64<0xB1>(b0 ? q2 : q3);
+    double k = b1 ? kh : kg;
+    k += dppu_f64<0x4E>(b1 ? kg : kh);   // quad_perm [2,3,0,1]
+    return stride4_sumu<PPW>(k);
+  }
+}
+
+// Sum over the lanes that hold one parameter's window slots: the 16 lanes of
+// its row (PPW == 1) or the residue class l & 3 of its group (PPW >= 2).
+template <int PPW>
+__device__ __forceinline__ double owner_sum(double v) {
+  if constexpr (PPW == 1) return row_sum16(v);
+  else return stride4_sumu<PPW>(v);
+}
+
+// Value held by the owner lane of quantity K, for every lane of the group.
+// 4 pairs per wave: a group is one DPP row, so row_newbcast:K (dpp_ctrl 0x150 +
+// K) does it; 2 pairs: newbcast, then permlane16_swap copies each even row into
+// the odd row above it; 1 pair: readlane of row K's first lane (wave-uniform).
 template <int PPW, int K>
 __device__ __forceinline__ double group_bcast(double v, int /*grp*/) {
   if constexpr (PPW == 1) {
-    return readlane_f64(v, K);
+    return readlane_f64(v, 16 * K);
   } else {
-    const double t = dpp_f64<0x150 + K>(v);
+    const double t = dppu_f64<0x150 + K>(v);
     if constexpr (PPW == 4) {
       return t;
     } else {
@@ -87,13 +143,23 @@ __device__ __forceinline__ double rsqrt_pos(double y) {
 }
 
 // PPW column pairs per wavefront (PPW in {1, 2, 4}); pair = wave * PPW + lane / LPP.
+// Owner lanes: quantity / parameter q (0 muA, 1 muB, 2 log sA, 3 log sB) is
+// owned by lane q of the group (PPW >= 2) or by every lane of row q (PPW == 1,
+// whose rep lane 16 q updates it); see reduce4.
 // REGRING: the adagrad window (W <= 16) lives in registers, one entry per
-// (lane, j): slot j * (LPP / 4) + gl / 4 of parameter gl & 3; otherwise in LDS.
+// (lane, j) among the SL lanes that own the parameter: slot j * SL + sub;
+// otherwise in LDS.
+// Per-step values: each lane keeps the last four steps' partial values in
+// registers and one reduce-scatter every fourth step sums all four (the
+// entropy term sum log s rides in the partial of the log-scale rep lanes).
 template <class TGT, bool TFAM, bool HOST, int PPW, bool REGRING>
 __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, int wave,
                                          const double2* sct, const double2* ltab) {
   constexpr int LPP = 64 / PPW;       // lanes per column pair
   constexpr int SL = LPP / 4;         // slot lanes per parameter
+#ifdef VB_SEP_PROF
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   const int lane = threadIdx.x & 63;
   const int grp = lane / LPP;
   const int gl = lane & (LPP - 1);    // lane within the pair's group
@@ -105,10 +171,12 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
   const bool hasB = live && dB < D;
   double* ring = ring_base + grp * 4;  // LDS ring [slot][PPW * 4]
 
-  const int own = lane & 3;            // 0 muA, 1 muB, 2 lsA, 3 lsB
+  const int own = PPW == 1 ? lane >> 4 : lane & 3;        // 0 muA, 1 muB, 2 lsA, 3 lsB
+  const int sub = PPW == 1 ? lane & 15 : gl >> 2;         // index among the owner lanes
+  const bool rep = sub == 0;                              // the owner lane that writes
   const long long own_idx = (own & 2 ? D : 0) + (own & 1 ? dB : dA);
   const bool own_ok = live && (hasB || !(own & 1));
-  const bool updater = gl < 4 && own_ok;
+  const bool updater = rep && own_ok;
   double lam_own = own_ok ? a.lam[own_idx] : 0.0;
   double s_own = exp(lam_own);
   double muA = group_bcast<PPW, 0>(lam_own, grp), muB = group_bcast<PPW, 1>(lam_own, grp);
@@ -122,40 +190,35 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
     if constexpr (REGRING) {
 #pragma unroll
       for (int j = 0; j < PPW; ++j) {
-        const int sl = j * SL + (gl >> 2);
+        const int sl = j * SL + sub;
         if (sl < W && own_ok) rg[j] = a.ring[(long long)sl * P + own_idx];
       }
     } else {
-      if (gl < 4)
+      if (rep)
         for (int k = 0; k < W; ++k)
-          ring[k * 4 * PPW + gl] = own_ok ? a.ring[(long long)k * P + own_idx] : 0.0;
+          ring[k * 4 * PPW + own] = own_ok ? a.ring[(long long)k * P + own_idx] : 0.0;
     }
     slot = (int)(a.step0 % W);
     cnt = a.step0 < W ? (int)a.step0 : W;
   }
   const Rng rng{a.k0, a.k1, a.stream};
   const double invN = 1.0 / (double)N;
+  // entropy share of this lane's value partial: log s of its rep lane
+  const bool ent = updater && own >= 2;
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;  // partials of steps s, s-1, s-2, s-3
+  // Philox Gaussian draws: the first sample row of each step is drawn one step
+  // ahead (software pipelining across the step boundary)
+  constexpr bool PIPE = !HOST && !TFAM;
+  double pA = 0.0, pB = 0.0;
+  if constexpr (PIPE)
+    normal_pair_tab(rng.draw((uint32_t)w, (uint32_t)gl, (uint32_t)a.rng_step0, 0u), pA, pB, sct, ltab);
 
   for (int s = 0; s < a.n_steps; ++s) {
     const long long i = a.step0 + s;
     const uint32_t ri = (uint32_t)(a.rng_step0 + s);
     double gA = 0.0, gB = 0.0, hA = 0.0, hB = 0.0, v = 0.0;
-#pragma unroll 1
-    for (int n = gl; n < N; n += LPP) {
-      double eA, eB;
-      if constexpr (HOST) {
-        const double* row = a.noise + ((long long)s * N + n) * D;
-        eA = live ? row[dA] : 0.0;
-        eB = hasB ? row[dB] : 0.0;
-      } else {
-        normal_pair_tab(rng.draw((uint32_t)w, (uint32_t)n, ri, 0u), eA, eB, sct, ltab);
-        if constexpr (TFAM) {
-          double GA, GB;
-          gamma_pair<true>(rng, (uint32_t)w, (uint32_t)n, ri, a.shape, GA, GB, sct, ltab);
-          eA = a.t_scale * eA / sqrt(GA);
-          eB = a.t_scale * eB / sqrt(GB);
-        }
-      }
+    // reparameterise one sample row of the pair, evaluate the target, accumulate
+    auto consume = [&](double eA, double eB) {
       double dg;
       const double xA = eA * sA + muA;
       double lpA = TGT::lp1(xA, dg);
@@ -179,24 +242,59 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
       v += hasB ? lpA + lpB : lpA;
       gB += dg;
       hB += dg * eB;
+    };
+    // draw sample row n (host noise, or Philox normals [+ gamma for t]) and consume it
+    auto sample = [&](int n) {
+      double eA, eB;
+      if constexpr (HOST) {
+        const double* row = a.noise + ((long long)s * N + n) * D;
+        eA = live ? row[dA] : 0.0;
+        eB = hasB ? row[dB] : 0.0;
+      } else {
+        normal_pair_tab(rng.draw((uint32_t)w, (uint32_t)n, ri, 0u), eA, eB, sct, ltab);
+        if constexpr (TFAM) {
+          double GA, GB;
+          gamma_pair<true>(rng, (uint32_t)w, (uint32_t)n, ri, a.shape, GA, GB, sct, ltab);
+          eA = a.t_scale * eA / sqrt(GA);
+          eB = a.t_scale * eB / sqrt(GB);
+        }
+      }
+      consume(eA, eB);
+    };
+    int n = gl;
+    if constexpr (PIPE) {
+      // sample row gl was drawn during the previous step's update
+      if (n < N) consume(pA, pB);
+      n += LPP;
     }
-    const double S = reduce_scatter4<PPW>(lane, gA, gB, hA, hB);
-    v = group_sum<PPW>(v);
+#pragma unroll 1
+    for (; n < N; n += LPP) sample(n);
+    const double S = reduce4<PPW>(lane, gA, gB, hA, hB);
     // d/dmu = -mean g ; d/dlog sigma = -(1 + sigma * mean(g * eps))
     const double m = S * invN;
     const double g_own = own < 2 ? -m : -(1.0 + s_own * m);
-    // cross-lane reads with every lane active (a readlane of a lane outside the
-    // exec mask may see a register the compiler did not keep for that lane)
-    const double lsA_b = group_bcast<PPW, 2>(lam_own, grp);
-    const double lsB_b = group_bcast<PPW, 3>(lam_own, grp);
-    const double vpart = (hasB ? lsA_b + lsB_b : lsA_b) + v * invN;
-    if (gl == 0 && live) a.vpart[(long long)s * a.n_waves + w] = vpart;
+
+    // value partial sum log s + mean log p over the pair; summed over lanes and
+    // written for four steps at a time (vpart[step][pair])
+    v3 = v2;
+    v2 = v1;
+    v1 = v0;
+    v0 = ent ? fma(v, invN, lam_own) : v * invN;
+    if ((s & 3) == 3 || s + 1 == a.n_steps) {
+      const double tot = reduce4<PPW>(lane, v3, v2, v1, v0);  // owner q: step s - 3 + q
+      const int st = s - 3 + own;
+      if (rep && live && st >= (s & ~3)) a.vpart[(long long)st * a.n_waves + w] = tot;
+    }
 
     if (a.emit_grad) {
       if (updater) a.grad[own_idx] = g_own;
       continue;
     }
 
+    // the next step's first draw does not depend on lambda: issued here, in the
+    // same basic block as the window / update / broadcast chain below, it fills
+    // that chain's latency
+    if constexpr (PIPE) normal_pair_tab(rng.draw((uint32_t)w, (uint32_t)gl, ri + 1u, 0u), pA, pB, sct, ltab);
     // window push (vb.py:365-370) and accum = sum of g^2 over the window
     // (vb.py:371-373).  Slots outside the window hold 0 or stale values that
     // the count mask removes.
@@ -206,18 +304,18 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
       double acc = 0.0;
 #pragma unroll
       for (int j = 0; j < PPW; ++j) {
-        const int sl = j * SL + (gl >> 2);
+        const int sl = j * SL + sub;
         if (sl == slot) rg[j] = g_own;
         const double t = rg[j];
         acc += (sl < W) ? t * t : 0.0;
       }
-      q = stride4_sum<PPW>(acc);
+      q = owner_sum<PPW>(acc);
     } else {
-      if (gl < 4) ring[slot * 4 * PPW + gl] = g_own;
+      if (rep) ring[slot * 4 * PPW + own] = g_own;
       int L = (cnt < W) ? 0 : (slot + 1 == W ? 0 : slot + 1);
       q = 0.0;
       for (int k = 0; k < cnt; ++k) {
-        const double t = ring[L * 4 * PPW + (gl & 3)];
+        const double t = ring[L * 4 * PPW + own];
         q += t * t;
         L = (L + 1 == W) ? 0 : L + 1;
       }
@@ -233,17 +331,24 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
     slot = (slot + 1 == W) ? 0 : slot + 1;
   }
 
+#ifdef VB_SEP_PROF
+  if (lane == 0 && a.step0 == VB_SEP_PROF) {
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    printf("SEPW %d %d %u %u %llu %llu\n", PPW, w, __builtin_amdgcn_s_getreg(63492),
+           __builtin_amdgcn_s_getreg(63508), t_start, t_end);
+  }
+#endif
   if (!a.emit_grad && own_ok) {
-    if (gl < 4) a.lam[own_idx] = lam_own;
+    if (rep) a.lam[own_idx] = lam_own;
     if constexpr (REGRING) {
 #pragma unroll
       for (int j = 0; j < PPW; ++j) {
-        const int sl = j * SL + (gl >> 2);
+        const int sl = j * SL + sub;
         if (sl < W) a.ring[(long long)sl * P + own_idx] = rg[j];
       }
     } else {
-      if (gl < 4)
-        for (int k = 0; k < W; ++k) a.ring[(long long)k * P + own_idx] = ring[k * 4 * PPW + gl];
+      if (rep)
+        for (int k = 0; k < W; ++k) a.ring[(long long)k * P + own_idx] = ring[k * 4 * PPW + own];
     }
   }
 }
