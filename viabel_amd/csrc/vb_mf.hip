@@ -506,7 +506,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   __shared__ double s_max[kBlockMaxRowWaves];
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN];
-  __shared__ double s_e[HOST ? 1 : kBlockDrawLds];
+  __shared__ double s_e[HOST ? 1 : kBlockDrawLds + DMAX];  // + slack for the row loads
   if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
 
   using Row = RowOf<TGT>;
@@ -586,11 +586,15 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
     const long long ri = a.rng_step0 + s;
     double mu[DMAX], sg[DMAX];
     double sl = 0.0;  // sum_d log sigma_d of the pre-update lam
+    // unconditional LDS loads (every index is inside the arrays) then selects:
+    // a load guarded by d < D compiles to a branch per coordinate, each waiting
+    // on its own loads (and, at DMAX = 10, on a scratch reload of the guard)
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
-      mu[d] = d < D ? s_lam[d] : 0.0;
-      sg[d] = d < D ? s_sg[d] : 0.0;
-      if (d < D) sl += s_lam[D + d];
+      const double m = s_lam[d], g = s_sg[d], l = s_lam[D + d];
+      mu[d] = d < D ? m : 0.0;
+      sg[d] = d < D ? g : 0.0;
+      sl += d < D ? l : 0.0;
     }
     double acc[K];
 #pragma unroll
@@ -656,8 +660,13 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
         for (int n = tid; n < nc; n += RT) {
           const double* rec = buf + n * R;
           double e[DMAX];
+          // unconditional loads + selects (see the step prologue); rec + d stays
+          // inside s_e (DMAX doubles of slack after the record area)
 #pragma unroll
-          for (int d = 0; d < DMAX; ++d) e[d] = d < D ? rec[d] : 0.0;
+          for (int d = 0; d < DMAX; ++d) {
+            const double t = rec[d];
+            e[d] = d < D ? t : 0.0;
+          }
           double lqs = 0.0;
           if (need_lq)
             for (int j = 0; j < NP; ++j) lqs += rec[2 * NP + j];
