@@ -179,6 +179,27 @@ __device__ __forceinline__ double log_unit_tab(double u, const double2* ltab) {
   return fma(de, 0.6931471805598903, fma(de, 5.497923018708371e-14, t.y + l1p));
 }
 
+// log(u) for u in (0, 1) (Box-Muller radius and acceptance uniforms, never 0):
+// u = m 2^e with m in [1/2, 1) and e <= 0, so e ln2, log c and log1p(r) never
+// cancel; c = 1/2 + j/256 the nearest table point, |r| <= 1/256, log1p to r^7.
+// The LDS log table holds kLogTab followed by kLogU01Tab (load_bm_tables); at
+// m ~ 1 the entry is exactly (1, 0).
+__device__ __forceinline__ double log_u01_tab(double u, const double2* ltab) {
+  int e;
+  const double m = frexp(u, &e);
+  const double2 t = ltab[kLogN + (int)rint(fma(m, 256.0, -128.0))];  // j in [0, 128]
+  const double r = fma(m, t.x, -1.0);
+  double p = 0.14285714285714285;                // 1/7
+  p = hfma(p, r, -0.16666666666666666);
+  p = hfma(p, r, 0.2);
+  p = hfma(p, r, -0.25);
+  p = hfma(p, r, 0.3333333333333333);
+  p = hfma(p, r, -0.5);
+  const double l1p = fma(r * r, p, r);
+  const double de = (double)e;
+  return fma(de, 0.6931471805598903, fma(de, 5.497923018708371e-14, t.y + l1p));
+}
+
 // sin(pi x), cos(pi x) for x in [0, 2]: x = i/128 + r, |r| <= 1/256, table
 // (sin, cos)(pi i / 128) rotated by theta = pi r with short Taylor forms.
 __device__ __forceinline__ void sincospi_tab(double x, double& sn, double& cs,
@@ -216,7 +237,7 @@ __device__ __forceinline__ void normal_pair_tab(u4 w, double& z0, double& z1, co
                                                 const double2* ltab) {
   const double u1 = unit_mantissa(w.x, w.y) - 0x1.fffffffffffffp-1;
   const double u2 = unit_mantissa(w.z, w.w) - 1.0;
-  const double r = sqrt_pos(-2.0 * log_unit_tab(u1, ltab));
+  const double r = sqrt_pos(-2.0 * log_u01_tab(u1, ltab));
   double s, c;
   sincospi_tab(2.0 * u2, s, c, sct);
   z0 = r * c;
@@ -229,6 +250,8 @@ __device__ __forceinline__ void load_bm_tables(double2* sct, double2* ltab) {
     sct[i] = double2{kSinCosPiTab[i][0], kSinCosPiTab[i][1]};
   for (int i = threadIdx.x; i < kLogN; i += blockDim.x)
     ltab[i] = double2{kLogTab[i][0], kLogTab[i][1]};
+  for (int i = threadIdx.x; i < kLogU01N; i += blockDim.x)
+    ltab[kLogN + i] = double2{kLogU01Tab[i][0], kLogU01Tab[i][1]};
 }
 
 // Two standard normals from one Philox block (Box-Muller).
@@ -263,7 +286,7 @@ __device__ __forceinline__ void gamma_pair(const Rng& rng, uint32_t pair, uint32
     const double u2 = (double)w.y * 0x1p-32;
     double s, cs, r;
     if constexpr (TAB) {
-      r = sqrt_pos(-2.0 * log_unit_tab(u1, ltab));
+      r = sqrt_pos(-2.0 * log_u01_tab(u1, ltab));
       sincospi_tab(2.0 * u2, s, cs, sct);
     } else {
       r = sqrt_pos(-2.0 * log_unit(u1));
@@ -276,7 +299,7 @@ __device__ __forceinline__ void gamma_pair(const Rng& rng, uint32_t pair, uint32
       double v = 1.0 + c * za;
       if (v > 0.0) {
         v = v * v * v;
-        const double lu = TAB ? log_unit_tab(ua, ltab) : log(ua);
+        const double lu = TAB ? log_u01_tab(ua, ltab) : log(ua);
         const double lv = (TAB && v >= 0x1p-1022 && v < 0x1p+1023) ? log_unit_tab(v, ltab) : log(v);
         if (lu < 0.5 * za * za + d - d * v + d * lv) {
           ga = d * v;
@@ -288,7 +311,7 @@ __device__ __forceinline__ void gamma_pair(const Rng& rng, uint32_t pair, uint32
       double v = 1.0 + c * zb;
       if (v > 0.0) {
         v = v * v * v;
-        const double lu = TAB ? log_unit_tab(ub, ltab) : log(ub);
+        const double lu = TAB ? log_u01_tab(ub, ltab) : log(ub);
         const double lv = (TAB && v >= 0x1p-1022 && v < 0x1p+1023) ? log_unit_tab(v, ltab) : log(v);
         if (lu < 0.5 * zb * zb + d - d * v + d * lv) {
           gb = d * v;
@@ -431,16 +454,17 @@ struct Funnel {
     const double zv = v / s0;
     double lp = -0.5 * zv * zv - log(s0) - 0.5 * kLog2Pi;
     double gv = -zv / s0;
-    const double scale = exp(v);
-    const double inv_s2 = exp(-2.0 * v);
+    const double inv_s = exp(-v);
+    const double inv_s2 = inv_s * inv_s;
+    // branch-free over the DMAX slots (the D < DMAX tail is masked by selects)
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
-      if (d < D && d != 1) {
-        const double z = x[d] / scale;
-        lp += -0.5 * z * z - v - 0.5 * kLog2Pi;
-        g[d] = -x[d] * inv_s2;
-        gv += z * z - 1.0;
-      }
+      if (d == 1) continue;
+      const double z = x[d] * inv_s;
+      const bool on = d < D;
+      lp += on ? -0.5 * z * z - v - 0.5 * kLog2Pi : 0.0;
+      g[d] = on ? -x[d] * inv_s2 : 0.0;
+      gv += on ? z * z - 1.0 : 0.0;
     }
     g[1] = gv;
     return lp;
@@ -482,8 +506,13 @@ struct SepRow {
   __device__ __forceinline__ static double row(const double* x, double* g, int D) {
     double lp = 0.0;
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d)
-      if (d < D) lp += T::lp1(x[d], g[d]);
+    for (int d = 0; d < DMAX; ++d) {
+      double gd;
+      const double l = T::lp1(x[d], gd);
+      const bool on = d < D;
+      lp += on ? l : 0.0;
+      g[d] = on ? gd : 0.0;
+    }
     return lp;
   }
 };

@@ -362,7 +362,7 @@ void sep_kernel(SepArgs a) {
   __shared__ double s_ring[REGRING ? 1 : 4][REGRING ? 1 : 64 * 4 * PPW_BIG];
   // Box-Muller tables (vb_tables.hpp) for the in-kernel Philox draws
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
-  __shared__ double2 s_lt[HOST ? 1 : kLogN];
+  __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
   if constexpr (!HOST) {
     load_bm_tables(s_sct, s_lt);
     __syncthreads();
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   __shared__ double s_red[kBlockMaxRowWaves][K];
   __shared__ double s_max[kBlockMaxRowWaves];
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
-  __shared__ double2 s_lt[HOST ? 1 : kLogN];
+  __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
   __shared__ double s_e[HOST ? 1 : kBlockDrawLds + DMAX];  // + slack for the row loads
   if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
 
