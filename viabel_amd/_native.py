@@ -162,10 +162,30 @@ def check(rc):
     raise RuntimeError(msg)
 
 
+def _torch_runtime_first():
+    """PyTorch ships its own HIP runtime (torch/lib/libamdhip64.so) beside the
+    ROCm runtime this library links.  Both work in one process only when
+    torch's opens the GPU first: after the ROCm runtime has, torch reports "No
+    HIP GPUs are available".  Device tensors are how callers hand this library
+    HBM-resident data (and the restart / log-weight paths allocate them), so
+    torch's runtime is initialised before the first context when torch is
+    installed."""
+    try:
+        import torch
+    except Exception:
+        return
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
+
+
 class Context:
     """One vb_ctx (device + HIP stream)."""
 
     def __init__(self, device=0, stream=None):
+        _torch_runtime_first()
         h = ctypes.c_void_p()
         check(lib().vb_ctx_create(int(device), stream, ctypes.byref(h)))
         self.handle = h
