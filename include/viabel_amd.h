@@ -37,6 +37,7 @@
  *   vb_covariance          viabel/bounds.py:55-56 (np.cov(samples.T), ddof = 1)
  *   vb_weighted_covariance notebooks/experiments.py:83-85 (PSIS-weighted mean / np.cov)
  *   vb_psislw              notebooks/psis.py:112-208 (psislw)
+ *   vb_psislw_colmajor     notebooks/psis.py:112-208 (psislw, Fortran-ordered input)
  *   vb_gpdfit              notebooks/psis.py:211-331 (gpdfitnew)
  *   vb_gpinv               notebooks/psis.py:334-376 (gpinv)
  *   vb_sumlogs             notebooks/psis.py:379-395 (sumlogs)
@@ -283,6 +284,13 @@ int vb_weighted_covariance(vb_ctx* ctx, const double* x, int64_t n, int64_t d,
 int vb_psislw(vb_ctx* ctx, const double* lw, int64_t n, int64_t m, double reff,
               double* lw_out, double* k_out, int64_t* tail_idx_out,
               int64_t tail_cap, int64_t* n_tail_out);
+/* vb_psislw for column-major input: lw holds m columns of n contiguous log
+ * weights (a Fortran-ordered [n, m] array, the layout psis.py:146 copies the
+ * input into); lw_out likewise.  All m columns run through the pipeline
+ * together (column-batched launches). */
+int vb_psislw_colmajor(vb_ctx* ctx, const double* lw, int64_t n, int64_t m, double reff,
+                       double* lw_out, double* k_out, int64_t* tail_idx_out,
+                       int64_t tail_cap, int64_t* n_tail_out);
 /* Zhang-Stephens GPD fit of x[n] (any order).  ks_out / w_out nullable,
  * length 30 + floor(sqrt(n)); *n_w_out = number of weights kept. */
 int vb_gpdfit(vb_ctx* ctx, const double* x, int64_t n, double* k, double* sigma,

@@ -15,10 +15,16 @@
 
 int main() {
   struct Case { int M, N, K; bool ta, tb; bool ks; };
+#ifdef SPLITK_PROBE
+  Case cases[] = {{512, 512, 512, false, false, false}, {512, 512, 256, false, false, false},
+                  {1024, 512, 256, false, false, false}, {512, 512, 128, false, false, false},
+                  {2048, 512, 128, false, false, false}, {1024, 1024, 256, false, false, false}};
+#else
   Case cases[] = {{512, 512, 512, false, false, false}, {512, 512, 512, false, true, false},
                   {512, 512, 512, true, false, false},  {128, 512, 512, false, false, false},
                   {512, 512, 128, true, false, true},   {1024, 1024, 1024, false, false, false},
                   {37, 45, 29, true, true, true}};
+#endif
   rocblas_handle h;
   rocblas_create_handle(&h);
   std::mt19937_64 rng(1);

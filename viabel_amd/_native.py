@@ -106,6 +106,9 @@ _SIGNATURES = {
                                 c_double_p, ctypes.c_int32, c_double_p, c_double_p], ctypes.c_int),
     'vb_psislw': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
                    c_double_p, c_double_p, c_int64_p, ctypes.c_int64, c_int64_p], ctypes.c_int),
+    'vb_psislw_colmajor': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,
+                            ctypes.c_double, c_double_p, c_double_p, c_int64_p, ctypes.c_int64,
+                            c_int64_p], ctypes.c_int),
     'vb_gpdfit': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, c_double_p, c_double_p,
                    c_double_p, c_double_p, c_int64_p], ctypes.c_int),
     'vb_gpinv': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_double, ctypes.c_double,

@@ -1200,38 +1200,70 @@ int vb_covariance(vb_ctx* c, const double* x, int64_t n, int64_t d, double* mean
 // ---------------------------------------------------------------------------
 extern "C" {
 
-int vb_psislw(vb_ctx* c, const double* lw, int64_t n, int64_t m, double reff, double* lw_out,
-              double* k_out, int64_t* tail_idx_out, int64_t tail_cap, int64_t* n_tail_out) {
-  VB_TRY(check_ctx(c));
-  if (!lw || !lw_out || !k_out || m < 1) return fail(VB_EINVAL, "invalid argument");
-  if (n <= 1) return fail(VB_EINVAL, "More than one log-weight needed.");  // psis.py:143-144
-  // cutoff_ind = -ceil(min(0.2 n, 3 sqrt(n / Reff))) - 1   (psis.py:157)
-  const double mt_f = std::ceil(std::fmin(0.2 * (double)n, 3.0 * std::sqrt((double)n / reff)));
-  const long long Mt = (long long)mt_f;
-  if (Mt > vbk::psis_tail_max())
-    return fail(VB_EUNSUPPORTED, "PSIS tail of %lld draws exceeds the device sort capacity %lld",
-                Mt, vbk::psis_tail_max());
-  if (tail_idx_out && tail_cap < Mt) return fail(VB_EINVAL, "tail_cap must be >= %lld", Mt);
+// cutoff_ind = -ceil(min(0.2 n, 3 sqrt(n / Reff))) - 1   (psis.py:157)
+static long long psis_tail_len(int64_t n, double reff) {
+  return (long long)std::ceil(std::fmin(0.2 * (double)n, 3.0 * std::sqrt((double)n / reff)));
+}
+
+// m columns, element (i, col) at [col * cs + i * rs] of lw and lw_out; the
+// columns run through the PSIS pipeline together (column-batched launches),
+// in groups whose scratch stays within kPsisScratchBudget
+static int psislw_impl(vb_ctx* c, const double* lw, int64_t n, int64_t m, long long rs,
+                       long long cs, long long Mt, double* lw_out, double* k_out,
+                       int64_t* tail_idx_out, int64_t tail_cap, int64_t* n_tail_out) {
+  constexpr size_t kPsisScratchBudget = size_t(256) << 20;
   In dlw;
   VB_TRY(dlw.stage(c, 0, lw, (size_t)n * m));
   Out dout, dk;
   VB_TRY(dout.stage(c, 1, lw_out, (size_t)n * m));
   VB_TRY(dk.stage(c, 2, k_out, (size_t)m));
-  VB_TRY(c->slot[3].reserve(vbk::psis_scratch_bytes(Mt)));
+  const size_t sb = vbk::psis_col_stride(Mt < 1 ? 1 : Mt);
+  const int64_t group = std::max<int64_t>(1, std::min<int64_t>(m, (int64_t)(kPsisScratchBudget / sb)));
+  VB_TRY(c->slot[3].reserve(sb * (size_t)group));
   OutT<long long> dti, dnt;
   VB_TRY(dti.stage(c, 4, reinterpret_cast<long long*>(tail_idx_out),
                    tail_idx_out ? (size_t)tail_cap * m : 0));
   VB_TRY(dnt.stage(c, 5, reinterpret_cast<long long*>(n_tail_out), n_tail_out ? (size_t)m : 0));
-  for (int64_t col = 0; col < m; ++col) {
-    VB_HIP(vbk::psis_column(dlw.d + col, dout.d + col, n, m, Mt, c->slot[3].p, dk.d + col,
-                            dti.d ? dti.d + (size_t)col * tail_cap : nullptr,
-                            dnt.d ? dnt.d + col : nullptr, c->stream));
+  for (int64_t c0 = 0; c0 < m; c0 += group) {
+    const int g = (int)std::min<int64_t>(group, m - c0);
+    VB_HIP(vbk::psis_columns(dlw.d + c0 * cs, dout.d + c0 * cs, n, g, rs, cs, Mt, c->slot[3].p,
+                             dk.d + c0, dti.d ? dti.d + (size_t)c0 * tail_cap : nullptr,
+                             (long long)tail_cap, dnt.d ? dnt.d + c0 : nullptr, c->stream));
   }
   VB_TRY(dout.finish(c));
   VB_TRY(dk.finish(c));
   VB_TRY(dti.finish(c));
   VB_TRY(dnt.finish(c));
   return sync(c);
+}
+
+int vb_psislw(vb_ctx* c, const double* lw, int64_t n, int64_t m, double reff, double* lw_out,
+              double* k_out, int64_t* tail_idx_out, int64_t tail_cap, int64_t* n_tail_out) {
+  VB_TRY(check_ctx(c));
+  if (!lw || !lw_out || !k_out || m < 1) return fail(VB_EINVAL, "invalid argument");
+  if (n <= 1) return fail(VB_EINVAL, "More than one log-weight needed.");  // psis.py:143-144
+  const long long Mt = psis_tail_len(n, reff);
+  if (Mt > vbk::psis_tail_max())
+    return fail(VB_EUNSUPPORTED, "PSIS tail of %lld draws exceeds the device sort capacity %lld",
+                Mt, vbk::psis_tail_max());
+  if (tail_idx_out && tail_cap < Mt) return fail(VB_EINVAL, "tail_cap must be >= %lld", Mt);
+  return psislw_impl(c, lw, n, m, /*rs=*/m, /*cs=*/1, Mt, lw_out, k_out, tail_idx_out, tail_cap,
+                     n_tail_out);
+}
+
+int vb_psislw_colmajor(vb_ctx* c, const double* lw, int64_t n, int64_t m, double reff,
+                       double* lw_out, double* k_out, int64_t* tail_idx_out, int64_t tail_cap,
+                       int64_t* n_tail_out) {
+  VB_TRY(check_ctx(c));
+  if (!lw || !lw_out || !k_out || m < 1) return fail(VB_EINVAL, "invalid argument");
+  if (n <= 1) return fail(VB_EINVAL, "More than one log-weight needed.");  // psis.py:143-144
+  const long long Mt = psis_tail_len(n, reff);
+  if (Mt > vbk::psis_tail_max())
+    return fail(VB_EUNSUPPORTED, "PSIS tail of %lld draws exceeds the device sort capacity %lld",
+                Mt, vbk::psis_tail_max());
+  if (tail_idx_out && tail_cap < Mt) return fail(VB_EINVAL, "tail_cap must be >= %lld", Mt);
+  return psislw_impl(c, lw, n, m, /*rs=*/1, /*cs=*/n, Mt, lw_out, k_out, tail_idx_out, tail_cap,
+                     n_tail_out);
 }
 
 int vb_gpdfit(vb_ctx* c, const double* x, int64_t n, double* k, double* sigma, double* ks_out,

@@ -79,50 +79,78 @@ __device__ __forceinline__ double bmax(double v, double* red) {
   return r;
 }
 
+// Column batching: every per-column kernel takes its column from blockIdx.y.
+// Element (i, c) of the input / output is x[c * cs + i * rs]; column c's
+// scratch (PsisState, partials, tail buffers, ...) sits sb bytes after column
+// c - 1's, so one launch sequence serves all m columns of a psislw call.
+template <class T>
+__device__ __forceinline__ T* colp(T* p, long long sb) {
+  return reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(p) + (long long)blockIdx.y * sb);
+}
+template <class T>
+__device__ __forceinline__ const T* colp(const T* p, long long sb) {
+  return reinterpret_cast<const T*>(reinterpret_cast<const unsigned char*>(p) +
+                                    (long long)blockIdx.y * sb);
+}
+
 // ---- 1. column max -----------------------------------------------------------
-__global__ __launch_bounds__(256) void col_max_kernel(const double* x, long long n, long long st,
-                                                      double* part) {
+__global__ __launch_bounds__(256) void col_max_kernel(const double* x, long long n, long long rs,
+                                                      long long cs, double* part, long long sb) {
   __shared__ double red[16];
+  x += (long long)blockIdx.y * cs;
   double m = -INFINITY;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256)
-    m = fmax(m, x[i * st]);
+    m = fmax(m, x[i * rs]);
   m = bmax(m, red);
-  if (threadIdx.x == 0) part[blockIdx.x] = m;
+  if (threadIdx.x == 0) colp(part, sb)[blockIdx.x] = m;
 }
 
-__global__ __launch_bounds__(256) void max_final_kernel(const double* part, int nb, double* out) {
+__global__ __launch_bounds__(256) void max_final_kernel(const double* part, int nb, double* out,
+                                                        long long sb) {
   __shared__ double red[16];
+  part = colp(part, sb);
   double m = -INFINITY;
   for (int b = threadIdx.x; b < nb; b += 256) m = fmax(m, part[b]);
   m = bmax(m, red);
-  if (threadIdx.x == 0) *out = m;
+  if (threadIdx.x == 0) *colp(out, sb) = m;
 }
 
 // ---- 2. radix select ---------------------------------------------------------
 __global__ __launch_bounds__(256) void radix_hist_kernel(const double* x, long long n,
-                                                         long long st, const PsisState* ps,
-                                                         int shift, unsigned* ghist) {
+                                                         long long rs, long long cs,
+                                                         const PsisState* ps, int shift,
+                                                         unsigned* ghist, long long sb) {
   __shared__ unsigned h[256];
   h[threadIdx.x] = 0;
   __syncthreads();
+  x += (long long)blockIdx.y * cs;
+  ps = colp(ps, sb);
   const unsigned long long prefix = ps->prefix, mask = ps->mask;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256) {
-    const unsigned long long k = dkey(x[i * st]);
+    const unsigned long long k = dkey(x[i * rs]);
     if ((k & mask) == prefix) atomicAdd(&h[(k >> shift) & 255u], 1u);
   }
   __syncthreads();
-  if (h[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], h[threadIdx.x]);
+  if (h[threadIdx.x]) atomicAdd(&colp(ghist, sb)[threadIdx.x], h[threadIdx.x]);
 }
 
-__global__ void radix_pick_kernel(const unsigned* ghist, int shift, PsisState* ps) {
+// picks the digit, then clears the histogram for the next pass
+__global__ __launch_bounds__(256) void radix_pick_kernel(unsigned* ghist, int shift, PsisState* ps,
+                                                         long long sb) {
+  __shared__ unsigned h[256];
+  ghist = colp(ghist, sb);
+  ps = colp(ps, sb);
+  h[threadIdx.x] = ghist[threadIdx.x];
+  ghist[threadIdx.x] = 0;
+  __syncthreads();
   if (threadIdx.x != 0) return;
   long long r = ps->rank, cum = 0;
   int b = 0;
   for (; b < 255; ++b) {
-    if (cum + (long long)ghist[b] > r) break;
-    cum += ghist[b];
+    if (cum + (long long)h[b] > r) break;
+    cum += h[b];
   }
   ps->prefix |= ((unsigned long long)b) << shift;
   ps->mask |= 255ull << shift;
@@ -131,15 +159,19 @@ __global__ void radix_pick_kernel(const unsigned* ghist, int shift, PsisState* p
 
 // cutoff = max(x_sel - max, log(tiny))  (psis.py:169-173); Python's max keeps
 // the first argument unless the second is strictly greater.
-__global__ void cutoff_kernel(PsisState* ps, double cutoffmin) {
+__global__ void cutoff_kernel(PsisState* ps, double cutoffmin, long long sb) {
   if (threadIdx.x != 0) return;
+  ps = colp(ps, sb);
   const double xs = dval(ps->prefix) - ps->mx;
   ps->xcut = (cutoffmin > xs) ? cutoffmin : xs;
   ps->expcut = exp(ps->xcut);
 }
 
-__global__ void radix_init_kernel(PsisState* ps, long long rank) {
+__global__ __launch_bounds__(256) void radix_init_kernel(PsisState* ps, unsigned* ghist,
+                                                         long long rank, long long sb) {
+  colp(ghist, sb)[threadIdx.x] = 0;
   if (threadIdx.x != 0) return;
+  ps = colp(ps, sb);
   ps->prefix = 0;
   ps->mask = 0;
   ps->rank = rank;
@@ -150,55 +182,65 @@ __global__ void radix_init_kernel(PsisState* ps, long long rank) {
 
 // ---- 3. shift + stable compaction ------------------------------------------
 __global__ __launch_bounds__(256) void shift_kernel(const double* lw, double* out, long long n,
-                                                    long long st, const PsisState* ps) {
-  const double mx = ps->mx;
+                                                    long long rs, long long cs,
+                                                    const PsisState* ps, long long sb) {
+  const double mx = colp(ps, sb)->mx;
+  lw += (long long)blockIdx.y * cs;
+  out += (long long)blockIdx.y * cs;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256)
-    out[i * st] = lw[i * st] - mx;
+    out[i * rs] = lw[i * rs] - mx;
 }
 
 __global__ __launch_bounds__(256) void tail_count_kernel(const double* x, long long n,
-                                                         long long st, long long chunk,
-                                                         const PsisState* ps, unsigned* cnt) {
+                                                         long long rs, long long cs,
+                                                         long long chunk, const PsisState* ps,
+                                                         unsigned* cnt, long long sb) {
   __shared__ unsigned wc[4];
-  const double xc = ps->xcut;
+  const double xc = colp(ps, sb)->xcut;
+  x += (long long)blockIdx.y * cs;
   const long long r0 = (long long)blockIdx.x * chunk, r1 = min(n, r0 + chunk);
   unsigned c = 0;
-  for (long long i = r0 + threadIdx.x; i < r1; i += 256) c += (x[i * st] > xc) ? 1u : 0u;
+  for (long long i = r0 + threadIdx.x; i < r1; i += 256) c += (x[i * rs] > xc) ? 1u : 0u;
   // wave + block sum of integers
   for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
   if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
   __syncthreads();
-  if (threadIdx.x == 0) cnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+  if (threadIdx.x == 0) colp(cnt, sb)[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
 }
 
-__global__ void tail_scan_kernel(unsigned* cnt, int nb, PsisState* ps) {
+__global__ void tail_scan_kernel(unsigned* cnt, int nb, PsisState* ps, long long sb) {
   if (threadIdx.x != 0) return;
+  cnt = colp(cnt, sb);
   unsigned long long acc = 0;
   for (int b = 0; b < nb; ++b) {
     const unsigned c = cnt[b];
     cnt[b] = (unsigned)acc;
     acc += c;
   }
-  ps->n2 = (long long)acc;
+  colp(ps, sb)->n2 = (long long)acc;
 }
 
 __global__ __launch_bounds__(256) void tail_compact_kernel(const double* x, long long n,
-                                                           long long st, long long chunk,
-                                                           const PsisState* ps,
+                                                           long long rs, long long cs,
+                                                           long long chunk, const PsisState* ps,
                                                            const unsigned* off, long long cap,
-                                                           double* tv, long long* ti) {
+                                                           double* tv, long long* ti,
+                                                           long long sb) {
   __shared__ unsigned wtot[4];
-  const double xc = ps->xcut;
+  const double xc = colp(ps, sb)->xcut;
+  x += (long long)blockIdx.y * cs;
+  tv = colp(tv, sb);
+  ti = colp(ti, sb);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const long long r0 = (long long)blockIdx.x * chunk, r1 = min(n, r0 + chunk);
-  unsigned base = off[blockIdx.x];
+  unsigned base = colp(off, sb)[blockIdx.x];
   for (long long i0 = r0; i0 < r1; i0 += 256) {
     const long long i = i0 + threadIdx.x;
     double v = 0.0;
     bool f = false;
     if (i < r1) {
-      v = x[i * st];
+      v = x[i * rs];
       f = v > xc;
     }
     const unsigned long long bal = __ballot(f);
@@ -220,17 +262,22 @@ __global__ __launch_bounds__(256) void tail_compact_kernel(const double* x, long
   }
 }
 
-// ---- 4. bitonic sort of the tail in LDS (one workgroup) -------------------------
+// ---- 4. bitonic sort of the tail in LDS (one workgroup per column) ------------
 // Sorts (key(value), position) ascending; writes the sorted values and the
 // original column indices tailinds[x2si].
 __global__ __launch_bounds__(1024) void tail_sort_kernel(const double* tv, const long long* ti,
                                                          const PsisState* ps, double* sv,
-                                                         long long* si, long long cap) {
+                                                         long long* si, long long cap,
+                                                         long long sb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long* key = reinterpret_cast<unsigned long long*>(smem);
   unsigned* pos = reinterpret_cast<unsigned*>(smem + sizeof(unsigned long long) * kTailMax);
+  tv = colp(tv, sb);
+  ti = colp(ti, sb);
+  sv = colp(sv, sb);
+  si = colp(si, sb);
   if (cap > kTailMax) cap = kTailMax;
-  long long n2 = ps->n2;
+  long long n2 = colp(ps, sb)->n2;
   if (n2 > cap) n2 = cap;
   int np2 = 1;
   while (np2 < n2) np2 <<= 1;
@@ -268,7 +315,10 @@ __global__ __launch_bounds__(1024) void tail_sort_kernel(const double* tv, const
 // ---- 5. GPD fit (gpdfitnew, psis.py:266-331) on y = exp(sorted tail) - exp(cut)
 // y[] sorted ascending, length n2 (device), or a caller array of length n.
 __global__ __launch_bounds__(256) void gpd_prep_kernel(const double* sv, const PsisState* ps,
-                                                       double* y, long long cap) {
+                                                       double* y, long long cap, long long sb) {
+  ps = colp(ps, sb);
+  sv = colp(sv, sb);
+  y = colp(y, sb);
   long long n2 = ps->n2;
   if (n2 > cap) n2 = cap;
   const double ec = ps->expcut;
@@ -280,8 +330,12 @@ __global__ __launch_bounds__(256) void gpd_prep_kernel(const double* sv, const P
 // one block per quadrature point j: bs[j], ks[j] = mean log1p(-b_j y)
 __global__ __launch_bounds__(256) void gpd_grid_kernel(const double* y, const PsisState* ps,
                                                        long long n_fixed, double* bs,
-                                                       double* ks) {
+                                                       double* ks, long long sb) {
   __shared__ double red[16];
+  y = colp(y, sb);
+  ps = colp(ps, sb);
+  bs = colp(bs, sb);
+  ks = colp(ks, sb);
   const long long n = n_fixed > 0 ? n_fixed : ps->n2;
   if (n_fixed == 0 && n <= 4) return;  // psislw: no fit, k = inf
   const long long m = 30 + (long long)sqrt((double)n);
@@ -306,9 +360,15 @@ __global__ __launch_bounds__(256) void gpd_grid_kernel(const double* y, const Ps
 __global__ __launch_bounds__(256) void gpd_final_kernel(const double* y, PsisState* ps,
                                                         long long n_fixed, const double* bs,
                                                         const double* ks, double* Lw,
-                                                        double* ks_out, double* w_out) {
+                                                        double* ks_out, double* w_out,
+                                                        long long sb) {
   __shared__ double red[16];
-  __shared__ double sb;
+  __shared__ double sb_hat;
+  y = colp(y, sb);
+  ps = colp(ps, sb);
+  bs = colp(bs, sb);
+  ks = colp(ks, sb);
+  Lw = colp(Lw, sb);
   const long long n = n_fixed > 0 ? n_fixed : ps->n2;
   if (n_fixed == 0 && n <= 4) return;
   const int m = (int)(30 + (long long)sqrt((double)n));
@@ -344,10 +404,10 @@ __global__ __launch_bounds__(256) void gpd_final_kernel(const double* y, PsisSta
       }
     ps->nkeep = keep;
     ps->m = m;
-    sb = b;
+    sb_hat = b;
   }
   __syncthreads();
-  const double b = sb;
+  const double b = sb_hat;
   const double nb = -b;
   double s = 0.0;
   for (long long i = threadIdx.x; i < n; i += 256) s += log1p(nb * y[i]);
@@ -367,7 +427,8 @@ __global__ __launch_bounds__(256) void gpd_final_kernel(const double* y, PsisSta
 }
 
 // psislw: too few tail samples -> k = inf (psis.py:177-179)
-__global__ void k_inf_kernel(PsisState* ps) {
+__global__ void k_inf_kernel(PsisState* ps, long long sb) {
+  ps = colp(ps, sb);
   if (threadIdx.x == 0 && ps->n2 <= 4) {
     ps->k = INFINITY;
     ps->sigma = NAN;
@@ -389,8 +450,12 @@ __device__ __forceinline__ double gpinv_open(double p, double k, double sigma) {
 }
 
 // ---- 6. smoothing (psis.py:187-198) ------------------------------------------
-__global__ __launch_bounds__(256) void smooth_kernel(double* x, long long st, const PsisState* ps,
-                                                     const long long* si, long long cap) {
+__global__ __launch_bounds__(256) void smooth_kernel(double* x, long long rs, long long cs,
+                                                     const PsisState* ps, const long long* si,
+                                                     long long cap, long long sb) {
+  ps = colp(ps, sb);
+  si = colp(si, sb);
+  x += (long long)blockIdx.y * cs;
   const double k = ps->k;
   long long n2 = ps->n2;
   if (n2 > cap) n2 = cap;
@@ -403,38 +468,61 @@ __global__ __launch_bounds__(256) void smooth_kernel(double* x, long long st, co
     q += ec;
     q = log(q);
     if (q > 0) q = 0.0;
-    x[si[i] * st] = q;
+    x[si[i] * rs] = q;
   }
 }
 
 // ---- 7. sumlogs + renormalise -------------------------------------------------
-__global__ __launch_bounds__(256) void sumexp_kernel(const double* x, long long n, long long st,
-                                                     const double* mx, double* part) {
+__global__ __launch_bounds__(256) void sumexp_kernel(const double* x, long long n, long long rs,
+                                                     long long cs, const double* mx,
+                                                     double* part, long long sb) {
   __shared__ double red[16];
-  const double m = *mx;
+  x += (long long)blockIdx.y * cs;
+  const double m = *colp(mx, sb);
   double s = 0.0;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256)
-    s += exp(x[i * st] - m);
+    s += exp(x[i * rs] - m);
   s = bsum(s, red);
-  if (threadIdx.x == 0) part[blockIdx.x] = s;
+  if (threadIdx.x == 0) colp(part, sb)[blockIdx.x] = s;
 }
 
 __global__ __launch_bounds__(256) void lse_final_kernel(const double* part, int nb,
-                                                        const double* mx, double* out) {
+                                                        const double* mx, double* out,
+                                                        long long sb) {
   __shared__ double red[16];
+  part = colp(part, sb);
   double s = 0.0;
   for (int b = threadIdx.x; b < nb; b += 256) s += part[b];
   s = bsum(s, red);
-  if (threadIdx.x == 0) *out = log(s) + *mx;
+  if (threadIdx.x == 0) *colp(out, sb) = log(s) + *colp(mx, sb);
 }
 
-__global__ __launch_bounds__(256) void sub_kernel(double* x, long long n, long long st,
-                                                  const double* v) {
-  const double s = *v;
+__global__ __launch_bounds__(256) void sub_kernel(double* x, long long n, long long rs,
+                                                  long long cs, const double* v, long long sb) {
+  const double s = *colp(v, sb);
+  x += (long long)blockIdx.y * cs;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256)
-    x[i * st] -= s;
+    x[i * rs] -= s;
+}
+
+// per-column results out of the scratch: k[c], n_tail[c], tail indices row c
+__global__ __launch_bounds__(256) void psis_out_kernel(const PsisState* ps, const long long* si,
+                                                       long long Mt, double* k_out,
+                                                       long long* n_tail_out, long long* tail_out,
+                                                       long long tail_cap, long long sb) {
+  const int c = blockIdx.y;
+  ps = colp(ps, sb);
+  si = colp(si, sb);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    k_out[c] = ps->k;
+    if (n_tail_out) n_tail_out[c] = ps->n2;
+  }
+  if (tail_out)
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < Mt;
+         i += (long long)gridDim.x * 256)
+      tail_out[(long long)c * tail_cap + i] = si[i];
 }
 
 __global__ __launch_bounds__(256) void gpinv_kernel(const double* p, long long n, double k,
@@ -546,86 +634,100 @@ static PsisScratch carve(void* base, long long tail_cap) {
 long long psis_tail_max() { return 1LL << 30; }
 
 namespace {
-__global__ __launch_bounds__(256) void fill_inf_kernel(double* v, long long n) {
+__global__ __launch_bounds__(256) void fill_inf_kernel(double* v, long long n, long long sb) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) v[i] = INFINITY;
+  if (i < n) colp(v, sb)[i] = INFINITY;
+}
+
+template <class T>
+T* offset_bytes(T* p, long long b) {
+  return reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(p) + b);
 }
 
 // tail values tv / indices ti (n2 <= cap valid entries, the rest +inf when cap >
-// kTailMax) -> ascending sv / si, stable on position
-hipError_t sort_tail(const PsisScratch& S, long long cap, hipStream_t s) {
+// kTailMax) -> ascending sv / si, stable on position; m columns sb bytes apart
+hipError_t sort_tail(const PsisScratch& S, long long cap, int m, long long sb, hipStream_t s) {
   if (cap <= kTailMax) {
     const size_t lds = (sizeof(unsigned long long) + sizeof(unsigned)) * kTailMax;
-    hipLaunchKernelGGL(tail_sort_kernel, dim3(1), dim3(1024), lds, s, S.tv, S.ti, S.ps, S.sv, S.si,
-                       cap);
+    hipLaunchKernelGGL(tail_sort_kernel, dim3(1, m), dim3(1024), lds, s, S.tv, S.ti, S.ps, S.sv,
+                       S.si, cap, sb);
     return hipGetLastError();
   }
-  size_t bytes = S.sort_bytes;
-  return hipcub::DeviceRadixSort::SortPairs(S.sort_tmp, bytes, S.tv, S.sv, S.ti, S.si, (int)cap, 0,
-                                            64, s);
+  for (int c = 0; c < m; ++c) {
+    const long long o = (long long)c * sb;
+    size_t bytes = S.sort_bytes;
+    const hipError_t e = hipcub::DeviceRadixSort::SortPairs(
+        offset_bytes(S.sort_tmp, o), bytes, offset_bytes(S.tv, o), offset_bytes(S.sv, o),
+        offset_bytes(S.ti, o), offset_bytes(S.si, o), (int)cap, 0, 64, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 }  // namespace
 
-// One column of psislw.  lw/out are device pointers with stride st.
-hipError_t psis_column(const double* lw, double* out, long long n, long long st, long long Mt,
-                       void* scratch, double* k_dev, long long* tail_idx_dev,
-                       long long* n_tail_dev, hipStream_t s) {
+size_t psis_col_stride(long long tail_cap) {
+  return (psis_scratch_bytes(tail_cap) + 255) / 256 * 256;
+}
+
+// psislw of m columns at once: element (i, c) of lw / out at [c * cs + i * rs]
+// (device pointers); column c's scratch at scratch + c * psis_col_stride(Mt).
+// Results: k_dev[c], n_tail_dev[c], tail_idx_dev[c * tail_cap + i] (optional).
+hipError_t psis_columns(const double* lw, double* out, long long n, int m, long long rs,
+                        long long cs, long long Mt, void* scratch, double* k_dev,
+                        long long* tail_idx_dev, long long tail_cap, long long* n_tail_dev,
+                        hipStream_t s) {
   const long long cap = Mt < 1 ? 1 : Mt;   // the tail holds at most M_t draws
+  const long long sb = (long long)psis_col_stride(cap);
   PsisScratch S = carve(scratch, cap);
   const int g = psis_grid(n);
   // 1. max
-  hipLaunchKernelGGL(col_max_kernel, dim3(g), dim3(256), 0, s, lw, n, st, S.part);
-  hipLaunchKernelGGL(max_final_kernel, dim3(1), dim3(256), 0, s, S.part, g, &S.ps->mx);
-  // 2. radix select of ascending rank n - Mt - 1
-  hipLaunchKernelGGL(radix_init_kernel, dim3(1), dim3(64), 0, s, S.ps, n - Mt - 1);
-  hipError_t e;
+  hipLaunchKernelGGL(col_max_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.part, sb);
+  hipLaunchKernelGGL(max_final_kernel, dim3(1, m), dim3(256), 0, s, S.part, g, &S.ps->mx, sb);
+  // 2. radix select of ascending rank n - Mt - 1 (the pick clears the histogram)
+  hipLaunchKernelGGL(radix_init_kernel, dim3(1, m), dim3(256), 0, s, S.ps, S.hist, n - Mt - 1, sb);
   for (int pass = 0; pass < 8; ++pass) {
     const int shift = 56 - 8 * pass;
-    e = hipMemsetAsync(S.hist, 0, sizeof(unsigned) * 256, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(radix_hist_kernel, dim3(g), dim3(256), 0, s, lw, n, st, S.ps, shift, S.hist);
-    hipLaunchKernelGGL(radix_pick_kernel, dim3(1), dim3(64), 0, s, S.hist, shift, S.ps);
+    hipLaunchKernelGGL(radix_hist_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.ps, shift,
+                       S.hist, sb);
+    hipLaunchKernelGGL(radix_pick_kernel, dim3(1, m), dim3(256), 0, s, S.hist, shift, S.ps, sb);
   }
-  hipLaunchKernelGGL(cutoff_kernel, dim3(1), dim3(64), 0, s, S.ps, log(DBL_MIN));
+  hipLaunchKernelGGL(cutoff_kernel, dim3(1, m), dim3(64), 0, s, S.ps, log(DBL_MIN), sb);
   // 3. shifted copy + stable tail compaction
   const long long chunk = ((n + g - 1) / g + 255) / 256 * 256;
   const int gc = (int)((n + chunk - 1) / chunk);
-  hipLaunchKernelGGL(shift_kernel, dim3(g), dim3(256), 0, s, lw, out, n, st, S.ps);
-  hipLaunchKernelGGL(tail_count_kernel, dim3(gc), dim3(256), 0, s, out, n, st, chunk, S.ps, S.cnt);
-  hipLaunchKernelGGL(tail_scan_kernel, dim3(1), dim3(64), 0, s, S.cnt, gc, S.ps);
+  hipLaunchKernelGGL(shift_kernel, dim3(g, m), dim3(256), 0, s, lw, out, n, rs, cs, S.ps, sb);
+  hipLaunchKernelGGL(tail_count_kernel, dim3(gc, m), dim3(256), 0, s, out, n, rs, cs, chunk, S.ps,
+                     S.cnt, sb);
+  hipLaunchKernelGGL(tail_scan_kernel, dim3(1, m), dim3(64), 0, s, S.cnt, gc, S.ps, sb);
   if (cap > kTailMax)
-    hipLaunchKernelGGL(fill_inf_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, S.tv,
-                       cap);
-  hipLaunchKernelGGL(tail_compact_kernel, dim3(gc), dim3(256), 0, s, out, n, st, chunk, S.ps, S.cnt,
-                     cap, S.tv, S.ti);
-  // 4. sort the tail
-  e = sort_tail(S, cap, s);
+    hipLaunchKernelGGL(fill_inf_kernel, dim3((unsigned)((cap + 255) / 256), m), dim3(256), 0, s,
+                       S.tv, cap, sb);
+  hipLaunchKernelGGL(tail_compact_kernel, dim3(gc, m), dim3(256), 0, s, out, n, rs, cs, chunk,
+                     S.ps, S.cnt, cap, S.tv, S.ti, sb);
+  // 4. sort the tails
+  hipError_t e = sort_tail(S, cap, m, sb, s);
   if (e != hipSuccess) return e;
   // 5. GPD fit (skipped on device when n2 <= 4)
-  hipLaunchKernelGGL(gpd_prep_kernel, dim3(32), dim3(256), 0, s, S.sv, S.ps, S.y, cap);
+  hipLaunchKernelGGL(gpd_prep_kernel, dim3(32, m), dim3(256), 0, s, S.sv, S.ps, S.y, cap, sb);
   const int mmax = 30 + (int)std::sqrt((double)Mt) + 1;
-  hipLaunchKernelGGL(gpd_grid_kernel, dim3(mmax), dim3(256), 0, s, S.y, S.ps, 0LL, S.bs, S.ks);
-  hipLaunchKernelGGL(gpd_final_kernel, dim3(1), dim3(256), 0, s, S.y, S.ps, 0LL, S.bs, S.ks, S.Lw,
-                     nullptr, nullptr);
-  hipLaunchKernelGGL(k_inf_kernel, dim3(1), dim3(64), 0, s, S.ps);
+  hipLaunchKernelGGL(gpd_grid_kernel, dim3(mmax, m), dim3(256), 0, s, S.y, S.ps, 0LL, S.bs, S.ks,
+                     sb);
+  hipLaunchKernelGGL(gpd_final_kernel, dim3(1, m), dim3(256), 0, s, S.y, S.ps, 0LL, S.bs, S.ks,
+                     S.Lw, nullptr, nullptr, sb);
+  hipLaunchKernelGGL(k_inf_kernel, dim3(1, m), dim3(64), 0, s, S.ps, sb);
   // 6. smoothing
-  hipLaunchKernelGGL(smooth_kernel, dim3(32), dim3(256), 0, s, out, st, S.ps, S.si, cap);
+  hipLaunchKernelGGL(smooth_kernel, dim3(32, m), dim3(256), 0, s, out, rs, cs, S.ps, S.si, cap, sb);
   // 7. renormalise: x -= sumlogs(x)
-  hipLaunchKernelGGL(col_max_kernel, dim3(g), dim3(256), 0, s, out, n, st, S.part);
-  hipLaunchKernelGGL(max_final_kernel, dim3(1), dim3(256), 0, s, S.part, g, &S.ps->b);
-  hipLaunchKernelGGL(sumexp_kernel, dim3(g), dim3(256), 0, s, out, n, st, &S.ps->b, S.part);
-  hipLaunchKernelGGL(lse_final_kernel, dim3(1), dim3(256), 0, s, S.part, g, &S.ps->b, &S.ps->lse);
-  hipLaunchKernelGGL(sub_kernel, dim3(g), dim3(256), 0, s, out, n, st, &S.ps->lse);
-  e = hipMemcpyAsync(k_dev, &S.ps->k, sizeof(double), hipMemcpyDeviceToDevice, s);
-  if (e != hipSuccess) return e;
-  if (n_tail_dev) {
-    e = hipMemcpyAsync(n_tail_dev, &S.ps->n2, sizeof(long long), hipMemcpyDeviceToDevice, s);
-    if (e != hipSuccess) return e;
-  }
-  if (tail_idx_dev) {
-    e = hipMemcpyAsync(tail_idx_dev, S.si, sizeof(long long) * Mt, hipMemcpyDeviceToDevice, s);
-    if (e != hipSuccess) return e;
-  }
+  hipLaunchKernelGGL(col_max_kernel, dim3(g, m), dim3(256), 0, s, out, n, rs, cs, S.part, sb);
+  hipLaunchKernelGGL(max_final_kernel, dim3(1, m), dim3(256), 0, s, S.part, g, &S.ps->b, sb);
+  hipLaunchKernelGGL(sumexp_kernel, dim3(g, m), dim3(256), 0, s, out, n, rs, cs, &S.ps->b, S.part,
+                     sb);
+  hipLaunchKernelGGL(lse_final_kernel, dim3(1, m), dim3(256), 0, s, S.part, g, &S.ps->b,
+                     &S.ps->lse, sb);
+  hipLaunchKernelGGL(sub_kernel, dim3(g, m), dim3(256), 0, s, out, n, rs, cs, &S.ps->lse, sb);
+  const unsigned go = (unsigned)std::max<long long>(1, std::min<long long>(32, (Mt + 255) / 256));
+  hipLaunchKernelGGL(psis_out_kernel, dim3(go, m), dim3(256), 0, s, S.ps, S.si, Mt, k_dev,
+                     n_tail_dev, tail_idx_dev, tail_cap, sb);
   return hipGetLastError();
 }
 
@@ -635,12 +737,12 @@ hipError_t psis_gpdfit(const double* x, long long n, void* scratch, double* out4
   PsisScratch S = carve(scratch, n);
   hipLaunchKernelGGL(iota_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n,
                      S.tv, S.ti, S.ps);
-  hipError_t e0 = sort_tail(S, n, s);
+  hipError_t e0 = sort_tail(S, n, 1, 0, s);
   if (e0 != hipSuccess) return e0;
   const int m = 30 + (int)std::sqrt((double)n);
-  hipLaunchKernelGGL(gpd_grid_kernel, dim3(m), dim3(256), 0, s, S.sv, S.ps, n, S.bs, S.ks);
+  hipLaunchKernelGGL(gpd_grid_kernel, dim3(m), dim3(256), 0, s, S.sv, S.ps, n, S.bs, S.ks, 0LL);
   hipLaunchKernelGGL(gpd_final_kernel, dim3(1), dim3(256), 0, s, S.sv, S.ps, n, S.bs, S.ks, S.Lw,
-                     ks_out, w_out);
+                     ks_out, w_out, 0LL);
   hipError_t e = hipMemcpyAsync(out4, &S.ps->k, sizeof(double) * 2, hipMemcpyDeviceToDevice, s);
   if (e != hipSuccess) return e;
   e = hipMemcpyAsync(out4 + 2, &S.ps->m, sizeof(long long) * 2, hipMemcpyDeviceToDevice, s);
@@ -659,10 +761,11 @@ hipError_t psis_gpinv(const double* p, long long n, double k, double sigma, doub
 hipError_t psis_sumlogs(const double* x, long long n, void* scratch, double* out, hipStream_t s) {
   PsisScratch S = carve(scratch, 0);
   const int g = psis_grid(n);
-  hipLaunchKernelGGL(col_max_kernel, dim3(g), dim3(256), 0, s, x, n, 1LL, S.part);
-  hipLaunchKernelGGL(max_final_kernel, dim3(1), dim3(256), 0, s, S.part, g, &S.ps->b);
-  hipLaunchKernelGGL(sumexp_kernel, dim3(g), dim3(256), 0, s, x, n, 1LL, &S.ps->b, S.part);
-  hipLaunchKernelGGL(lse_final_kernel, dim3(1), dim3(256), 0, s, S.part, g, &S.ps->b, out);
+  hipLaunchKernelGGL(col_max_kernel, dim3(g), dim3(256), 0, s, x, n, 1LL, 0LL, S.part, 0LL);
+  hipLaunchKernelGGL(max_final_kernel, dim3(1), dim3(256), 0, s, S.part, g, &S.ps->b, 0LL);
+  hipLaunchKernelGGL(sumexp_kernel, dim3(g), dim3(256), 0, s, x, n, 1LL, 0LL, &S.ps->b, S.part,
+                     0LL);
+  hipLaunchKernelGGL(lse_final_kernel, dim3(1), dim3(256), 0, s, S.part, g, &S.ps->b, out, 0LL);
   return hipGetLastError();
 }
 

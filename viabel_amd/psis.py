@@ -21,13 +21,37 @@ def _tail_cap(n, Reff):
     return int(np.ceil(min(0.2 * n, 3 * np.sqrt(n / Reff))))
 
 
+def _colmajor(lw):
+    """The (m, n) C-contiguous storage of a 2-D Fortran-ordered log-weight matrix
+    (n, m): an F-contiguous numpy array or a transposed contiguous float64
+    device tensor; None otherwise."""
+    if getattr(lw, 'ndim', 0) != 2 or lw.shape[1] < 2:
+        return None
+    if getattr(lw, 'is_cuda', False):
+        import torch
+        t = lw.t()
+        if lw.dtype == torch.float64 and not lw.is_contiguous() and t.is_contiguous():
+            return t
+        return None
+    if (isinstance(lw, np.ndarray) and lw.dtype == np.float64 and lw.flags.f_contiguous
+            and not lw.flags.c_contiguous):
+        return lw.T
+    return None
+
+
 def psislw_with_tail(lw, Reff=1.0):
     """psislw plus the tail order of each column.  A float64 device tensor
     input stays in HBM: the smoothed log weights come back as a device tensor
-    of shape (n, m); k and the tail orders are host arrays."""
-    dev = nat.device_tensor(lw)
-    if dev is None:
-        lw = np.asarray(lw, dtype=float)
+    of shape (n, m); k and the tail orders are host arrays.  Fortran-ordered
+    input (psis.py:146 works on such a copy), i.e. an F-contiguous array or the
+    transpose of a contiguous device tensor, is read in place and gives output
+    of the same order.  All columns run through the device pipeline together."""
+    cm = _colmajor(lw)
+    dev = None
+    if cm is None:
+        dev = nat.device_tensor(lw)
+        if dev is None:
+            lw = np.asarray(lw, dtype=float)
     if lw.ndim == 2:
         n, m = lw.shape
     elif lw.ndim == 1:
@@ -36,20 +60,31 @@ def psislw_with_tail(lw, Reff=1.0):
         raise ValueError("Argument `lw` must be 1 or 2 dimensional.")
     if n <= 1:
         raise ValueError("More than one log-weight needed.")
-    if dev is None:
-        src = nat.as_f64(lw.reshape(n, m))
-        out = np.empty((n, m))
-    else:
-        import torch
-        src = dev.reshape(n, m)
-        out = torch.empty((n, m), dtype=torch.float64, device=dev.device)
     k = np.empty(m)
     cap = _tail_cap(n, Reff)
     tail = np.empty((m, max(cap, 1)), dtype=np.int64)
     ntail = np.empty(m, dtype=np.int64)
-    nat.check(nat.lib().vb_psislw(nat.context().handle, nat.dptr(src), n, m, float(Reff),
-                                  nat.dptr(out), nat.dptr(k), nat.i64ptr(tail), max(cap, 1),
-                                  nat.i64ptr(ntail)))
+    if cm is not None:
+        if getattr(cm, 'is_cuda', False):
+            import torch
+            out_cm = torch.empty((m, n), dtype=torch.float64, device=cm.device)
+        else:
+            out_cm = np.empty((m, n))
+        nat.check(nat.lib().vb_psislw_colmajor(nat.context().handle, nat.dptr(cm), n, m,
+                                               float(Reff), nat.dptr(out_cm), nat.dptr(k),
+                                               nat.i64ptr(tail), max(cap, 1), nat.i64ptr(ntail)))
+        out = out_cm.T
+    else:
+        if dev is None:
+            src = nat.as_f64(lw.reshape(n, m))
+            out = np.empty((n, m))
+        else:
+            import torch
+            src = dev.reshape(n, m)
+            out = torch.empty((n, m), dtype=torch.float64, device=dev.device)
+        nat.check(nat.lib().vb_psislw(nat.context().handle, nat.dptr(src), n, m, float(Reff),
+                                      nat.dptr(out), nat.dptr(k), nat.i64ptr(tail), max(cap, 1),
+                                      nat.i64ptr(ntail)))
     tails = [tail[c, :ntail[c]].copy() for c in range(m)]
     return out, k, tails
 
@@ -58,7 +93,7 @@ def psislw(lw, Reff=1.0, overwrite_lw=False):
     """Pareto smoothed importance sampling (PSIS).  Returns (lw_out, kss);
     kss is a scalar for 1-D input (psis.py:204-206)."""
     out, k, _ = psislw_with_tail(lw, Reff)
-    if nat.device_tensor(lw) is not None:   # device in, device out (no copy to the host)
+    if getattr(lw, 'is_cuda', False):       # device in, device out (no copy to the host)
         return (out[:, 0], k[0]) if lw.ndim == 1 else (out, k)
     lw_arr = np.asarray(lw)
     if lw_arr.ndim == 1:

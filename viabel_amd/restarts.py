@@ -48,24 +48,27 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
                        learning_rate_end=learning_rate_end)
     run.advance_philox(n_iters, seed, stream_base, 0, stream_stride=stride)
     _, _, vals, smooth = run.result()
-    # the M log weights of each restart stay in HBM from the draws through the
-    # bounds and PSIS (one device buffer, reused)
+    # the M log weights of every restart stay in HBM from the draws through the
+    # bounds and PSIS: row j of one [restarts][M] buffer; PSIS then runs all
+    # restarts' columns in one batched pipeline (the buffer's transpose is the
+    # reference's Fortran-ordered (M, restarts) log-weight matrix)
     import torch
-    lw = torch.empty(int(n_bounds), dtype=torch.float64, device=torch.device('cuda', nat.context().device))
+    lw = torch.empty((len(ids), int(n_bounds)), dtype=torch.float64,
+                     device=torch.device('cuda', nat.context().device))
     recs = []
     for j, r in enumerate(ids):
         opt = smooth[j]
         bfam = family_factory()
         bfam.stream = (1 << 20) + r          # bound draws: a Philox stream of their own
-        experiments.log_weights(target, bfam, opt, n_bounds, return_samples=False, lw_out=lw)
-        res = bounds.all_bounds(lw, q_var=bfam.mean_and_cov(opt)[1],
+        experiments.log_weights(target, bfam, opt, n_bounds, return_samples=False, lw_out=lw[j])
+        res = bounds.all_bounds(lw[j], q_var=bfam.mean_and_cov(opt)[1],
                                 moment_bound_fn=lambda p: bfam.pth_moment(p, opt))
         elbo = float(res['log_norm_bound'])  # = mean log weight (bounds.py:170-172)
-        _, khat = psis.psislw(lw)
-        recs.append(np.concatenate([[r, elbo, res['d2'], res['W1'], res['W2'],
-                                     res['mean_error'], res['std_error'], res['cov_error'],
-                                     khat, vals[j, -1]], opt]))
-    return np.array(recs)
+        recs.append([r, elbo, res['d2'], res['W1'], res['W2'], res['mean_error'],
+                     res['std_error'], res['cov_error']])
+    khat = psis.psislw(lw.t())[1] if len(ids) > 1 else np.array([psis.psislw(lw[0])[1]])
+    return np.array([np.concatenate([rec, [khat[j], vals[j, -1]], smooth[j]])
+                     for j, rec in enumerate(recs)])
 
 
 def gather_records(local, n_restarts, width, group=None):
