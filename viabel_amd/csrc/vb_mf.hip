@@ -581,7 +581,13 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
 #endif
 
   int slot = W > 0 ? (int)(a.step0 % W) : 0;  // window ring slot of step i (i % W)
-  for (int s = 0; s < a.n_steps; ++s) {
+  // One step.  RO = 0: every wave runs the whole step (host noise, chunked
+  // draws); with overlapped draws the row waves (RO = 1) and the draw waves
+  // (RO = 2) run their own copies of the step loop — same barriers, disjoint
+  // work — so neither role's registers are held across the other's code.
+  auto step = [&](int s, auto role_tag) {
+    constexpr int RO = decltype(role_tag)::value;
+    const bool rows = RO == 1 || (RO == 0 && row_wave);
     const long long i = a.step0 + s;
     const long long ri = a.rng_step0 + s;
     double mu[DMAX], sg[DMAX];
@@ -677,7 +683,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
       if (L.pipe) {
         double* cur = s_e + (s & 1) * (kBlockDrawLds / 2);
         double* nxt = s_e + ((s + 1) & 1) * (kBlockDrawLds / 2);
-        if (row_wave)
+        if (rows)
           consume(cur, 0, N);
         else if (s + 1 < a.n_steps)
           draw_item(tid - RT, NT - RT, N * NP, 0, ri + 1, nxt);
@@ -689,7 +695,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
           draw_item(tid, NT, nc * NP, c0n, ri, s_e);
           VB_PH(1);
           __syncthreads();
-          if (row_wave) consume(s_e, c0n, nc);
+          if (rows) consume(s_e, c0n, nc);
           VB_PH(2);
           if (c0n + CH < N) __syncthreads();  // s_e is refilled by the next chunk
         }
@@ -698,21 +704,23 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
 
     double M = 0.0;
     if (a.chivi) {
-      if (row_wave) {
+      if (rows) {
         const double wm = wave_max_dpp(mloc);
         if (lane == 0) s_max[wid] = wm;
       }
       __syncthreads();
       M = s_max[0];
       for (int q = 1; q < RW; ++q) M = fmax(M, s_max[q]);
-      const double f = (mloc == -INFINITY) ? 0.0 : exp(a.alpha * (mloc - M));
+      if (rows) {
+        const double f = (mloc == -INFINITY) ? 0.0 : exp(a.alpha * (mloc - M));
 #pragma unroll
-      for (int k = 0; k <= 2 * DMAX; ++k) acc[k] *= f;
+        for (int k = 0; k <= 2 * DMAX; ++k) acc[k] *= f;
+      }
     }
     VB_PH(3);
-    if (row_wave) wave_reduce_scatter<K>(acc, s_red[wid]);
+    if (rows) wave_reduce_scatter<K>(acc, s_red[wid]);
     __syncthreads();
-    if (tid < K) {
+    if (RO != 2 && tid < K) {
       double t = s_red[0][tid];
       for (int q = 1; q < RW; ++q) t += s_red[q][tid];
       s_red[0][tid] = t;  // each thread only touches its own column
@@ -720,8 +728,8 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
     __syncthreads();
     VB_PH(4);
 
-    // gradient + update: thread p owns parameter p
-    if (tid < P) {
+    // gradient + update: thread p owns parameter p (wave 0, a row wave)
+    if (RO != 2 && tid < P) {
       const int p = tid;
       double gp;
       if (!a.chivi) {
@@ -776,7 +784,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
         if (p >= D) s_sg[p - D] = exp(nl);
       }
     }
-    if (tid == val_tid) {
+    if (RO != 1 && tid == val_tid) {
       double val;
       if (!a.chivi) {
         // entropy uses the pre-update lam: sum_d log sigma_d
@@ -790,6 +798,21 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
     slot = slot + 1 == W ? 0 : slot + 1;
     __syncthreads();
     VB_PH(6);
+  };
+  // (the t family keeps one shared loop: its draw waves, the critical path there,
+  // measured slower in their own copy)
+  bool split = false;
+  if constexpr (!HOST && !TFAM) split = L.pipe;
+  if (split) {
+    if constexpr (!HOST && !TFAM) {
+      if (row_wave) {
+        for (int s = 0; s < a.n_steps; ++s) step(s, std::integral_constant<int, 1>{});
+      } else {
+        for (int s = 0; s < a.n_steps; ++s) step(s, std::integral_constant<int, 2>{});
+      }
+    }
+  } else {
+    for (int s = 0; s < a.n_steps; ++s) step(s, std::integral_constant<int, 0>{});
   }
 #ifdef VB_BLOCK_PROF
   if (prob == 0 && tid == 0) {
