@@ -532,6 +532,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   const double c0 = TFAM ? 0.0 : 0.5 * D * (1.0 + kLog2Pi);
   const int NP = (D + 1) / 2;
   const double lq_half = 0.5 * (a.df + 1.0);
+  const double inv_df = 1.0 / a.df;
 
   // one (sample, pair) draw item: e pair [+ log q partial of the pair, sans -log sigma]
   auto draw_item = [&](int it0, int it_step, int n_items, int nbase, long long ri, double* buf) {
@@ -543,8 +544,9 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
       if constexpr (TFAM) {
         double ga, gb;
         gamma_pair<true>(rng, (uint32_t)j, n, (uint32_t)ri, a.shape, ga, gb, s_sct, s_lt);
-        ea = a.t_scale * ea / sqrt(ga);
-        eb = a.t_scale * eb / sqrt(gb);
+        // t = sqrt(df / 2) z / sqrt(G): a refined rsqrt instead of sqrt + divide
+        ea = a.t_scale * ea * rsqrt_pos(ga);
+        eb = a.t_scale * eb * rsqrt_pos(gb);
       }
       double* rec = buf + nl * R;
       rec[2 * j] = ea;
@@ -553,8 +555,8 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
         const bool hasb = 2 * j + 1 < D;
         double lqp;
         if constexpr (TFAM) {
-          lqp = a.t_const - log1p(ea * ea / a.df) * lq_half;
-          if (hasb) lqp += a.t_const - log1p(eb * eb / a.df) * lq_half;
+          lqp = a.t_const - log1p(ea * ea * inv_df) * lq_half;
+          if (hasb) lqp += a.t_const - log1p(eb * eb * inv_df) * lq_half;
         } else {
           lqp = -0.5 * ea * ea - 0.5 * kLog2Pi;
           if (hasb) lqp += -0.5 * eb * eb - 0.5 * kLog2Pi;
