@@ -124,6 +124,20 @@ _lib = None
 _lock = threading.Lock()
 
 
+def _load_torch_runtime():
+    """PyTorch bundles its own HIP / HSA runtime (torch/lib/libamdhip64.so,
+    libhsa-runtime64.so) with the same sonames as the ROCm runtime this library
+    links (libamdhip64.so.7, libhsa-runtime64.so.1), so whichever loads first
+    serves the whole process.  Device tensors are how callers hand this library
+    HBM-resident data, and torch works only on its own runtime: load torch first
+    so that this library binds to it (with the ROCm runtime loaded first, torch
+    reports "No HIP GPUs are available")."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def lib():
     """Load libviabel_amd.so (raises ImportError when it was not built)."""
     global _lib
@@ -135,6 +149,7 @@ def lib():
                         'viabel_amd: HIP library %s not found; build it with '
                         '`python -c "import __graft_entry__ as g; g.build()"` or '
                         '`make -C viabel_amd/csrc`' % LIB_PATH)
+                _load_torch_runtime()
                 L = ctypes.CDLL(LIB_PATH)
                 for name, (args, res) in _SIGNATURES.items():
                     fn = getattr(L, name)
@@ -165,30 +180,10 @@ def check(rc):
     raise RuntimeError(msg)
 
 
-def _torch_runtime_first():
-    """PyTorch ships its own HIP runtime (torch/lib/libamdhip64.so) beside the
-    ROCm runtime this library links.  Both work in one process only when
-    torch's opens the GPU first: after the ROCm runtime has, torch reports "No
-    HIP GPUs are available".  Device tensors are how callers hand this library
-    HBM-resident data (and the restart / log-weight paths allocate them), so
-    torch's runtime is initialised before the first context when torch is
-    installed."""
-    try:
-        import torch
-    except Exception:
-        return
-    try:
-        if torch.cuda.is_available():
-            torch.cuda.init()
-    except Exception:
-        pass
-
-
 class Context:
     """One vb_ctx (device + HIP stream)."""
 
     def __init__(self, device=0, stream=None):
-        _torch_runtime_first()
         h = ctypes.c_void_p()
         check(lib().vb_ctx_create(int(device), stream, ctypes.byref(h)))
         self.handle = h
