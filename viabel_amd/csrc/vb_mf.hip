@@ -927,6 +927,84 @@ __global__ __launch_bounds__(256) void funnel_wide_kernel(int D, long long n, co
   }
 }
 
+// ---- wide rows (D >= kWideRowD, few rows): one 1024-thread block per row --------
+// The one-wavefront-per-row kernels above suit many short rows (log weights: m
+// rows of D <= 16 or so); a step of the materialised mean-field path has N ~ 100
+// rows of D ~ 1e4, where one wave per row leaves the chip ~90 % idle.  Fixed-order
+// block reductions keep the sums deterministic.
+constexpr int kWideRowD = 512;
+
+__device__ __forceinline__ double block_sum_1024(double v, double* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) t += red[q];
+  __syncthreads();
+  return t;
+}
+
+template <bool TFAM>
+__global__ __launch_bounds__(1024) void family_logdensity_rowblock_kernel(int D, const double* lam,
+                                                                         double df, double t_const,
+                                                                         const double* x,
+                                                                         double* out) {
+  __shared__ double red[16];
+  const long long r = blockIdx.x;
+  double acc = 0.0;
+  for (int d = threadIdx.x; d < D; d += 1024) {
+    const double ls = lam[D + d];
+    const double z = (x[r * D + d] - lam[d]) / exp(ls);
+    if constexpr (TFAM)
+      acc += t_const - log1p(z * z / df) * (0.5 * (df + 1.0)) - ls;
+    else
+      acc += -0.5 * z * z - ls - 0.5 * kLog2Pi;
+  }
+  acc = block_sum_1024(acc, red);
+  if (threadIdx.x == 0) out[r] = acc;
+}
+
+template <class TGT>
+__global__ __launch_bounds__(1024) void target_sep_rowblock_kernel(int D, const double* x,
+                                                                  double* out, double* grad) {
+  __shared__ double red[16];
+  const long long r = blockIdx.x;
+  double acc = 0.0;
+  for (int d = threadIdx.x; d < D; d += 1024) {
+    double g;
+    acc += TGT::lp1(x[r * D + d], g);
+    if (grad) grad[r * D + d] = g;
+  }
+  acc = block_sum_1024(acc, red);
+  if (threadIdx.x == 0) out[r] = acc;
+}
+
+__global__ __launch_bounds__(1024) void funnel_rowblock_kernel(int D, const double* x, double* out,
+                                                               double* grad) {
+  __shared__ double red[16];
+  const long long r = blockIdx.x;
+  constexpr double s0 = 1.35;
+  const double v = x[r * D + 1];
+  const double scale = exp(v), inv_s2 = exp(-2.0 * v);
+  double lp = 0.0, gv = 0.0;
+  for (int d = threadIdx.x; d < D; d += 1024) {
+    if (d == 1) continue;
+    const double xd = x[r * D + d];
+    const double z = xd / scale;
+    lp += -0.5 * z * z - v - 0.5 * kLog2Pi;
+    if (grad) grad[r * D + d] = -xd * inv_s2;
+    gv += z * z - 1.0;
+  }
+  lp = block_sum_1024(lp, red);
+  gv = block_sum_1024(gv, red);
+  if (threadIdx.x == 0) {
+    const double zv = v / s0;
+    out[r] = (-0.5 * zv * zv - log(s0) - 0.5 * kLog2Pi) + lp;
+    if (grad) grad[r * D + 1] = -zv / s0 + gv;
+  }
+}
+
 template <class TGT, int DMAX>
 __global__ __launch_bounds__(256) void target_row_kernel(int D, long long n, const double* x,
                                                          double* out, double* grad) {
@@ -1270,6 +1348,15 @@ hipError_t launch_family_logdensity(int fam, int D, long long n, const double* l
                                     double t_const, const double* x, double* out,
                                     hipStream_t s) {
   if (n == 0) return hipSuccess;
+  if (D >= kWideRowD && n <= 65535) {
+    if (fam == 1)
+      hipLaunchKernelGGL((family_logdensity_rowblock_kernel<true>), dim3((unsigned)n), dim3(1024),
+                         0, s, D, lam, df, t_const, x, out);
+    else
+      hipLaunchKernelGGL((family_logdensity_rowblock_kernel<false>), dim3((unsigned)n), dim3(1024),
+                         0, s, D, lam, df, t_const, x, out);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)((n + 3) / 4)), block(256);
   if (fam == 1)
     hipLaunchKernelGGL((family_logdensity_kernel<true>), grid, block, 0, s, D, n, lam, df,
@@ -1284,6 +1371,15 @@ hipError_t launch_target_logdensity(int tgt, int D, long long n, const double* x
                                     double* grad, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const dim3 gw((unsigned)((n + 3) / 4)), gt((unsigned)((n + 255) / 256)), block(256);
+  if (D >= kWideRowD && n <= 65535 && tgt <= 2) {
+    const dim3 gb((unsigned)n), bb(1024);
+    switch (tgt) {
+      case 0: hipLaunchKernelGGL((target_sep_rowblock_kernel<IsoGauss>), gb, bb, 0, s, D, x, out, grad); break;
+      case 1: hipLaunchKernelGGL((target_sep_rowblock_kernel<Mixture>), gb, bb, 0, s, D, x, out, grad); break;
+      default: hipLaunchKernelGGL(funnel_rowblock_kernel, gb, bb, 0, s, D, x, out, grad); break;
+    }
+    return hipGetLastError();
+  }
   switch (tgt) {
     case 0: hipLaunchKernelGGL((target_sep_kernel<IsoGauss>), gw, block, 0, s, D, n, x, out, grad); break;
     case 1: hipLaunchKernelGGL((target_sep_kernel<Mixture>), gw, block, 0, s, D, n, x, out, grad); break;
