@@ -44,7 +44,7 @@ def _close(a, b, rtol):
 
 @pytest.mark.parametrize('kind,df', FAMS)
 @pytest.mark.parametrize('target,D', [('isogauss', 17), ('mixture', 300), ('funnel', 40),
-                                      ('funnel', 1000)])
+                                      ('funnel', 1000), ('isogauss', 700), ('mixture', 1001)])
 @pytest.mark.parametrize('alpha', [2.0, 1.5])
 def test_chivi_wide_numpy_stream(kind, df, target, D, alpha):
     vb, targets, vo = _mods()
@@ -59,6 +59,33 @@ def test_chivi_wide_numpy_stream(kind, df, target, D, alpha):
         ov, og = vo.chivi_value_grad(ofam, target, lam, 64, alpha)
         assert abs(v - ov) <= 1e-10 * max(1.0, abs(ov))
         _close(g, og, 1e-10)
+
+
+@pytest.mark.parametrize('kind,df', FAMS)
+@pytest.mark.parametrize('target,D', [('mixture', 1001), ('isogauss', 3000)])
+def test_chivi_wide_philox_fused_rows(kind, df, target, D):
+    """Fused per-row draw / target / log q kernel (separable targets, D >= 512):
+    its in-register Philox draws equal the C oracle's, so CHIVI matches the
+    oracle fed with rng_oracle noise."""
+    vb, targets, vo = _mods()
+    from oracle import rng_oracle as ro
+    N = 96
+    fam = (vb.mean_field_gaussian_variational_family(D, rng='philox') if kind == 'gauss'
+           else vb.mean_field_t_variational_family(D, df, rng='philox'))
+    ofam = vo.Family(kind, D, df)
+    obj = vb.black_box_chivi(2.0, fam, _target(targets, target, D), N)
+    for call in range(2):
+        lam = _lam(D, 40 + call)
+        # CHIVI keys each call's Philox draws with a seed from the global numpy
+        # RNG (vb.py:258 draws its seed the same way), family stream, step 0
+        np.random.seed(70 + call)
+        seed = np.random.randint(2 ** 32)
+        np.random.seed(70 + call)
+        v, g = obj(lam)
+        eps = ro.noise(seed, fam.stream, 0, N, D, kind, df or 0.0)
+        ov, og = vo.chivi_value_grad(ofam, target, lam, N, 2.0, eps=eps)
+        assert abs(v - ov) <= 1e-10 * max(1.0, abs(ov)), (v, ov)
+        _close(g, og, 1e-9)
 
 
 @pytest.mark.parametrize('kind,df', FAMS)

@@ -816,15 +816,25 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
                                     noise->stream + (uint32_t)q * stride,
                                     (uint32_t)(noise->step + off),
                                     r->values.d() + q * r->n_iters + step, r->grad.d(), c->stream));
-        else
+        double* hrow = step >= r->hist_start
+                           ? r->hist.d() + (q * r->n_hist + (step - r->hist_start)) * P
+                           : nullptr;
+        if (!r->fr && r->opt == VB_OPT_ADAGRAD) {
+          // gradient pass applies the adagrad step and writes the history row
+          const vbk::MfUpdate up{r->ring.d() + q * P * r->W, r->W, step, lr, r->eps, hrow};
+          VB_TRY(vbk::mf_wide_value_grad(W, r->mspec, lam, eps, k0, k1,
+                                         noise->stream + (uint32_t)q * stride,
+                                         (uint32_t)(noise->step + off),
+                                         r->values.d() + q * r->n_iters + step, r->grad.d(),
+                                         c->stream, &up));
+          continue;
+        }
+        if (!r->fr)
           VB_TRY(vbk::mf_wide_value_grad(W, r->mspec, lam, eps, k0, k1,
                                          noise->stream + (uint32_t)q * stride,
                                          (uint32_t)(noise->step + off),
                                          r->values.d() + q * r->n_iters + step, r->grad.d(),
                                          c->stream));
-        double* hrow = step >= r->hist_start
-                           ? r->hist.d() + (q * r->n_hist + (step - r->hist_start)) * P
-                           : nullptr;
         if (r->opt != VB_OPT_ADAGRAD) {
           VB_HIP(vbk::launch_ia_update(r->opt, (long long)P, lam, r->grad.d(),
                                        r->ring.d() + q * P * r->W, step, lr, r->eps, 0.0, hrow,

@@ -517,4 +517,27 @@ struct SepRow {
   }
 };
 
+// Windowed adagrad update of coordinate p (vb.py:365-374, the reference's
+// "adagrad" step): store g in the ring slot of this step, q = sum over the last
+// min(step + 1, W) slots of (scale_k g_k)^2, oldest first, and return
+// lam - lr g / sqrt(eps + q).  Shared by adagrad_update_kernel and the fused
+// gradient + update pass of the materialised mean-field path.
+__device__ __forceinline__ double adagrad_step(long long p, long long P, double lam, double g,
+                                               double* ring, int W, long long step, double lr,
+                                               double eps, const double* scale) {
+  const int slot = (int)(step % W);
+  ring[(long long)slot * P + p] = g;
+  const int cnt = (step + 1 < W) ? (int)(step + 1) : W;
+  const int oldest = (cnt < W) ? 0 : (int)((step + 1) % W);
+  double q = 0.0;
+  for (int k = 0; k < cnt; ++k) {
+    int L = oldest + k;
+    if (L >= W) L -= W;
+    double t = L == slot ? g : ring[(long long)L * P + p];
+    if (scale) t = __dmul_rn(scale[k], t);
+    q = __dadd_rn(q, __dmul_rn(t, t));
+  }
+  return __dsub_rn(lam, __dmul_rn(lr, g) / sqrt(__dadd_rn(eps, q)));
+}
+
 }  // namespace vbd

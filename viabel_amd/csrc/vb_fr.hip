@@ -852,17 +852,42 @@ namespace {
 // KLVI: value = -(entropy + mean logp), r_n = -1/N, rsum = -1 (the entropy's
 // d/dlog sigma).  CHIVI: lw = logp - logq, w = exp(lw - max)^alpha,
 // value = log(mean w)/alpha + max, r_n = alpha w_n / N, rsum = sum_n r_n.
+// logp / logq hold nparts partials per row ([part][N], summed in part order).
+__device__ __forceinline__ double parts_sum(const double* p, int nparts, int N, int k) {
+  double a = p[k];
+  for (int c = 1; c < nparts; ++c) a += p[(long long)c * N + k];
+  return a;
+}
+
 __global__ __launch_bounds__(1024) void mfw_weights_kernel(int N, int D, int chivi, int pd,
                                                            double alpha,
                                                            double c0, const double* lam,
                                                            const double* logp,
-                                                           const double* logq, double* r,
-                                                           double* scal, double* value) {
+                                                           const double* logq, int nparts,
+                                                           double* r, double* scal,
+                                                           double* value) {
   __shared__ double red[16];
+  // stage the chunk partials in LDS first: many independent loads in flight
+  // instead of each thread's chain of nparts dependent global round trips
+  constexpr int kPartsLds = 6144;
+  __shared__ double s_parts[kPartsLds];
+  const int pn = nparts * N;
+  if (nparts > 1 && 2LL * pn <= kPartsLds) {
+    const bool lq = chivi || pd;
+#pragma unroll 4
+    for (int i = threadIdx.x; i < pn; i += blockDim.x) {
+      s_parts[i] = logp[i];
+      s_parts[pn + i] = lq ? logq[i] : 0.0;
+    }
+    __syncthreads();
+    logp = s_parts;
+    logq = s_parts + pn;
+  }
   if (!chivi) {
     double a = 0.0, e = 0.0;
     for (int k = threadIdx.x; k < N; k += blockDim.x) {
-      a += pd ? logp[k] - logq[k] : logp[k];  // black_box_klvi_pd: sampled log q
+      const double lpk = parts_sum(logp, nparts, N, k);
+      a += pd ? lpk - parts_sum(logq, nparts, N, k) : lpk;  // black_box_klvi_pd: sampled log q
       r[k] = -1.0 / N;
     }
     for (int d = threadIdx.x; d < D; d += blockDim.x) e += lam[D + d];
@@ -874,20 +899,29 @@ __global__ __launch_bounds__(1024) void mfw_weights_kernel(int N, int D, int chi
     }
     return;
   }
-  double mx = -INFINITY;
-  for (int k = threadIdx.x; k < N; k += blockDim.x) {
-    const double lw = logp[k] - logq[k];
-    r[k] = lw;
-    mx = fmax(mx, lw);
+  double mx = -INFINITY, sw = 0.0;
+  if (N <= (int)blockDim.x) {  // one row per thread: log weights stay in registers
+    const int k = threadIdx.x;
+    const double lw =
+        k < N ? parts_sum(logp, nparts, N, k) - parts_sum(logq, nparts, N, k) : -INFINITY;
+    mx = block_max(lw, red);
+    const double w = k < N ? pow(exp(lw - mx), alpha) : 0.0;
+    if (k < N) r[k] = alpha * w / N;
+    sw = block_sum(w, red);
+  } else {
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+      const double lw = parts_sum(logp, nparts, N, k) - parts_sum(logq, nparts, N, k);
+      r[k] = lw;
+      mx = fmax(mx, lw);
+    }
+    mx = block_max(mx, red);
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+      const double w = pow(exp(r[k] - mx), alpha);
+      sw += w;
+      r[k] = alpha * w / N;
+    }
+    sw = block_sum(sw, red);
   }
-  mx = block_max(mx, red);
-  double sw = 0.0;
-  for (int k = threadIdx.x; k < N; k += blockDim.x) {
-    const double w = pow(exp(r[k] - mx), alpha);
-    sw += w;
-    r[k] = alpha * w / N;
-  }
-  sw = block_sum(sw, red);
   if (threadIdx.x == 0) {
     *value = log(sw / N) / alpha + mx;
     scal[1] = alpha * sw / N;
@@ -895,31 +929,108 @@ __global__ __launch_bounds__(1024) void mfw_weights_kernel(int N, int D, int chi
 }
 
 // grad_mu_j = sum_n r_n G_nj;  grad_logsigma_j = sigma_j sum_n r_n G_nj z_nj + rsum,
-// z = (x - mu) / sigma (the standardized draw).  Four waves split the rows.
-__global__ __launch_bounds__(256) void mfw_grad_kernel(int N, int D, const double* lam,
-                                                       const double* X, const double* G,
-                                                       const double* r, const double* scal,
-                                                       double* grad) {
-  __shared__ double pa[4][64], pb[4][64];
+// z = (x - mu) / sigma (the standardized draw).  kGradWaves waves split the rows
+// (enough waves in flight to stream X and G with N ~ 100 rows per column);
+// partial sums combined in a fixed order.
+//
+// WFUSE (CHIVI, N <= 1024): every block first recomputes the CHIVI weights of
+// mfw_weights_kernel from the per-row log p / log q partials (staged in LDS; the
+// same expressions, so r and rsum are bitwise those of the separate kernel) and
+// block 0 writes the value: one launch fewer per step.
+// UPD: apply the windowed adagrad step to the block's columns right after their
+// gradient (adagrad_step, as adagrad_update_kernel) and copy the new parameters
+// to the history row: two launches fewer.  Safe because a block reads and
+// writes only its own columns of lam.
+constexpr int kGradWaves = 16;
+constexpr int kGradLds = 6144;  // doubles: chunk-partial staging, then pa / pb
+
+struct MfwGradArgs {
+  int N, D, nparts;
+  double alpha;
+  double* lam;
+  const double *X, *G, *r, *scal, *logp, *logq;
+  double *grad, *value;
+  double* ring;  // UPD
+  int W;
+  long long step;
+  double lr, eps;
+  double* hrow;  // nullable
+};
+
+template <bool WFUSE, bool UPD>
+__global__ __launch_bounds__(64 * kGradWaves) void mfw_grad_kernel(MfwGradArgs A) {
+  __shared__ double buf[kGradLds];
+  __shared__ double s_r[WFUSE ? 1024 : 1];
+  __shared__ double red[16];
+  const int N = A.N, D = A.D;
+  const double* r = A.r;
+  double rsum;
+  if constexpr (WFUSE) {
+    const double *logp = A.logp, *logq = A.logq;
+    const int pn = A.nparts * N;
+    if (A.nparts > 1 && 2LL * pn <= kGradLds) {
+#pragma unroll 4
+      for (int i = threadIdx.x; i < pn; i += blockDim.x) {
+        buf[i] = logp[i];
+        buf[pn + i] = logq[i];
+      }
+      __syncthreads();
+      logp = buf;
+      logq = buf + pn;
+    }
+    const int k = threadIdx.x;
+    const double lw =
+        k < N ? parts_sum(logp, A.nparts, N, k) - parts_sum(logq, A.nparts, N, k) : -INFINITY;
+    const double mx = block_max(lw, red);
+    const double w = k < N ? pow(exp(lw - mx), A.alpha) : 0.0;
+    if (k < N) s_r[k] = A.alpha * w / N;
+    const double sw = block_sum(w, red);  // its barriers publish s_r and free buf
+    rsum = A.alpha * sw / N;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      *A.value = log(sw / N) / A.alpha + mx;
+    }
+    r = s_r;
+  } else {
+    rsum = A.scal[1];
+  }
+  double(*pa)[64] = reinterpret_cast<double(*)[64]>(buf);
+  double(*pb)[64] = reinterpret_cast<double(*)[64]>(buf + kGradWaves * 64);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + lane;
   double a = 0.0, b = 0.0;
   if (j < D) {
-    const double mu = lam[j], sg = exp(lam[D + j]);
-    for (int n = wv; n < N; n += 4) {
-      const double g = r[n] * G[(long long)n * D + j];
+    const double mu = A.lam[j], sg = exp(A.lam[D + j]);
+    for (int n = wv; n < N; n += kGradWaves) {
+      const double g = r[n] * A.G[(long long)n * D + j];
       a += g;
-      b += g * ((X[(long long)n * D + j] - mu) / sg);
+      b += g * ((A.X[(long long)n * D + j] - mu) / sg);
     }
   }
   pa[wv][lane] = a;
   pb[wv][lane] = b;
   __syncthreads();
   if (wv == 0 && j < D) {
-    const double sa = (pa[0][lane] + pa[1][lane]) + (pa[2][lane] + pa[3][lane]);
-    const double sb = (pb[0][lane] + pb[1][lane]) + (pb[2][lane] + pb[3][lane]);
-    grad[j] = sa;
-    grad[D + j] = exp(lam[D + j]) * sb + scal[1];
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int q = 0; q < kGradWaves; ++q) {
+      sa += pa[q][lane];
+      sb += pb[q][lane];
+    }
+    const double ls = A.lam[D + j];
+    const double gm = sa, gs = exp(ls) * sb + rsum;
+    A.grad[j] = gm;
+    A.grad[D + j] = gs;
+    if constexpr (UPD) {
+      const long long P = 2LL * D;
+      const double nm = adagrad_step(j, P, A.lam[j], gm, A.ring, A.W, A.step, A.lr, A.eps, nullptr);
+      const double ns = adagrad_step(D + j, P, ls, gs, A.ring, A.W, A.step, A.lr, A.eps, nullptr);
+      A.lam[j] = nm;
+      A.lam[D + j] = ns;
+      if (A.hrow) {
+        A.hrow[j] = nm;
+        A.hrow[D + j] = ns;
+      }
+    }
   }
 }
 
@@ -927,22 +1038,67 @@ __global__ __launch_bounds__(256) void mfw_grad_kernel(int N, int D, const doubl
 
 int mf_wide_value_grad(FrWork* W, const MfSpec& f, const double* lam, const double* host_eps,
                        uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
-                       double* grad, hipStream_t st) {
+                       double* grad, hipStream_t st, const MfUpdate* up) {
   const int D = f.D, N = f.N;
   if (int rc = reserve_d(W, 1, st)) return rc;
   if (int rc = reserve_n(W, D, N)) return rc;
-  FR_HIP(launch_sample(f.fam, D, N, lam, f.t_scale, f.shape, host_eps, k0, k1, stream, step,
-                       W->X.d(), st));
   if (f.tgt == kTargetCorrGauss)
     return vb_set_error(-4, "corr_gauss is implemented for the full-rank family only");
-  if (int rc = eval_target(W, f.tgt, f.host, D, N, W->X.d(), W->logp.d(), W->G.d(), st)) return rc;
-  if (f.chivi || f.pd)
-    FR_HIP(launch_family_logdensity(f.fam, D, N, lam, f.df, f.t_const, W->X.d(), W->zz.d(), st));
+  // per-row log p / log q: one value per row, or chunk partials of the fused kernel (in Z,
+  // unused on this path: nparts * N * 2 <= N * D for D >= 512)
+  int nparts = 1;
+  double *lp = W->logp.d(), *lq = W->zz.d();
+  if (mfw_rows_fusable(f.tgt, D, N)) {
+    nparts = mfw_rows_parts(D);
+    lp = W->Z.d();
+    lq = lp + (size_t)nparts * N;
+    FR_HIP(launch_mfw_rows(f.fam, f.tgt, D, N, lam, f.t_scale, f.shape, f.df, f.t_const,
+                           f.chivi || f.pd, host_eps, k0, k1, stream, step, W->X.d(), W->G.d(),
+                           lp, lq, st));
+  } else {
+    FR_HIP(launch_sample(f.fam, D, N, lam, f.t_scale, f.shape, host_eps, k0, k1, stream, step,
+                         W->X.d(), st));
+    if (int rc = eval_target(W, f.tgt, f.host, D, N, W->X.d(), W->logp.d(), W->G.d(), st))
+      return rc;
+    if (f.chivi || f.pd)
+      FR_HIP(launch_family_logdensity(f.fam, D, N, lam, f.df, f.t_const, W->X.d(), W->zz.d(), st));
+  }
   const double c0 = f.fam == 1 ? 0.0 : 0.5 * D * (1.0 + kLog2Pi);
-  hipLaunchKernelGGL(mfw_weights_kernel, dim3(1), dim3(1024), 0, st, N, D, f.chivi, f.pd, f.alpha, c0,
-                     lam, W->logp.d(), W->zz.d(), W->r.d(), W->scal.d(), value);
-  hipLaunchKernelGGL(mfw_grad_kernel, dim3(blocks(D, 64)), dim3(256), 0, st, N, D, lam, W->X.d(),
-                     W->G.d(), W->r.d(), W->scal.d(), grad);
+  const bool wfuse = f.chivi && N <= 1024;
+  if (!wfuse)
+    hipLaunchKernelGGL(mfw_weights_kernel, dim3(1), dim3(1024), 0, st, N, D, f.chivi, f.pd,
+                       f.alpha, c0, lam, lp, lq, nparts, W->r.d(), W->scal.d(), value);
+  MfwGradArgs A{};
+  A.N = N;
+  A.D = D;
+  A.nparts = nparts;
+  A.alpha = f.alpha;
+  A.lam = const_cast<double*>(lam);  // written only with an update (the caller's parameters)
+  A.X = W->X.d();
+  A.G = W->G.d();
+  A.r = W->r.d();
+  A.scal = W->scal.d();
+  A.logp = lp;
+  A.logq = lq;
+  A.grad = grad;
+  A.value = value;
+  if (up) {
+    A.ring = up->ring;
+    A.W = up->W;
+    A.step = up->step;
+    A.lr = up->lr;
+    A.eps = up->eps;
+    A.hrow = up->hrow;
+  }
+  const dim3 gg(blocks(D, 64)), gb(64 * kGradWaves);
+  if (wfuse && up)
+    hipLaunchKernelGGL((mfw_grad_kernel<true, true>), gg, gb, 0, st, A);
+  else if (wfuse)
+    hipLaunchKernelGGL((mfw_grad_kernel<true, false>), gg, gb, 0, st, A);
+  else if (up)
+    hipLaunchKernelGGL((mfw_grad_kernel<false, true>), gg, gb, 0, st, A);
+  else
+    hipLaunchKernelGGL((mfw_grad_kernel<false, false>), gg, gb, 0, st, A);
   FR_HIP(hipGetLastError());
   return 0;
 }

@@ -85,6 +85,16 @@ hipError_t launch_family_logdensity(int fam, int D, long long n, const double* l
                                     double t_const, const double* x, double* out, hipStream_t s);
 hipError_t launch_target_logdensity(int tgt, int D, long long n, const double* x, double* out,
                                     double* grad, hipStream_t s);
+// fused materialised step rows (draw, x, target log p + gradient, optional log q)
+// for separable device targets with wide rows; see mfw_rows_kernel.  logp / logq
+// receive mfw_rows_parts(D) chunk partials per row, laid out [part][n].
+bool mfw_rows_fusable(int tgt, int D, long long n);
+int mfw_rows_parts(int D);
+hipError_t launch_mfw_rows(int fam, int tgt, int D, long long n, const double* lam, double t_scale,
+                           double shape, double df, double t_const, bool with_lq,
+                           const double* noise, uint32_t k0, uint32_t k1, uint32_t stream,
+                           uint32_t step, double* x, double* grad, double* logp, double* logq,
+                           hipStream_t s);
 hipError_t launch_log_weights(int fam, int tgt, int D, long long m, const double* lam,
                               double t_scale, double shape, double df, double t_const,
                               const double* noise, uint32_t k0, uint32_t k1, uint32_t stream,
@@ -196,9 +206,19 @@ struct MfSpec {
   double alpha, t_scale, shape, df, t_const;
   HostTarget host;  // tgt == kTargetCallback
 };
+// Optional windowed-adagrad step fused into the gradient pass (lam updated in
+// place, the step's gradient pushed into ring [W][P], new parameters copied to
+// hrow when non-null); same arithmetic as launch_adagrad_update without scales.
+struct MfUpdate {
+  double* ring;
+  int W;
+  long long step;
+  double lr, eps;
+  double* hrow;
+};
 int mf_wide_value_grad(FrWork* W, const MfSpec& f, const double* lam, const double* host_eps,
                        uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
-                       double* grad, hipStream_t st);
+                       double* grad, hipStream_t st, const MfUpdate* up = nullptr);
 int mf_wide_log_weights(FrWork* W, const MfSpec& f, const double* lam, long long m,
                         const double* host_eps, uint32_t k0, uint32_t k1, uint32_t stream,
                         uint32_t step, double* lw, double* xs, hipStream_t st);

@@ -1030,19 +1030,7 @@ __global__ __launch_bounds__(256) void adagrad_update_kernel(long long P, double
                                                              double eps, const double* scale) {
   const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
   if (p >= P) return;
-  const int slot = (int)(step % W);
-  ring[(long long)slot * P + p] = g[p];
-  const int cnt = (step + 1 < W) ? (int)(step + 1) : W;
-  const int oldest = (cnt < W) ? 0 : (int)((step + 1) % W);
-  double q = 0.0;
-  for (int k = 0; k < cnt; ++k) {
-    int L = oldest + k;
-    if (L >= W) L -= W;
-    double t = ring[(long long)L * P + p];
-    if (scale) t = __dmul_rn(scale[k], t);
-    q = __dadd_rn(q, __dmul_rn(t, t));
-  }
-  lam[p] = __dsub_rn(lam[p], __dmul_rn(lr, g[p]) / sqrt(__dadd_rn(eps, q)));
+  lam[p] = adagrad_step(p, P, lam[p], g[p], ring, W, step, lr, eps, scale);
 }
 
 __global__ __launch_bounds__(256) void ia_update_kernel(int opt, long long P, double* lam,
@@ -1341,6 +1329,163 @@ hipError_t launch_sample(int fam, int D, long long n, const double* lam, double 
   else
     hipLaunchKernelGGL((sample_kernel<false, false>), grid, block, 0, s, D, n, lam, t_scale,
                        shape, noise, rng, step, x);
+  return hipGetLastError();
+}
+
+// Fused materialised step for separable targets on wide rows.  Thread t of
+// block (c, b) owns column pair j = 256 c + t and walks kRowsPerBlock rows
+// b kRowsPerBlock + q: it draws the pair (same Philox counters as
+// sample_kernel, table transcendentals as the fused KLVI kernels), forms
+// x = eps sigma + mu, evaluates the target log density and its gradient and
+// (CHIVI / klvi_pd) the family log density of the same x, all from registers:
+// one pass over the rows instead of three kernels that re-read x from HBM.
+// The column constants (mu, sigma, 1/sigma, log q offsets) load once per
+// thread.  Writes x, grad and the chunk partials logp[c n + r], logq[c n + r]
+// (with_lq); the consumer sums the mfw_rows_parts(D) partials of a row in
+// chunk order (deterministic).
+constexpr int kRowChunkPairs = 256;
+constexpr int kRowsPerBlock = 4;  // 1, 2, 8: within 3 % (D = 1e4, N = 128)
+
+int mfw_rows_parts(int D) { return ((D + 1) / 2 + kRowChunkPairs - 1) / kRowChunkPairs; }
+
+template <class TGT, bool TFAM, bool HOST>
+__global__ __launch_bounds__(256) void mfw_rows_kernel(int D, long long n, const double* lam,
+                                                       double t_scale, double shape, double df,
+                                                       double t_const, int with_lq,
+                                                       const double* noise, Rng rng, uint32_t step,
+                                                       double* x, double* grad, double* logp,
+                                                       double* logq) {
+  __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
+  __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
+  __shared__ double red[2][kRowsPerBlock][4];
+  if constexpr (!HOST) {
+    load_bm_tables(s_sct, s_lt);
+    __syncthreads();
+  }
+  const int c = blockIdx.x;
+  const int j = c * kRowChunkPairs + (int)threadIdx.x;
+  const int npairs = (D + 1) / 2;
+  const bool act = j < npairs;
+  const int dA = 2 * j, dB = 2 * j + 1;
+  const bool hasB = act && dB < D;
+  const bool evenD = (D & 1) == 0;
+  double muA = 0.0, sA = 1.0, isA = 1.0, cA = 0.0;
+  double muB = 0.0, sB = 1.0, isB = 1.0, cB = 0.0;
+  if (act) {
+    const double ls = lam[D + dA];
+    muA = lam[dA];
+    sA = exp(ls);
+    isA = 1.0 / sA;
+    cA = TFAM ? t_const - ls : -ls - 0.5 * kLog2Pi;
+  }
+  if (hasB) {
+    const double ls = lam[D + dB];
+    muB = lam[dB];
+    sB = exp(ls);
+    isB = 1.0 / sB;
+    cB = TFAM ? t_const - ls : -ls - 0.5 * kLog2Pi;
+  }
+  const double hexp = 0.5 * (df + 1.0), idf = 1.0 / df;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long r0 = (long long)blockIdx.y * kRowsPerBlock;
+#pragma unroll 1
+  for (int q = 0; q < kRowsPerBlock; ++q) {
+    const long long r = r0 + q;
+    double lp = 0.0, lq = 0.0;
+    if (act && r < n) {
+      double eA, eB;
+      if constexpr (HOST) {
+        eA = noise[r * D + dA];
+        eB = hasB ? noise[r * D + dB] : 0.0;
+      } else {
+        normal_pair_tab(rng.draw((uint32_t)j, (uint32_t)r, step, 0u), eA, eB, s_sct, s_lt);
+        if constexpr (TFAM) {
+          double ga, gb;
+          gamma_pair<true>(rng, (uint32_t)j, (uint32_t)r, step, shape, ga, gb, s_sct, s_lt);
+          eA = t_scale * eA / sqrt(ga);
+          eB = t_scale * eB / sqrt(gb);
+        }
+      }
+      double gA, gB = 0.0;
+      const double xA = eA * sA + muA, xB = eB * sB + muB;
+      lp = TGT::lp1(xA, gA);
+      const double zA = (xA - muA) * isA;
+      lq = TFAM ? cA - log1p(zA * zA * idf) * hexp : fma(-0.5 * zA, zA, cA);
+      if (hasB) {
+        lp += TGT::lp1(xB, gB);
+        const double zB = (xB - muB) * isB;
+        lq += TFAM ? cB - log1p(zB * zB * idf) * hexp : fma(-0.5 * zB, zB, cB);
+      }
+      if (evenD) {  // 16-byte stores: the wave writes 1 KB of x and of grad contiguously
+        *reinterpret_cast<double2*>(x + r * D + dA) = double2{xA, xB};
+        *reinterpret_cast<double2*>(grad + r * D + dA) = double2{gA, gB};
+      } else {
+        x[r * D + dA] = xA;
+        grad[r * D + dA] = gA;
+        if (hasB) {
+          x[r * D + dB] = xB;
+          grad[r * D + dB] = gB;
+        }
+      }
+    }
+    lp = wave_sum_dpp(lp);
+    if (with_lq) lq = wave_sum_dpp(lq);
+    if (lane == 0) {
+      red[0][q][wave] = lp;
+      red[1][q][wave] = lq;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kRowsPerBlock) {
+    const int q = threadIdx.x;
+    const long long r = r0 + q;
+    if (r < n) {
+      logp[(long long)c * n + r] = (red[0][q][0] + red[0][q][1]) + (red[0][q][2] + red[0][q][3]);
+      if (with_lq)
+        logq[(long long)c * n + r] = (red[1][q][0] + red[1][q][1]) + (red[1][q][2] + red[1][q][3]);
+    }
+  }
+}
+
+template <class TGT>
+static void mfw_rows_dispatch(int fam, int D, long long n, const double* lam, double t_scale,
+                              double shape, double df, double t_const, bool with_lq,
+                              const double* noise, const Rng& rng, uint32_t step, double* x,
+                              double* grad, double* logp, double* logq, hipStream_t s) {
+  const dim3 g((unsigned)mfw_rows_parts(D), (unsigned)((n + kRowsPerBlock - 1) / kRowsPerBlock)),
+      b(256);
+  const int wl = with_lq ? 1 : 0;
+  if (noise && fam == 1)
+    hipLaunchKernelGGL((mfw_rows_kernel<TGT, true, true>), g, b, 0, s, D, n, lam, t_scale, shape,
+                       df, t_const, wl, noise, rng, step, x, grad, logp, logq);
+  else if (noise)
+    hipLaunchKernelGGL((mfw_rows_kernel<TGT, false, true>), g, b, 0, s, D, n, lam, t_scale, shape,
+                       df, t_const, wl, noise, rng, step, x, grad, logp, logq);
+  else if (fam == 1)
+    hipLaunchKernelGGL((mfw_rows_kernel<TGT, true, false>), g, b, 0, s, D, n, lam, t_scale, shape,
+                       df, t_const, wl, noise, rng, step, x, grad, logp, logq);
+  else
+    hipLaunchKernelGGL((mfw_rows_kernel<TGT, false, false>), g, b, 0, s, D, n, lam, t_scale, shape,
+                       df, t_const, wl, noise, rng, step, x, grad, logp, logq);
+}
+
+bool mfw_rows_fusable(int tgt, int D, long long n) {
+  return (tgt == 0 || tgt == 1) && D >= kWideRowD && n >= 1 && n <= 65535;
+}
+
+hipError_t launch_mfw_rows(int fam, int tgt, int D, long long n, const double* lam, double t_scale,
+                           double shape, double df, double t_const, bool with_lq,
+                           const double* noise, uint32_t k0, uint32_t k1, uint32_t stream,
+                           uint32_t step, double* x, double* grad, double* logp, double* logq,
+                           hipStream_t s) {
+  if (!mfw_rows_fusable(tgt, D, n)) return hipErrorInvalidValue;
+  const Rng rng{k0, k1, stream};
+  if (tgt == 0)
+    mfw_rows_dispatch<IsoGauss>(fam, D, n, lam, t_scale, shape, df, t_const, with_lq, noise, rng,
+                                step, x, grad, logp, logq, s);
+  else
+    mfw_rows_dispatch<Mixture>(fam, D, n, lam, t_scale, shape, df, t_const, with_lq, noise, rng,
+                               step, x, grad, logp, logq, s);
   return hipGetLastError();
 }
 
