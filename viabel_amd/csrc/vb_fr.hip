@@ -966,25 +966,50 @@ __global__ __launch_bounds__(64 * kGradWaves) void mfw_grad_kernel(MfwGradArgs A
   const double* r = A.r;
   double rsum;
   if constexpr (WFUSE) {
-    const double *logp = A.logp, *logq = A.logq;
-    const int pn = A.nparts * N;
-    if (A.nparts > 1 && 2LL * pn <= kGradLds) {
+    const int k = threadIdx.x, np = A.nparts;
+    double lw = -INFINITY;
+    const int G = np > 1 ? min(np, 1024 / max(N, 1)) : 1;  // threads per row for the part sums
+    if (G > 1) {
+      // thread (g, k) sums parts g, g + G, ... of row k (logp and logq) into LDS;
+      // then row k adds its G group sums in group order.  Independent loads, short
+      // chains: the per-row chain of 2 * nparts dependent loads was the long pole.
+      const int g = k / N, kk = k - g * N;
+      if (g < G) {
+        double a = 0.0, b = 0.0;
 #pragma unroll 4
-      for (int i = threadIdx.x; i < pn; i += blockDim.x) {
-        buf[i] = logp[i];
-        buf[pn + i] = logq[i];
+        for (int c = g; c < np; c += G) {
+          a += A.logp[(long long)c * N + kk];
+          b += A.logq[(long long)c * N + kk];
+        }
+        buf[g * N + kk] = a;
+        buf[(G + g) * N + kk] = b;
       }
       __syncthreads();
-      logp = buf;
-      logq = buf + pn;
+      if (k < N) {
+        double a = buf[k], b = buf[G * N + k];
+        for (int q = 1; q < G; ++q) {
+          a += buf[q * N + k];
+          b += buf[(G + q) * N + k];
+        }
+        lw = a - b;
+      }
+    } else if (k < N) {
+      lw = parts_sum(A.logp, np, N, k) - parts_sum(A.logq, np, N, k);
     }
-    const int k = threadIdx.x;
-    const double lw =
-        k < N ? parts_sum(logp, A.nparts, N, k) - parts_sum(logq, A.nparts, N, k) : -INFINITY;
-    const double mx = block_max(lw, red);
+    const int nw = (N + 63) >> 6, wave = k >> 6;  // waves holding rows
+    double m = wave_max_dpp(lw);
+    if ((k & 63) == 0) red[wave] = m;
+    __syncthreads();
+    double mx = red[0];
+    for (int q = 1; q < nw; ++q) mx = fmax(mx, red[q]);
     const double w = k < N ? pow(exp(lw - mx), A.alpha) : 0.0;
     if (k < N) s_r[k] = A.alpha * w / N;
-    const double sw = block_sum(w, red);  // its barriers publish s_r and free buf
+    const double ws = wave_sum_dpp(w);
+    __syncthreads();
+    if ((k & 63) == 0) red[wave] = ws;
+    __syncthreads();  // also publishes s_r and frees buf for pa / pb
+    double sw = red[0];
+    for (int q = 1; q < nw; ++q) sw += red[q];
     rsum = A.alpha * sw / N;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       *A.value = log(sw / N) / A.alpha + mx;
