@@ -153,6 +153,24 @@ def test_rmsprop_ia_wide():
     _close(res[4], ores[4], 1e-7)
 
 
+@pytest.mark.parametrize('kind,df', FAMS)
+def test_rmsprop_ia_wide_fused_rows(kind, df):
+    """KLVI through the fused rows kernel (separable target, D >= 512) with the
+    separate weights pass and no fused update (IA optimiser)."""
+    vb, targets, vo = _mods()
+    from oracle import functions_oracle as fo
+    D, N = 601, 24
+    fam = _family(vb, kind, df, D)
+    ofam = vo.Family(kind, D, df)
+    obj = vb.black_box_klvi(fam, targets.mixture(D), N)
+    ofn = lambda lam: vo.klvi_value_grad(ofam, 'mixture', lam, N)
+    kw = dict(window=100, rhat_window=50, n_optimisers=2, tail_avg_iters=50)
+    res = vb.rmsprop_IA_optimize_with_rhat(100, obj, _lam(D, 9), D, **kw)
+    ores = fo.rmsprop_IA_optimize_with_rhat(100, ofn, _lam(D, 9), D, **kw)
+    _close(res[1], ores[1], 1e-7)
+    _close(res[4], ores[4], 1e-7)
+
+
 @pytest.mark.parametrize('kind,df', [('gauss', None), ('t', 40.0), ('t', 5.0)])
 @pytest.mark.parametrize('target,D', [('isogauss', 6), ('mixture', 2000), ('funnel', 10),
                                       ('funnel', 40), ('isogauss', 17)])
