@@ -179,6 +179,15 @@ __device__ __forceinline__ double log_unit_tab(double u, const double2* ltab) {
   return fma(de, 0.6931471805598903, fma(de, 5.497923018708371e-14, t.y + l1p));
 }
 
+// log1p(y) for finite y >= 0 (the t family's log(1 + z^2 / df)): u = 1 + y
+// rounded, log1p(y) = log(u) + (y - (u - 1)) / u, the correction (below one ulp
+// of u, relative to u) taken with the hardware reciprocal.
+__device__ __forceinline__ double log1p_pos_tab(double y, const double2* ltab) {
+  const double u = 1.0 + y;
+  const double corr = (y - (u - 1.0)) * __builtin_amdgcn_rcp(u);
+  return log_unit_tab(u, ltab) + corr;
+}
+
 // log(u) for u in (0, 1) (Box-Muller radius and acceptance uniforms, never 0):
 // u = m 2^e with m in [1/2, 1) and e <= 0, so e ln2, log c and log1p(r) never
 // cancel; c = 1/2 + j/256 the nearest table point, |r| <= 1/256, log1p to r^7.

@@ -555,8 +555,13 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
         const bool hasb = 2 * j + 1 < D;
         double lqp;
         if constexpr (TFAM) {
+#ifdef VB_NO_LQ_TAB
           lqp = a.t_const - log1p(ea * ea * inv_df) * lq_half;
           if (hasb) lqp += a.t_const - log1p(eb * eb * inv_df) * lq_half;
+#else
+          lqp = a.t_const - log1p_pos_tab(ea * ea * inv_df, s_lt) * lq_half;
+          if (hasb) lqp += a.t_const - log1p_pos_tab(eb * eb * inv_df, s_lt) * lq_half;
+#endif
         } else {
           lqp = -0.5 * ea * ea - 0.5 * kLog2Pi;
           if (hasb) lqp += -0.5 * eb * eb - 0.5 * kLog2Pi;
@@ -1065,30 +1070,39 @@ __global__ __launch_bounds__(256) void ia_update_kernel(int opt, long long P, do
 }
 
 // log weights lw[r] = log p(x_r) - log q(x_r; lam) for x_r ~ q   (experiments.py:60-63)
+// Philox draws use the LDS Box-Muller tables (sct, lt; loaded by the caller's
+// block) like the fused kernels.
 template <bool TFAM, bool HOST>
 __device__ __forceinline__ void draw_pair(const Rng& rng, const double* noise, int D, long long r,
                                           int j, uint32_t step, double t_scale, double shape,
-                                          double& eA, double& eB) {
+                                          double& eA, double& eB, const double2* sct,
+                                          const double2* lt) {
   const int dA = 2 * j, dB = 2 * j + 1;
   if constexpr (HOST) {
     eA = noise[r * D + dA];
     eB = dB < D ? noise[r * D + dB] : 0.0;
   } else {
-    normal_pair(rng.draw((uint32_t)j, (uint32_t)r, step, 0u), eA, eB);
+    normal_pair_tab(rng.draw((uint32_t)j, (uint32_t)r, step, 0u), eA, eB, sct, lt);
     if constexpr (TFAM) {
       double ga, gb;
-      gamma_pair(rng, (uint32_t)j, (uint32_t)r, step, shape, ga, gb);
+      gamma_pair<true>(rng, (uint32_t)j, (uint32_t)r, step, shape, ga, gb, sct, lt);
       eA = t_scale * eA / sqrt(ga);
       eB = t_scale * eB / sqrt(gb);
     }
   }
 }
 
-template <bool TFAM>
+template <bool TFAM, bool HOST>
 __device__ __forceinline__ double logq1(double x, double mu, double ls, double df,
-                                        double t_const) {
+                                        double t_const, const double2* lt) {
   const double z = (x - mu) / exp(ls);
-  if constexpr (TFAM) return t_const - log1p(z * z / df) * (0.5 * (df + 1.0)) - ls;
+  if constexpr (TFAM) {
+    const double y = z * z / df;
+    double l1;
+    if constexpr (HOST) l1 = log1p(y);
+    else l1 = log1p_pos_tab(y, lt);
+    return t_const - l1 * (0.5 * (df + 1.0)) - ls;
+  }
   return -0.5 * z * z - ls - 0.5 * kLog2Pi;
 }
 
@@ -1099,13 +1113,19 @@ __global__ __launch_bounds__(256) void logw_sep_kernel(int D, long long m, const
                                                        double t_const, const double* noise,
                                                        Rng rng, uint32_t step, double* lw,
                                                        double* xs) {
+  __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
+  __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
+  if constexpr (!HOST) {
+    load_bm_tables(s_sct, s_lt);
+    __syncthreads();
+  }
   const long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= m) return;
   const int lane = threadIdx.x & 63, npairs = (D + 1) / 2;
   double lp = 0.0, lq = 0.0;
   for (int j = lane; j < npairs; j += 64) {
     double e[2];
-    draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e[0], e[1]);
+    draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e[0], e[1], s_sct, s_lt);
     for (int c = 0; c < 2; ++c) {
       const int d = 2 * j + c;
       if (d < D) {
@@ -1113,7 +1133,7 @@ __global__ __launch_bounds__(256) void logw_sep_kernel(int D, long long m, const
         const double x = e[c] * exp(ls) + mu;
         double g;
         lp += TGT::lp1(x, g);
-        lq += logq1<TFAM>(x, mu, ls, df, t_const);
+        lq += logq1<TFAM, HOST>(x, mu, ls, df, t_const, s_lt);
         if (xs) xs[r * D + d] = x;
       }
     }
@@ -1130,6 +1150,12 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
                                                        double t_const, const double* noise,
                                                        Rng rng, uint32_t step, double* lw,
                                                        double* xs) {
+  __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
+  __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
+  if constexpr (!HOST) {
+    load_bm_tables(s_sct, s_lt);
+    __syncthreads();
+  }
   const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
   if (r >= m) return;
   double x[DMAX], g[DMAX];
@@ -1137,7 +1163,8 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
 #pragma unroll
   for (int j = 0; j < DMAX / 2; ++j) {
     double e0 = 0.0, e1 = 0.0;
-    if (2 * j < D) draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e0, e1);
+    if (2 * j < D)
+      draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e0, e1, s_sct, s_lt);
     const double e[2] = {e0, e1};
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -1147,7 +1174,7 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
       if (d < D) {
         const double mu = lam[d], ls = lam[D + d];
         x[d] = e[c] * exp(ls) + mu;
-        lq += logq1<TFAM>(x[d], mu, ls, df, t_const);
+        lq += logq1<TFAM, HOST>(x[d], mu, ls, df, t_const, s_lt);
         if (xs) xs[r * D + d] = x[d];
       }
     }
@@ -1343,6 +1370,18 @@ hipError_t launch_sample(int fam, int D, long long n, const double* lam, double 
 // thread.  Writes x, grad and the chunk partials logp[c n + r], logq[c n + r]
 // (with_lq); the consumer sums the mfw_rows_parts(D) partials of a row in
 // chunk order (deterministic).
+// log1p of the t family's log q term: LDS-table form when the Box-Muller tables
+// are loaded (Philox draws), the library log1p otherwise.
+template <bool HOST>
+__device__ __forceinline__ double lq1p(double y, const double2* ltab) {
+#ifdef VB_NO_LQ_TAB
+  return log1p(y);
+#else
+  if constexpr (HOST) return log1p(y);
+  else return log1p_pos_tab(y, ltab);
+#endif
+}
+
 constexpr int kRowChunkPairs = 256;
 constexpr int kRowsPerBlock = 4;  // 1, 2, 8: within 3 % (D = 1e4, N = 128)
 
@@ -1410,11 +1449,11 @@ __global__ __launch_bounds__(256) void mfw_rows_kernel(int D, long long n, const
       const double xA = eA * sA + muA, xB = eB * sB + muB;
       lp = TGT::lp1(xA, gA);
       const double zA = (xA - muA) * isA;
-      lq = TFAM ? cA - log1p(zA * zA * idf) * hexp : fma(-0.5 * zA, zA, cA);
+      lq = TFAM ? cA - lq1p<HOST>(zA * zA * idf, s_lt) * hexp : fma(-0.5 * zA, zA, cA);
       if (hasB) {
         lp += TGT::lp1(xB, gB);
         const double zB = (xB - muB) * isB;
-        lq += TFAM ? cB - log1p(zB * zB * idf) * hexp : fma(-0.5 * zB, zB, cB);
+        lq += TFAM ? cB - lq1p<HOST>(zB * zB * idf, s_lt) * hexp : fma(-0.5 * zB, zB, cB);
       }
       if (evenD) {  // 16-byte stores: the wave writes 1 KB of x and of grad contiguously
         *reinterpret_cast<double2*>(x + r * D + dA) = double2{xA, xB};
