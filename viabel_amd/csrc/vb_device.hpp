@@ -487,20 +487,24 @@ struct EightSchools {
   template <int DMAX>
   __device__ __forceinline__ static double row(const double* x, double* g, int /*D*/) {
     const double y[8] = {28., 8., -3., 7., -1., 1., 18., 12.};
-    const double sg[8] = {15., 10., 16., 11., 9., 11., 10., 18.};
+    // 1 / sigma_j rounded at compile time: multiplications instead of 24 fp64
+    // divisions per row (within an ulp of the divided forms)
+    constexpr double is[8] = {1. / 15., 1. / 10., 1. / 16., 1. / 11.,
+                              1. / 9.,  1. / 11., 1. / 10., 1. / 18.};
     const double mu = x[0], u = x[1], tau = exp(u);
-    const double t5 = tau / 5.0;
-    double lp = -0.5 * (mu / 5.0) * (mu / 5.0) - log1p(t5 * t5) + u;
-    double gmu = -mu / 25.0;
+    const double t5 = tau * 0.2, m5 = mu * 0.2;
+    double lp = -0.5 * m5 * m5 - log1p(t5 * t5) + u;
+    double gmu = -m5 * 0.2;
     double gu = -2.0 * t5 * t5 / (1.0 + t5 * t5) + 1.0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const double th = x[2 + j];
-      const double r = (y[j] - mu - tau * th) / sg[j];
+      const double r = (y[j] - mu - tau * th) * is[j];
+      const double rs = r * is[j];  // r / sigma_j
       lp += -0.5 * th * th - 0.5 * r * r;
-      gmu += r / sg[j];
-      gu += r * tau * th / sg[j];
-      g[2 + j] = -th + r * tau / sg[j];
+      gmu += rs;
+      gu += rs * (tau * th);
+      g[2 + j] = -th + rs * tau;
     }
     g[0] = gmu;
     g[1] = gu;
