@@ -33,6 +33,7 @@
  *                          foreign objective, or with avg_grad_norm)
  *   vb_log_weights         notebooks/experiments.py:60-63 (get_samples_and_log_weights)
  *   vb_divergence_bound    viabel/bounds.py:142-192 (divergence_bound, mean_and_check_mc_error)
+ *   vb_divergence_bound_rows viabel/bounds.py:142-192 (divergence_bound over many log-weight rows)
  *   vb_centered_moments    viabel/bounds.py:127-135 (wasserstein_bounds sample moments)
  *   vb_covariance          viabel/bounds.py:55-56 (np.cov(samples.T), ddof = 1)
  *   vb_weighted_covariance notebooks/experiments.py:83-85 (PSIS-weighted mean / np.cov)
@@ -264,6 +265,11 @@ int vb_log_weights(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,
  * out[5] = ELBO MC standard error (NaN when elbo supplied), out[6] = log max. */
 int vb_divergence_bound(vb_ctx* ctx, const double* lw, int64_t n, double alpha,
                         int32_t has_elbo, double elbo, double* out7);
+/* vb_divergence_bound for `rows` independent log-weight vectors of length n,
+ * row r at lw + r * ld (ld >= n), in one launch chain: out7 [rows][7] as above
+ * (row r's d_alpha, elbo, ...).  rows <= 65535. */
+int vb_divergence_bound_rows(vb_ctx* ctx, const double* lw, int64_t rows, int64_t n, int64_t ld,
+                             double alpha, int32_t has_elbo, double elbo, double* out7);
 /* c2 = mean_n sum_d (x - xbar)^2, c4 = mean_n sum_d (x - xbar)^4. */
 int vb_centered_moments(vb_ctx* ctx, const double* x, int64_t n, int64_t d,
                         double* c2, double* c4);

@@ -361,3 +361,32 @@ def test_psislw_many_columns_large_tail():
     _close(np.asarray(out), oout, rtol=1e-11, atol=1e-11)
     for t, ot in zip(tails, otails):
         np.testing.assert_array_equal(t, ot)
+
+
+@pytest.mark.parametrize('device', [False, True])
+def test_divergence_rows_matches_per_row(device):
+    """bounds.divergence_rows (one batched reduction chain over [rows, M]) equals
+    the single-row device divergence bit for bit, and the oracle to 1e-10."""
+    import torch
+    from viabel_amd import bounds
+    from oracle import bounds_oracle as bo
+    rs = np.random.RandomState(5)
+    rows, M = 7, 30_001
+    lw = rs.standard_t(5, size=(rows, M)) * 0.7 - 3.0
+    src = torch.from_numpy(lw).cuda() if device else lw
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        div = bounds.divergence_rows(src, alpha=2.0)
+        assert div.shape == (rows, 7)
+        for r in range(rows):
+            one = bounds._device_divergence(lw[r], 2.0, None)
+            np.testing.assert_array_equal(div[r], one)
+            d2, lnb = bo.divergence_bound(lw[r], return_log_norm_bound=True)
+            _close(div[r, 0], d2)
+            _close(div[r, 1], lnb)
+            res = bounds.all_bounds_from_divergence(div[r], moment_bound_fn=lambda p: 1.0 + p,
+                                                    q_var=2.0)
+            ref = bounds.all_bounds(lw[r], moment_bound_fn=lambda p: 1.0 + p, q_var=2.0)
+            assert res.keys() == ref.keys()
+            for k in ref:
+                assert res[k] == ref[k], k

@@ -98,6 +98,9 @@ _SIGNATURES = {
                         P(Noise), c_double_p, c_double_p], ctypes.c_int),
     'vb_divergence_bound': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_double,
                              ctypes.c_int32, ctypes.c_double, c_double_p], ctypes.c_int),
+    'vb_divergence_bound_rows': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,
+                                  ctypes.c_int64, ctypes.c_double, ctypes.c_int32, ctypes.c_double,
+                                  c_double_p], ctypes.c_int),
     'vb_centered_moments': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,
                              c_double_p, c_double_p], ctypes.c_int),
     'vb_covariance': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, c_double_p,

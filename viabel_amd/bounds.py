@@ -142,6 +142,45 @@ def divergence_bound(log_weights, alpha=2., log_norm_bound=None,
     return dalpha
 
 
+def divergence_rows(log_weights, alpha=2.):
+    """Device divergence statistics of every row of a [rows, M] log-weight matrix
+    (HBM tensor or array) in one launch chain: ndarray [rows, 7] of (d_alpha,
+    elbo, mean_r, se_r, mean_lw, se_lw, log max) per row, the values
+    `divergence_bound` derives its result and warnings from."""
+    if alpha <= 1:
+        raise ValueError('alpha must be greater than 1')
+    lw = nat.device_tensor(log_weights)
+    if lw is None:
+        lw = nat.as_f64(np.atleast_2d(np.asarray(log_weights, dtype=float)))
+        rows, n = lw.shape
+        ld = n
+    else:
+        if lw.dim() == 1:
+            lw = lw.reshape(1, -1)
+        rows, n = lw.shape
+        if lw.stride(1) != 1:
+            lw = lw.contiguous()
+        ld = lw.stride(0)
+    out = np.empty((rows, 7))
+    nat.check(nat.lib().vb_divergence_bound_rows(nat.context().handle, nat.dptr(lw), int(rows),
+                                                 int(n), int(ld), float(alpha), 0, 0.0,
+                                                 nat.dptr(out)))
+    return out
+
+
+def all_bounds_from_divergence(div7, moment_bound_fn, q_var=None, p_var=None):
+    """`all_bounds(log_weights, moment_bound_fn=..., q_var=...)` (bounds.py:13-61)
+    from one row of `divergence_rows` (same warnings, same dict)."""
+    d2, lnb, mean_r, se_r, mean_lw, se_lw = div7[:6]
+    _mc_warning(mean_r, se_r, 'CUBO')
+    _mc_warning(mean_lw, se_lw, 'ELBO')
+    results = wasserstein_bounds(d2, None, moment_bound_fn)
+    results.update(error_bounds(q_var=q_var, p_var=p_var, **results))
+    results['d2'] = d2
+    results['log_norm_bound'] = lnb
+    return results
+
+
 _var_bound_const_1 = 2 * np.sqrt(2)
 _var_bound_const_2 = 1 + 3 * np.sqrt(2)
 

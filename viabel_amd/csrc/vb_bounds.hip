@@ -19,6 +19,8 @@ namespace vbk {
 namespace {
 
 constexpr int kRedBlocks = 1024;
+// divergence scratch per log-weight row: partials [2 kRedBlocks], sc [4], m2 [2] (+ pad)
+constexpr long long kDivStride = 2 * kRedBlocks + 8;
 
 __device__ __forceinline__ double block_sum1(double v, double* red) {
   v = wave_sum(v);
@@ -47,8 +49,10 @@ int red_grid(long long n) {
 
 // pass 1: per-block max and sum of lw
 __global__ __launch_bounds__(256) void lw_max_sum_kernel(const double* lw, long long n,
-                                                         double* part) {
+                                                         double* part, long long ld) {
   __shared__ double red[4];
+  lw += (long long)blockIdx.y * ld;
+  part += (long long)blockIdx.y * kDivStride;
   double m = -INFINITY, s = 0.0;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256) {
@@ -68,6 +72,8 @@ __global__ __launch_bounds__(256) void lw_max_sum_kernel(const double* lw, long 
 __global__ __launch_bounds__(256) void lw_max_sum_final(const double* part, int nb, long long n,
                                                         double* sc) {
   __shared__ double red[4];
+  part += (long long)blockIdx.y * kDivStride;
+  sc += (long long)blockIdx.y * kDivStride;
   double m = -INFINITY, s = 0.0;
   for (int b = threadIdx.x; b < nb; b += 256) {
     m = fmax(m, part[2 * b]);
@@ -84,8 +90,11 @@ __global__ __launch_bounds__(256) void lw_max_sum_final(const double* part, int 
 // pass 2: sum of r = exp(lw - max)^alpha and of (lw - mean)^2
 __global__ __launch_bounds__(256) void lw_rescaled_kernel(const double* lw, long long n,
                                                           double alpha, const double* sc,
-                                                          double* part) {
+                                                          double* part, long long ld) {
   __shared__ double red[4];
+  lw += (long long)blockIdx.y * ld;
+  sc += (long long)blockIdx.y * kDivStride;
+  part += (long long)blockIdx.y * kDivStride;
   const double mx = sc[0], mean = sc[1];
   double s = 0.0, q = 0.0;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
@@ -120,11 +129,34 @@ __global__ __launch_bounds__(256) void sum2_final(const double* part, int nb, lo
   }
 }
 
+// sum2_final for the divergence rows (partials and result at the row's scratch)
+__global__ __launch_bounds__(256) void div_sum2_final(const double* part, int nb, long long n,
+                                                      double* out2) {
+  part += (long long)blockIdx.y * kDivStride;
+  out2 += (long long)blockIdx.y * kDivStride;
+  __shared__ double red[4];
+  double a = 0.0, b = 0.0;
+  for (int k = threadIdx.x; k < nb; k += 256) {
+    a += part[2 * k];
+    b += part[2 * k + 1];
+  }
+  a = block_sum1(a, red);
+  b = block_sum1(b, red);
+  if (threadIdx.x == 0) {
+    out2[0] = a / (double)n;
+    out2[1] = b / (double)n;
+  }
+}
+
 // pass 3: sum of (r - mean_r)^2
 __global__ __launch_bounds__(256) void lw_rdev_kernel(const double* lw, long long n, double alpha,
                                                       const double* sc, const double* m2,
-                                                      double* part) {
+                                                      double* part, long long ld) {
   __shared__ double red[4];
+  lw += (long long)blockIdx.y * ld;
+  sc += (long long)blockIdx.y * kDivStride;
+  m2 += (long long)blockIdx.y * kDivStride;
+  part += (long long)blockIdx.y * kDivStride;
   const double mx = sc[0], mr = m2[0];
   double q = 0.0;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
@@ -145,6 +177,10 @@ __global__ void divergence_final(const double* part, int nb, long long n, double
                                  int has_elbo, double elbo, const double* sc, const double* m2,
                                  double* out7) {
   __shared__ double red[4];
+  part += (long long)blockIdx.y * kDivStride;
+  sc += (long long)blockIdx.y * kDivStride;
+  m2 += (long long)blockIdx.y * kDivStride;
+  out7 += (long long)blockIdx.y * 7;
   double q = 0.0;
   for (int k = threadIdx.x; k < nb; k += 256) q += part[2 * k];
   q = block_sum1(q, red);
@@ -314,19 +350,31 @@ size_t bounds_scratch_doubles(long long n, long long d) {
 
 hipError_t bounds_divergence(const double* lw, long long n, double alpha, int has_elbo,
                              double elbo, double* scratch, double* out7, hipStream_t s) {
+  return bounds_divergence_rows(lw, 1, n, n, alpha, has_elbo, elbo, scratch, out7, s);
+}
+
+// rows independent log-weight vectors (row r at lw + r ld) in one launch chain:
+// every kernel takes its row from blockIdx.y, scratch kDivStride doubles per row
+hipError_t bounds_divergence_rows(const double* lw, long long rows, long long n, long long ld,
+                                  double alpha, int has_elbo, double elbo, double* scratch,
+                                  double* out7, hipStream_t s) {
+  if (rows < 1 || rows > 65535) return hipErrorInvalidValue;
   const int g = red_grid(n);
+  const unsigned R = (unsigned)rows;
   double* part = scratch;
   double* sc = scratch + 2 * kRedBlocks;
   double* m2 = sc + 4;
-  hipLaunchKernelGGL(lw_max_sum_kernel, dim3(g), dim3(256), 0, s, lw, n, part);
-  hipLaunchKernelGGL(lw_max_sum_final, dim3(1), dim3(256), 0, s, part, g, n, sc);
-  hipLaunchKernelGGL(lw_rescaled_kernel, dim3(g), dim3(256), 0, s, lw, n, alpha, sc, part);
-  hipLaunchKernelGGL(sum2_final, dim3(1), dim3(256), 0, s, part, g, n, m2);
-  hipLaunchKernelGGL(lw_rdev_kernel, dim3(g), dim3(256), 0, s, lw, n, alpha, sc, m2, part);
-  hipLaunchKernelGGL(divergence_final, dim3(1), dim3(256), 0, s, part, g, n, alpha, has_elbo, elbo,
-                     sc, m2, out7);
+  hipLaunchKernelGGL(lw_max_sum_kernel, dim3(g, R), dim3(256), 0, s, lw, n, part, ld);
+  hipLaunchKernelGGL(lw_max_sum_final, dim3(1, R), dim3(256), 0, s, part, g, n, sc);
+  hipLaunchKernelGGL(lw_rescaled_kernel, dim3(g, R), dim3(256), 0, s, lw, n, alpha, sc, part, ld);
+  hipLaunchKernelGGL(div_sum2_final, dim3(1, R), dim3(256), 0, s, part, g, n, m2);
+  hipLaunchKernelGGL(lw_rdev_kernel, dim3(g, R), dim3(256), 0, s, lw, n, alpha, sc, m2, part, ld);
+  hipLaunchKernelGGL(divergence_final, dim3(1, R), dim3(256), 0, s, part, g, n, alpha, has_elbo,
+                     elbo, sc, m2, out7);
   return hipGetLastError();
 }
+
+size_t bounds_divergence_scratch_doubles(long long rows) { return (size_t)(rows * kDivStride); }
 
 hipError_t bounds_centered_moments(const double* x, long long n, long long d, double* scratch,
                                    double* out2, hipStream_t s) {

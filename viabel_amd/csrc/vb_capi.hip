@@ -1131,6 +1131,24 @@ int vb_divergence_bound(vb_ctx* c, const double* lw, int64_t n, double alpha, in
   return sync(c);
 }
 
+int vb_divergence_bound_rows(vb_ctx* c, const double* lw, int64_t rows, int64_t n, int64_t ld,
+                             double alpha, int32_t has_elbo, double elbo, double* out7) {
+  VB_TRY(check_ctx(c));
+  if (!lw || !out7) return fail(VB_EINVAL, "null argument");
+  if (!(alpha > 1)) return fail(VB_EINVAL, "alpha must be greater than 1");  // bounds.py:166-167
+  if (n < 1) return fail(VB_EINVAL, "log_weights must be non-empty");
+  if (rows < 1 || rows > 65535 || ld < n) return fail(VB_EINVAL, "invalid rows / ld");
+  In dlw;
+  VB_TRY(dlw.stage(c, 0, lw, (size_t)((rows - 1) * ld + n)));
+  VB_TRY(c->slot[1].reserve(sizeof(double) * vbk::bounds_divergence_scratch_doubles(rows)));
+  Out o;
+  VB_TRY(o.stage(c, 2, out7, (size_t)rows * 7));
+  VB_HIP(vbk::bounds_divergence_rows(dlw.d, rows, n, ld, alpha, has_elbo, elbo, c->slot[1].d(),
+                                     o.d, c->stream));
+  VB_TRY(o.finish(c));
+  return sync(c);
+}
+
 int vb_centered_moments(vb_ctx* c, const double* x, int64_t n, int64_t d, double* c2,
                         double* c4) {
   VB_TRY(check_ctx(c));

@@ -122,6 +122,10 @@ hipError_t launch_iterate_average(const double* x, long long n, long long ld, lo
 // bounds
 hipError_t bounds_divergence(const double* lw, long long n, double alpha, int has_elbo,
                              double elbo, double* dev_scratch, double* out7_dev, hipStream_t s);
+hipError_t bounds_divergence_rows(const double* lw, long long rows, long long n, long long ld,
+                                  double alpha, int has_elbo, double elbo, double* scratch,
+                                  double* out7, hipStream_t s);
+size_t bounds_divergence_scratch_doubles(long long rows);
 hipError_t bounds_centered_moments(const double* x, long long n, long long d,
                                    double* dev_scratch, double* out2_dev, hipStream_t s);
 hipError_t bounds_covariance(const double* x, long long n, long long d, double* dev_scratch,

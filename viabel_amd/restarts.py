@@ -55,14 +55,21 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
     import torch
     lw = torch.empty((len(ids), int(n_bounds)), dtype=torch.float64,
                      device=torch.device('cuda', nat.context().device))
-    recs = []
+    bfams = []
     for j, r in enumerate(ids):
-        opt = smooth[j]
         bfam = family_factory()
         bfam.stream = (1 << 20) + r          # bound draws: a Philox stream of their own
-        experiments.log_weights(target, bfam, opt, n_bounds, return_samples=False, lw_out=lw[j])
-        res = bounds.all_bounds(lw[j], q_var=bfam.mean_and_cov(opt)[1],
-                                moment_bound_fn=lambda p: bfam.pth_moment(p, opt))
+        experiments.log_weights(target, bfam, smooth[j], n_bounds, return_samples=False,
+                                lw_out=lw[j])
+        bfams.append(bfam)
+    # the divergence statistics of all restarts in one batched reduction chain
+    div = bounds.divergence_rows(lw)
+    recs = []
+    for j, r in enumerate(ids):
+        opt, bfam = smooth[j], bfams[j]
+        res = bounds.all_bounds_from_divergence(
+            div[j], moment_bound_fn=lambda p, bfam=bfam, opt=opt: bfam.pth_moment(p, opt),
+            q_var=bfam.mean_and_cov(opt)[1])
         elbo = float(res['log_norm_bound'])  # = mean log weight (bounds.py:170-172)
         recs.append([r, elbo, res['d2'], res['W1'], res['W2'], res['mean_error'],
                      res['std_error'], res['cov_error']])
