@@ -613,6 +613,14 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
     double mloc = -INFINITY;  // CHIVI: running max of this thread's log weights
+    // overlapped draws: items [0, cut_a) of step s + 1 are drawn while the rows
+    // consume step s, the rest during the update (see below)
+#ifdef VB_NO_DRAW_SPLIT
+    const int cut_a = N * NP;
+#else
+    const int d_lanes = NT - RT, d_rounds = (N * NP + d_lanes - 1) / max(d_lanes, 1);
+    const int cut_a = d_rounds >= 2 ? (d_rounds - 1) * d_lanes : N * NP;
+#endif
     VB_PH(0);
 
     auto row_of = [&](const double* e, double lqs) {
@@ -693,7 +701,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
         if (rows)
           consume(cur, 0, N);
         else if (s + 1 < a.n_steps)
-          draw_item(tid - RT, NT - RT, N * NP, 0, ri + 1, nxt);
+          draw_item(tid - RT, NT - RT, cut_a, 0, ri + 1, nxt);
         VB_PH(2);
       } else {
         const int CH = kBlockDrawLds / R;  // samples per draw chunk
@@ -800,6 +808,14 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
         val = log(s_red[0][2 * DMAX] / dN) / a.alpha + M;
       }
       a.values[(long long)prob * a.n_iters + (a.emit_grad ? 0 : i)] = val;
+    }
+    if constexpr (!HOST) {
+      // the draw waves' last item round of step s + 1 runs here, beside the
+      // update (one row wave's P threads), instead of lengthening the
+      // consume phase they already bound
+      if (L.pipe && !rows && cut_a < N * NP && s + 1 < a.n_steps)
+        draw_item(cut_a + tid - RT, NT - RT, N * NP, 0, ri + 1,
+                  s_e + ((s + 1) & 1) * (kBlockDrawLds / 2));
     }
     VB_PH(5);
     slot = slot + 1 == W ? 0 : slot + 1;
