@@ -380,17 +380,39 @@ void sep_kernel(SepArgs a) {
   }
 }
 
-// values[i] = -(c0 + sum_w vpart[s][w]), fixed-order tree reduction.
-__global__ __launch_bounds__(256) void sep_values_kernel(const double* vpart, int n_waves,
-                                                         double c0, double* values) {
-  __shared__ double red[4];
-  const int s = blockIdx.x;
-  double acc = 0.0;
-  for (int w = threadIdx.x; w < n_waves; w += 256) acc += vpart[(long long)s * n_waves + w];
-  acc = wave_sum(acc);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+// values[i] = -(c0 + sum_w vpart[s][w]), fixed-order tree reduction.  One
+// 1024-thread block per step; each thread issues kValU independent loads per
+// round (one round covers 4 096 pairs, D = 1e4 needs two), so the block waits
+// on ~2 load latencies instead of a dependent chain of n_waves / 256.
+constexpr int kValThreads = 1024, kValU = 4;
+__global__ __launch_bounds__(kValThreads) void sep_values_kernel(const double* vpart,
+                                                                 int n_waves, double c0,
+                                                                 double* values) {
+  __shared__ double red[kValThreads / 64];
+  const double* row = vpart + (long long)blockIdx.x * n_waves;
+  double acc[kValU];
+#pragma unroll
+  for (int u = 0; u < kValU; ++u) acc[u] = 0.0;
+  for (int base = threadIdx.x; base < n_waves; base += kValU * kValThreads) {
+    double v[kValU];
+#pragma unroll
+    for (int u = 0; u < kValU; ++u) {
+      const int w = base + u * kValThreads;
+      v[u] = w < n_waves ? row[w] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kValU; ++u) acc[u] += v[u];
+  }
+  double t = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  t = wave_sum(t);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
   __syncthreads();
-  if (threadIdx.x == 0) values[s] = -(c0 + ((red[0] + red[1]) + (red[2] + red[3])));
+  if (threadIdx.x == 0) {
+    double r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = (red[4 * j] + red[4 * j + 1]) + (red[4 * j + 2] + red[4 * j + 3]);
+    values[blockIdx.x] = -(c0 + ((r[0] + r[1]) + (r[2] + r[3])));
+  }
 }
 
 // out[q][p] = mean_r hist[q][r][p]; sequential over r like numpy's axis-0 reduce.
@@ -1343,8 +1365,8 @@ hipError_t launch_block(int fam, int tgt, bool host, const BlockArgs& a, int npr
 
 hipError_t launch_sep_values(const double* vpart, int n_steps, int n_waves, double c0,
                              double* values, hipStream_t s) {
-  hipLaunchKernelGGL(sep_values_kernel, dim3(n_steps), dim3(256), 0, s, vpart, n_waves, c0,
-                     values);
+  hipLaunchKernelGGL(sep_values_kernel, dim3(n_steps), dim3(kValThreads), 0, s, vpart, n_waves,
+                     c0, values);
   return hipGetLastError();
 }
 

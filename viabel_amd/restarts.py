@@ -14,11 +14,14 @@ Summary record (float64), per restart:
   [restart id, ELBO estimate (mean log weight), CUBO-based d2, W1, W2,
    mean_error, std_error, cov_error, k_hat, final objective value, lambda*(P)]
 """
+import os
+import time
+
 import numpy as np
 
 from . import _native as nat
 
-__all__ = ['shard', 'run_restarts', 'gather_records', 'RECORD_HEAD']
+__all__ = ['shard', 'run_restarts', 'gather_records', 'bind_local_device', 'RECORD_HEAD']
 
 RECORD_HEAD = ['restart', 'elbo', 'd2', 'W1', 'W2', 'mean_error', 'std_error', 'cov_error',
                'khat', 'final_value']
@@ -36,18 +39,45 @@ def default_inits(n_restarts, P, scale=0.5, base=None):
     return np.stack([base + np.random.RandomState(r).randn(P) * scale for r in range(n_restarts)])
 
 
+def bind_local_device(rank=0):
+    """Select this rank's GPU before any allocation: LOCAL_RANK (set by
+    torchrun) or the global rank, modulo the visible device count.  The vb
+    context (nat.set_device) and torch's current device (used by the NCCL
+    all_gather) then name the same GPU."""
+    import torch
+    n = torch.cuda.device_count()
+    if n == 0:
+        raise RuntimeError('run_restarts: no GPU visible to rank %d' % rank)
+    dev = int(os.environ.get('LOCAL_RANK', rank)) % n
+    torch.cuda.set_device(dev)
+    nat.set_device(dev)
+    return dev
+
+
+def _sync():
+    nat.context().synchronize()
+
+
 def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bounds,
-                    learning_rate, learning_rate_end, window, seed, stream_base, stride):
+                    learning_rate, learning_rate_end, window, seed, stream_base, stride,
+                    timings=None):
     """Fit this rank's restarts in ONE device run (one workgroup per restart;
     restart r draws from Philox stream 1 + r whatever the sharding) and
-    summarise each with device log weights, bounds and PSIS."""
+    summarise each with device log weights, bounds and PSIS.  `timings`, if a
+    dict, receives the seconds of the fitting and of the bounds/PSIS stage."""
     from . import vb, bounds, psis, experiments
     fam = family_factory()
+    if fam.rng != 'philox':
+        raise ValueError("run_restarts needs a family_factory with rng='philox' (restart r "
+                         "draws from its own Philox stream; a numpy-stream family would give "
+                         "every restart the same RandomState(0) noise)")
+    t0 = time.perf_counter()
     obj = vb.black_box_klvi(fam, target, n_samples)
     run = vb.DeviceRun(obj, n_iters, inits, window=window, learning_rate=learning_rate,
                        learning_rate_end=learning_rate_end)
     run.advance_philox(n_iters, seed, stream_base, 0, stream_stride=stride)
     _, _, vals, smooth = run.result()
+    t1 = time.perf_counter()
     # the M log weights of every restart stay in HBM from the draws through the
     # bounds and PSIS: row j of one [restarts][M] buffer; PSIS then runs all
     # restarts' columns in one batched pipeline (the buffer's transpose is the
@@ -74,6 +104,11 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
         recs.append([r, elbo, res['d2'], res['W1'], res['W2'], res['mean_error'],
                      res['std_error'], res['cov_error']])
     khat = psis.psislw(lw.t())[1] if len(ids) > 1 else np.array([psis.psislw(lw[0])[1]])
+    if timings is not None:
+        _sync()
+        t2 = time.perf_counter()
+        timings['fit_s'] = t1 - t0
+        timings['bounds_psis_s'] = t2 - t1
     return np.array([np.concatenate([rec, [khat[j], vals[j, -1]], smooth[j]])
                      for j, rec in enumerate(recs)])
 
@@ -99,13 +134,16 @@ def gather_records(local, n_restarts, width, group=None):
 
 def run_restarts(family_factory, target, n_restarts, n_iters, n_samples=100, n_bounds=1_000_000,
                  learning_rate=.01, learning_rate_end=.001, window=10, inits=None, seed=0,
-                 group=None, compute=None):
+                 group=None, compute=None, timings=None):
     """Fit n_restarts KLVI restarts sharded over the ranks of `group` (or this
     process alone when torch.distributed is not initialised) and return the
     gathered summary table (RECORD_HEAD + lambda*) on every rank.
 
     `compute(ids, inits) -> records` replaces the device computation (tests use
-    it to run the sharding and the collective without a GPU)."""
+    it to run the sharding and the collective without a GPU).  With the device
+    computation under torch.distributed, each rank first binds its own GPU
+    (bind_local_device).  `timings` (a dict) receives this rank's fit and
+    bounds/PSIS stage seconds."""
     try:
         import torch.distributed as dist
         dist_on = dist.is_available() and dist.is_initialized()
@@ -116,12 +154,14 @@ def run_restarts(family_factory, target, n_restarts, n_iters, n_samples=100, n_b
     P = fam0.var_param_dim
     if inits is None:
         inits = default_inits(n_restarts, P)
+    if compute is None and dist_on:
+        bind_local_device(rank)
     ids = shard(n_restarts, rank, world)
     local_inits = np.asarray(inits)[ids] if ids else np.zeros((0, P))
     if compute is None:
         local = (_native_compute(ids, local_inits, family_factory, target, n_iters, n_samples,
                                  n_bounds, learning_rate, learning_rate_end, window, seed,
-                                 1 + rank, world)
+                                 1 + rank, world, timings)
                  if ids else np.zeros((0, len(RECORD_HEAD) + P)))
     else:
         local = compute(ids, local_inits)

@@ -400,9 +400,17 @@ class DeviceRun:
         self.done = 0
 
     def advance_philox(self, n_steps, seed, stream, step, stream_stride=1):
-        """Problem q draws from Philox stream `stream + q * stream_stride`."""
-        nz = nat.Noise(nat.NOISE_PHILOX, stream & 0xFFFFFF, seed, step, None, stream_stride)
-        nat.check(nat.lib().vb_run_advance(self.handle, int(n_steps), nz))
+        """Problem q draws from Philox stream `stream + q * stream_stride`.
+        The noise descriptor is reused across calls (short runs are host-bound)."""
+        nz = self.__dict__.get('_nz')
+        if nz is None:
+            nz = self._nz = nat.Noise(nat.NOISE_PHILOX, 0, 0, 0, None, 1)
+            self._advance = nat.lib().vb_run_advance
+        nz.stream = stream & 0xFFFFFF
+        nz.seed = seed
+        nz.step = step
+        nz.stream_stride = stream_stride
+        nat.check(self._advance(self.handle, int(n_steps), nz))
         self.done += int(n_steps)
 
     def advance_host(self, eps):
