@@ -329,8 +329,7 @@ int fr_objective(vb_ctx* c, const FamInfo& fi, const vb_target* tgt, const vb_ob
   VB_HIP(hipMemcpyAsync(value, c->slot[4].p, sizeof(double), hipMemcpyDefault, c->stream));
   VB_TRY(dg.finish(c));
   VB_TRY(sync(c));
-  if (int info = vbk::fr_info(W, c->stream))
-    return fail(VB_EDEVICE, "eigendecomposition of Sigma did not converge (info %d)", info);
+  if (int rc = vbk::fr_info(W, c->stream)) return rc;
   return VB_OK;
 }
 
@@ -493,8 +492,7 @@ int vb_family_moments(vb_ctx* c, const vb_family* fam, const double* lam, double
   VB_TRY(de.finish(c));
   VB_TRY(sync(c));
   if (eig_out) {
-    if (int info = vbk::fr_info(W, c->stream))
-      return fail(VB_EDEVICE, "eigendecomposition of Sigma did not converge (info %d)", info);
+    if (int rc = vbk::fr_info(W, c->stream)) return rc;
   }
   return VB_OK;
 }
@@ -815,7 +813,8 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
           VB_TRY(vbk::fr_value_grad(W, r->spec, lam, eps, k0, k1,
                                     noise->stream + (uint32_t)q * stride,
                                     (uint32_t)(noise->step + off),
-                                    r->values.d() + q * r->n_iters + step, r->grad.d(), c->stream));
+                                    r->values.d() + q * r->n_iters + step, r->grad.d(), c->stream,
+                                    r->nprob == 1 && step > 0));
         double* hrow = step >= r->hist_start
                            ? r->hist.d() + (q * r->n_hist + (step - r->hist_start)) * P
                            : nullptr;
@@ -924,8 +923,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
     VB_TRY(sync(c));
     vbk::FrWork* W;
     VB_TRY(fr_work(c, &W));
-    if (int info = vbk::fr_info(W, c->stream))
-      return fail(VB_EDEVICE, "eigendecomposition of Sigma did not converge (info %d)", info);
+    if (int rc = vbk::fr_info(W, c->stream)) return rc;
     return VB_OK;
   }
   // host noise staging buffer is reused by the next call: finish before returning

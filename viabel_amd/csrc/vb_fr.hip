@@ -8,7 +8,7 @@
 //
 // One step, GEMMs only (fp64 MFMA, vb_gemm.hpp), no eigendecomposition:
 //   L <- unpack(lambda);  Sigma <- L L^T;  0.5 log det Sigma = sum log L_ii
-//   S = sqrtm(Sigma) by coupled Newton-Schulz on Sigma / ||Sigma||_F (fr_sqrt)
+//   S = sqrtm(Sigma) by scaled coupled Newton-Schulz on Sigma / c (fr_sqrt)
 //   X = mu + (Z S) / s                           (vb.py:208, fused epilogue)
 //   G = d log p / dx, log p                      (corr_gauss: G = -X P*, GEMM)
 //   KLVI : r_n = -1/N,            c = -1/2       (entropy .5 log det Sigma)
@@ -16,10 +16,12 @@
 //          Mahalanobis term is invariant under the reparameterisation)
 //   G_S = Z^T diag(r / s) G                       (cotangent of S)
 //   autograd's sqrtm VJP solves S X + X S = G_S (solve_sylvester); Sigma = L L^T
-//   only needs the symmetric part, so X_sym solves S X + X S = G_S + G_S^T,
-//   computed as the forward-mode tangent of the same Newton-Schulz iteration
-//   (fr_sylvester).  H = X_sym + 2 c Sigma^-1 (Sigma^-1 = Z_K^2 / ||Sigma||_F);
-//   G_L = H L;  grad = [sum r G, tril(G_L) with the diagonal times L_ii].
+//   only needs the symmetric part, so X_sym solves S X + X S = G_S + G_S^T, by
+//   preconditioned conjugate gradients (fr_pcg).  H = X_sym + 2 c Sigma^-1;
+//   G_L = H L;  grad = [sum r G, tril(G_L) with the diagonal times L_ii], where
+//   the Sigma^-1 term reduces to 2 c on the packed log-diagonal.
+// No host synchronisation inside a step: scalars (scales, step sizes,
+// convergence flags) live on the device (FrSched); fr_info reads the status.
 // The eigendecomposition (rocSOLVER dsyevd) remains only for log q of arbitrary
 // points (multivariate_t_logpdf's pinv cutoff) and the eigenvalues of
 // mean_and_cov / pth_moment, off the optimisation loop.
@@ -223,15 +225,32 @@ __global__ __launch_bounds__(256) void fr_colsum_kernel(int N, int D, const doub
   if (wv == 0 && j < D) out[j] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
 }
 
-// grad[D + i(i+1)/2 + j] = G_L[i][j] (j < i), G_L[i][i] * L[i][i] (exp on the diagonal)
+// grad[D + i(i+1)/2 + j] = G_L[i][j] (j < i), G_L[i][i] L[i][i] + 2 scal[1] (exp on
+// the diagonal; the log det term, see fr_value_grad).  Thread 0 also folds this
+// step's Newton-Schulz / PCG outcome into the sticky status (FrSched).
+template <class Sched>
 __global__ __launch_bounds__(256) void fr_pack_kernel(int D, const double* GL, const double* L,
+                                                      const double* scal, Sched* sc,
+                                                      const double* rr_part, int n_rr,
                                                       double* grad) {
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx == 0) {
+    if (!sc->ns_conv) sc->status |= 1;
+    if (!sc->pcg_done) {
+      double rr = 0.0;
+      for (int k = 0; k < n_rr; ++k) rr += rr_part[k];
+      if (!(rr <= 1e-14 * sc->ee)) sc->status |= 2;  // relative residual above 1e-7
+    }
+    if (sc->warm_step) {
+      sc->hint_ns = max(sc->hint_ns, sc->ns_iter);
+      sc->hint_pcg = max(sc->hint_pcg, sc->pcg_iter);
+    }
+  }
   if (idx >= (long long)D * D) return;
   const int i = (int)(idx / D), j = (int)(idx % D);
   if (j > i) return;
   double v = GL[idx];
-  if (j == i) v *= L[idx];
+  if (j == i) v = fma(v, L[idx], 2.0 * scal[1]);
   grad[D + (long long)i * (i + 1) / 2 + j] = v;
 }
 
@@ -343,42 +362,241 @@ __global__ __launch_bounds__(256) void fr_norm2_kernel(int n, const double* x, d
   if (threadIdx.x == 0) *out = a;
 }
 
-// Y0 = Sigma / c, Z0 = I.  The coupled Newton-Schulz iteration converges for
-// eigenvalues of Sigma / c in (0, 3) (p -> p (3 - p)^2 / 4), fastest when the
-// largest is near 1: c = 1.25 x the power-iteration estimate of lambda_max
-// (which is <= lambda_max), capped by ||Sigma||_F (>= lambda_max).
-__global__ __launch_bounds__(256) void fr_ns_init_kernel(int D, const double* Sig,
-                                                         const double* nrm2, double* Y0,
-                                                         double* Z0, double* cout) {
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)D * D) return;
-  const double c = fmin(1.25 * sqrt(nrm2[1]), sqrt(nrm2[0]));
-  Y0[idx] = Sig[idx] / c;
-  Z0[idx] = (idx % (D + 1) == 0) ? 1.0 : 0.0;
-  if (idx == 0) *cout = c;
+// ---- Newton-Schulz schedule (device) -------------------------------------------
+// Coupled scaled Newton-Schulz on A = Sigma / c (Higham, Functions of Matrices
+// §6.3, with the Chen-Chow scaling): for k >= 0
+//   T_k = 3 I - a_k^2 Z_k Y_k,  Y_{k+1} = a_k Y_k T_k / 2,  Z_{k+1} = a_k T_k Z_k / 2,
+//   Y_0 = A, Z_0 = I.  Eigenvalue-wise x = sqrt(p), p of Z_k Y_k:
+//   x' = a x (3 - a^2 x^2) / 2 with a = sqrt(3 / (1 + l + l^2)) maps [l, 1] into
+//   [f(l), 1], so the lower bound l_k of x sets every a_k; a_k -> 1 as l_k -> 1.
+//   Y_k -> A^(1/2), Z_k -> A^(-1/2).
+// Scalars (FrSched, device): c = min(1.25 x power estimate of lambda_max,
+// ||Sigma||_F); l_0 = 0.8 sqrt(lambda_min / c) with lambda_min from the previous
+// root (||Z_prev||_2 by power iteration: lambda_min = c_prev / ||Z_prev||^2), or
+// l_default without one.  A low l_0 costs iterations, never accuracy: the
+// iteration is declared converged from the residual ||I - Z_k Y_k||_F alone.
+struct FrSched {
+  double c, sqrt_c, inv_sqrt_c, c_prev;
+  double ns0[4];                 // iteration 0 coefficients (GemmOp::ns0)
+  double nalpha2[kFrNSMax + 1];  // -a_k^2 (T_k GEMM alpha)
+  double shift[kFrNSMax + 1];    // 3 - a_k^2 (residual shift of T_k)
+  double halpha[kFrNSMax + 1];   // a_k / 2
+  double inv_a4[kFrNSMax + 1];   // 1 / a_k^4 (residual scale)
+  double rz[2], ee;              // PCG: <R, M^-1 R> (by iteration parity), ||E||^2
+  double l0, lmax_est;
+  int ns_conv, ns_iter, pcg_done, pcg_iter;
+  int status;                    // sticky: 1 NS not converged, 2 PCG not converged
+  int hint_ns, hint_pcg;         // sticky maxima of the iteration counts
+  int warm_step;                 // this root was warm-started (its count feeds hint_ns)
+};
+
+// y = M x / ||x|| for (Sigma, x) in grid row 0 and (Z_prev, u) in grid row 1
+// (8 rows per block, two per wave).  x null: x = ones.
+__global__ __launch_bounds__(256) void fr_power2_kernel(int D, const double* Sig, const double* x,
+                                                        double* y, const double* Zp,
+                                                        const double* u, double* v) {
+  __shared__ double red[16];
+  __shared__ double inv_n;
+  const double* M = blockIdx.y ? Zp : Sig;
+  const double* in = blockIdx.y ? u : x;
+  double* out = blockIdx.y ? v : y;
+  double a = 0.0;
+  for (int i = threadIdx.x; i < D; i += 256) {
+    const double t = in ? in[i] : 1.0;
+    a += t * t;
+  }
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) inv_n = 1.0 / sqrt(a);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int rr = 0; rr < 2; ++rr) {
+    const int row = blockIdx.x * 8 + wv * 2 + rr;
+    if (row >= D) break;
+    double t = 0.0;
+    for (int j = lane; j < D; j += 64) t += M[(long long)row * D + j] * (in ? in[j] : 1.0);
+    t = wave_sum(t);
+    if (lane == 0) out[row] = t * inv_n;
+  }
 }
 
-// dY0 = (G + G^T) / c   (symmetric part of the S cotangent, scaled like Sigma)
-__global__ __launch_bounds__(256) void fr_symscale_kernel(int D, const double* G,
-                                                          const double* cdev, double* out) {
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)D * D) return;
-  const int i = (int)(idx / D), j = (int)(idx % D);
-  out[idx] = (G[idx] + G[(long long)j * D + i]) / *cdev;
+__device__ double ns_alpha(double l) { return sqrt(3.0 / (1.0 + l + l * l)); }
+
+// One block: c, l_0 and the whole schedule; resets the per-step flags.
+__global__ __launch_bounds__(256) void fr_sched_kernel(int D, int kmax, const double* fro_part,
+                                                       int n_part, const double* y,
+                                                       const double* v, int has_z,
+                                                       double l_default, FrSched* sc) {
+  __shared__ double red[16];
+  double f = 0.0, ly = 0.0, lv = 0.0;
+  for (int i = threadIdx.x; i < n_part; i += 256) f += fro_part[i];
+  for (int i = threadIdx.x; i < D; i += 256) {
+    ly += y[i] * y[i];
+    if (has_z) lv += v[i] * v[i];
+  }
+  f = block_sum(f, red);
+  __syncthreads();
+  ly = block_sum(ly, red);
+  __syncthreads();
+  lv = block_sum(lv, red);
+  if (threadIdx.x != 0) return;
+  const double lmax = sqrt(ly);                  // ||Sigma x|| for unit x <= lambda_max
+  const double c = fmin(1.25 * lmax, sqrt(f));   // ||Sigma||_F >= lambda_max
+  double l = l_default;
+  if (has_z && lv > 0.0) {
+    const double lmin = sc->c_prev / lv;        // lambda_min(Sigma_prev)
+    l = 0.8 * sqrt(lmin / c);
+  }
+  l = fmin(fmax(l, 1e-4), 1.0);
+  sc->l0 = l;
+  sc->lmax_est = lmax;
+  sc->c = c;
+  sc->sqrt_c = sqrt(c);
+  sc->inv_sqrt_c = 1.0 / sqrt(c);
+  sc->c_prev = c;
+  for (int k = 0; k <= kmax && k <= kFrNSMax; ++k) {
+    const double a = ns_alpha(l), a2 = a * a;
+    if (k == 0) {
+      // Y_1 = (3/2) a A - (1/2) a^3 A^2, Z_1 = (a / 2) (3 I - a^2 A), A = Sigma / c
+      sc->ns0[0] = -0.5 * a * a2 / (c * c);
+      sc->ns0[1] = 1.5 * a / c;
+      sc->ns0[2] = 0.5 * a;
+      sc->ns0[3] = a2 / c;
+    }
+    sc->nalpha2[k] = -a2;
+    sc->shift[k] = 3.0 - a2;
+    sc->halpha[k] = 0.5 * a;
+    sc->inv_a4[k] = 1.0 / (a2 * a2);
+    l = fmin(0.5 * a * l * (3.0 - a2 * l * l), 1.0);
+  }
+  sc->ns_conv = 0;
+  sc->ns_iter = -1;
+  sc->warm_step = has_z;
+  sc->pcg_done = 0;
+  sc->pcg_iter = -1;
 }
 
-__global__ __launch_bounds__(256) void fr_axpby_kernel(long long n, double a, const double* X,
-                                                       double* Y) {
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx < n) Y[idx] = a * X[idx];
+// ---- PCG for the sqrtm VJP ----------------------------------------------------
+// autograd's sqrtm VJP solves S X + X S = G_S (solve_sylvester); Sigma = L L^T
+// needs only the symmetric part: S X + X S = E, E = G_S + G_S^T.  In the scaled
+// variables Y = A^(1/2) = S / sqrt(c), Z = Y^-1: Y X + X Y = E / sqrt(c) =: Eh.
+// The operator L(X) = Y X + X Y is SPD on symmetric matrices (Frobenius inner
+// product); the preconditioner M^-1(R) = (Z R + R Z) / 4 has eigenvalues
+// (1/4)(1/y_i + 1/y_j) against L's (y_i + y_j), so the preconditioned spectrum
+// lies in [1, (2 + k + 1/k) / 4] for k = cond(Y) (1.17 at config 4): conjugate
+// gradients reach 1e-11 in ~7 iterations, two GEMMs each (Y P and Z R; the
+// transposes of the symmetric products are read by the update kernels).
+// Inner products ride in GEMM epilogues (<P, Y P> = <P, L(P)> / 2, <R, Z R> =
+// 2 <R, M^-1 R>) and in the update kernels, as per-block partials that every
+// consumer block sums in the same order (no atomics).
+constexpr int kTile = 32;
+
+// 32 x 32 tile (bi, bj) of M and of M^T through LDS: thread t owns 4 elements.
+struct TileT {
+  __device__ static void load_t(const double* M, int D, int bi, int bj, double (*s)[kTile + 1]) {
+    for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
+      const int r = e / kTile, cc = e % kTile;
+      const int gr = bj * kTile + r, gc = bi * kTile + cc;
+      s[r][cc] = (gr < D && gc < D) ? M[(long long)gr * D + gc] : 0.0;
+    }
+    __syncthreads();
+  }
+};
+
+// Sum of n per-block partials by the whole (256-thread) block, in a fixed
+// order: every block of a grid gets the bitwise-identical total.
+__device__ double sum_parts(const double* p, int n, double* red) {
+  double a = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) a += p[i];
+  return block_sum(a, red);
 }
 
-// H = sqrt(c) dY + 2 coef Sigma^-1   (coef = scal[1], Sigma^-1 = Z_K^2 / c)
-__global__ __launch_bounds__(256) void fr_h_kernel(long long n, double sc, const double* dY,
-                                                   const double* SigInv, const double* scal,
-                                                   double* H) {
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx < n) H[idx] = sc * dY[idx] + 2.0 * scal[1] * SigInv[idx];
+// Eh = (G + G^T) / sqrt(c), R = Eh, X = 0, ee partials
+__global__ __launch_bounds__(256) void pcg_init_kernel(int D, const double* G, const FrSched* sc,
+                                                       double* Eh, double* R, double* X,
+                                                       double* ee_part) {
+  __shared__ double s[kTile][kTile + 1];
+  __shared__ double red[16];
+  const int bi = blockIdx.y, bj = blockIdx.x;
+  TileT::load_t(G, D, bi, bj, s);
+  const double isc = sc->inv_sqrt_c;
+  double a = 0.0;
+  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
+    const int r = e / kTile, cc = e % kTile;
+    const int i = bi * kTile + r, j = bj * kTile + cc;
+    if (i < D && j < D) {
+      const long long idx = (long long)i * D + j;
+      const double v = (G[idx] + s[cc][r]) * isc;
+      Eh[idx] = v;
+      R[idx] = v;
+      X[idx] = 0.0;
+      a += v * v;
+    }
+  }
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) ee_part[blockIdx.y * gridDim.x + blockIdx.x] = a;
+}
+
+// X += alpha P, R -= alpha (C + C^T), rr partials;  alpha = rz / <P, L(P)>,
+// <P, L(P)> = 2 sum(pq_part)
+__global__ __launch_bounds__(256) void pcg_xr_kernel(int D, int it, const double* C,
+                                                     const double* P, const double* pq_part,
+                                                     int n_pq, FrSched* sc, double* X, double* R,
+                                                     double* rr_part) {
+  __shared__ double s[kTile][kTile + 1];
+  __shared__ double red[16];
+  if (sc->pcg_done) return;
+  const double alpha = sc->rz[it & 1] / (2.0 * sum_parts(pq_part, n_pq, red));
+  __syncthreads();
+  const int bi = blockIdx.y, bj = blockIdx.x;
+  TileT::load_t(C, D, bi, bj, s);
+  double a = 0.0;
+  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
+    const int r = e / kTile, cc = e % kTile;
+    const int i = bi * kTile + r, j = bj * kTile + cc;
+    if (i < D && j < D) {
+      const long long idx = (long long)i * D + j;
+      X[idx] = fma(alpha, P[idx], X[idx]);
+      const double rn = R[idx] - alpha * (C[idx] + s[cc][r]);
+      R[idx] = rn;
+      a += rn * rn;
+    }
+  }
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) rr_part[blockIdx.y * gridDim.x + blockIdx.x] = a;
+}
+
+// P = (C + C^T) / 4 + beta P with <R, M^-1 R> = sum(rz_part) / 2 and
+// beta = <R, M^-1 R> / rz_prev (it < 0: the initial P, beta = 0; block 0 also
+// stores ||E||^2).  Block 0 records the new rz for the next iteration.
+__global__ __launch_bounds__(256) void pcg_p_kernel(int D, int it, const double* C,
+                                                    const double* rz_part, int n_rz,
+                                                    const double* ee_part, int n_ee, FrSched* sc,
+                                                    double* P) {
+  __shared__ double s[kTile][kTile + 1];
+  __shared__ double red[16];
+  if (sc->pcg_done) return;
+  const double rz = 0.5 * sum_parts(rz_part, n_rz, red);
+  const double beta = it < 0 ? 0.0 : rz / sc->rz[it & 1];
+  double ee = 0.0;
+  if (it < 0) {
+    __syncthreads();
+    ee = sum_parts(ee_part, n_ee, red);
+  }
+  const int bi = blockIdx.y, bj = blockIdx.x;
+  TileT::load_t(C, D, bi, bj, s);
+  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
+    const int r = e / kTile, cc = e % kTile;
+    const int i = bi * kTile + r, j = bj * kTile + cc;
+    if (i < D && j < D) {
+      const long long idx = (long long)i * D + j;
+      const double z = 0.25 * (C[idx] + s[cc][r]);
+      P[idx] = it < 0 ? z : fma(beta, P[idx], z);
+    }
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    sc->rz[(it + 1) & 1] = rz;
+    if (it < 0) sc->ee = ee;
+  }
 }
 
 }  // namespace
@@ -402,20 +620,24 @@ struct FrWork {
       if (p) (void)hipFree(p);
     }
   };
-  static constexpr int kNSMax = 64;  // Newton-Schulz iterations kept for the tangent pass
   rocblas_handle blas = nullptr;
   int D = 0;
   // D x D
-  Buf L, E, T, S, GS, M, H, Sig, SigInv, dY, dZ, dYn, dZn, dT;
-  Buf nsY[kNSMax], nsZ[kNSMax], nsT[kNSMax];
+  Buf L, E, T, GS, H, Sig, Yb[2], Zb[2], Eh, Xs, R, P, C1, C2;
   // D
-  Buf w, sq, offd, scal;
-  Buf info, part, ticket, res, tpart;
-  double* host_tpart = nullptr;  // pinned copy of the T_k residual partials
-  double* host_res = nullptr;  // pinned copy of res
-  int K = 0, K_prev = 0;       // Newton-Schulz iterations of the current / previous root
-  bool eig_pending = false;    // a dsyevd ran since the last fr_info
-  double c = 0.0;              // its scaling (~1.25 lambda_max)
+  Buf w, offd, scal, pv[4];
+  Buf info, sched, fro_part, tpart[2], pq_part, rz_part, rr_part, ee_part;
+  FrSched* host_sched = nullptr;  // pinned copy of the schedule / status block
+  const double* Yf = nullptr;     // final Newton-Schulz iterates (A^(1/2), A^(-1/2))
+  const double* Zf = nullptr;
+  bool have_z = false;            // Zf holds a previous root (power-iteration start)
+  int pv_cur = 0;                 // power-iteration vectors: pv[pv_cur] (Sigma), pv[2 + pv_cur] (Z)
+  bool warm = false;              // pv hold the previous root's vectors
+  bool zv_init = false;           // pv[2..3] hold a Z power vector
+  bool last_warm = false;         // the last root was a warm one (iteration hints apply)
+  int ns_kmax = 12, pcg_kmax = 14;  // iterations launched (device skips past convergence)
+  bool eig_pending = false;       // a dsyevd ran since the last fr_info
+  bool sqrt_pending = false;      // a Newton-Schulz / PCG status to read at fr_info
   // N x D / N
   Buf Z, X, G, s, logp, zz, r, rk;
   // pinned host staging for host-callback targets
@@ -423,8 +645,7 @@ struct FrWork {
   size_t hcap = 0;
   ~FrWork() {
     if (blas) rocblas_destroy_handle(blas);
-    if (host_res) (void)hipHostFree(host_res);
-    if (host_tpart) (void)hipHostFree(host_tpart);
+    if (host_sched) (void)hipHostFree(host_sched);
     for (double* p : {hx, hlp, hg})
       if (p) (void)hipHostFree(p);
   }
@@ -452,33 +673,25 @@ int reserve_d(FrWork* W, int D, hipStream_t st) {
     return vb_set_error(-2, "rocblas_set_stream failed");
   if (W->D >= D) return 0;
   const size_t dd = sizeof(double) * (size_t)D * D;
-  for (FrWork::Buf* b : {&W->L, &W->E, &W->T, &W->S, &W->GS, &W->M, &W->H, &W->Sig, &W->SigInv,
-                         &W->dY, &W->dZ, &W->dYn, &W->dZn, &W->dT})
+  for (FrWork::Buf* b : {&W->L, &W->E, &W->T, &W->GS, &W->H, &W->Sig, &W->Yb[0], &W->Yb[1],
+                         &W->Zb[0], &W->Zb[1], &W->Eh, &W->Xs, &W->R, &W->P, &W->C1, &W->C2})
     FR_HIP(b->reserve(dd));
-  for (int k = 0; k < FrWork::kNSMax; ++k)
-    if (W->nsY[k].p) {  // grow the kept iterates too
-      FR_HIP(W->nsY[k].reserve(dd));
-      FR_HIP(W->nsZ[k].reserve(dd));
-      FR_HIP(W->nsT[k].reserve(dd));
-    }
-  for (FrWork::Buf* b : {&W->w, &W->sq, &W->offd}) FR_HIP(b->reserve(sizeof(double) * D));
+  for (FrWork::Buf* b : {&W->w, &W->offd, &W->pv[0], &W->pv[1], &W->pv[2], &W->pv[3]})
+    FR_HIP(b->reserve(sizeof(double) * D));
   FR_HIP(W->scal.reserve(sizeof(double) * 8));
   FR_HIP(W->info.reserve(sizeof(int) * 4));
-  if (!W->ticket.p) {
-    FR_HIP(W->ticket.reserve(sizeof(unsigned) * 4));
-    FR_HIP(hipMemsetAsync(W->ticket.p, 0, sizeof(unsigned) * 4, st));
+  const size_t nblk = (size_t)((D + 31) / 32) * ((D + 31) / 32);
+  for (FrWork::Buf* b : {&W->fro_part, &W->tpart[0], &W->tpart[1], &W->pq_part, &W->rz_part})
+    FR_HIP(b->reserve(sizeof(double) * 4 * nblk));
+  for (FrWork::Buf* b : {&W->rr_part, &W->ee_part}) FR_HIP(b->reserve(sizeof(double) * nblk));
+  if (!W->sched.p) {
+    FR_HIP(W->sched.reserve(sizeof(FrSched)));
+    FR_HIP(hipMemsetAsync(W->sched.p, 0, sizeof(FrSched), st));
   }
-  FR_HIP(W->part.reserve(sizeof(double) * kNormBlocks));
-  FR_HIP(W->res.reserve(sizeof(double) * (FrWork::kNSMax + 3)));
-  {
-    // residual partials of T_k: 4 per 32 x 32 block, kept per iteration
-    const size_t nblk = (size_t)((D + 31) / 32) * ((D + 31) / 32) * 4;
-    FR_HIP(W->tpart.reserve(sizeof(double) * nblk * FrWork::kNSMax));
-    if (W->host_tpart) (void)hipHostFree(W->host_tpart);
-    W->host_tpart = nullptr;
-    FR_HIP(hipHostMalloc(&W->host_tpart, sizeof(double) * 2 * nblk));
-  }
-  if (!W->host_res) FR_HIP(hipHostMalloc(&W->host_res, sizeof(double) * (FrWork::kNSMax + 3)));
+  if (!W->host_sched) FR_HIP(hipHostMalloc(&W->host_sched, sizeof(FrSched)));
+  W->warm = false;
+  W->have_z = false;
+  W->zv_init = false;
   W->D = D;
   return 0;
 }
@@ -546,146 +759,140 @@ int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st) {
   return 0;
 }
 
-namespace {
-int frob2(FrWork* W, int n, const double* X, double shift, double* out, hipStream_t st) {
-  const long long nn = (long long)n * n;
-  const unsigned nb = (unsigned)std::min<long long>(kNormBlocks, std::max(1LL, (nn + 255) / 256));
-  hipLaunchKernelGGL(fr_frob2_kernel, dim3(nb), dim3(256), 0, st, n, X, shift, W->part.d(),
-                     static_cast<unsigned*>(W->ticket.p), out);
-  FR_HIP(hipGetLastError());
-  return 0;
-}
-}  // namespace
-
-// S = sqrtm(Sigma) without an eigendecomposition: coupled Newton-Schulz on
-// A = Sigma / c (Higham, Functions of Matrices §6.3):
-//   T_k = 3I - Z_k Y_k,  Y_{k+1} = Y_k T_k / 2,  Z_{k+1} = T_k Z_k / 2
-//   Y_k -> (Sigma / c)^{1/2},  Z_k -> (Sigma / c)^{-1/2}.
-// The iterates are kept for the tangent (Sylvester) pass.  Converged when
-// ||I - Z_k Y_k||_F <= 1e-10 sqrt(D) or has stalled at rounding level; the host
-// reads the residuals at most once per iteration after the previous root's count.
+// S = sqrtm(Sigma) without an eigendecomposition and without a host round trip:
+// scaled coupled Newton-Schulz (FrSched above).  Launches: Sigma = L L^T (its
+// epilogue gives ||Sigma||_F^2), n_pow power steps on Sigma and on the previous
+// root's Z, the schedule kernel, iteration 0 (one GEMM: Y_1, Z_1 are polynomials
+// in Sigma), then for k = 1 .. ns_kmax: T_k (its epilogue gives ||I - Z_k Y_k||_F
+// partials) and the grouped Y_{k+1}, Z_{k+1} product, whose blocks first test
+// convergence (||I - Z_k Y_k||_F <= 1e-10 sqrt(D), or a rounding-floor stall
+// below 1e-8 sqrt(D)) and then copy Y_k, Z_k through instead; later T GEMMs
+// return at once.  Non-convergence within ns_kmax sets FrSched::status (read by
+// fr_info).  `warm`: Sigma is close to the previous call's (an optimisation
+// run), so 3 warm-started power steps suffice and l_0 comes from the previous
+// root; otherwise 8 power steps from ones and l_0 = 0.05.
 // Also: L, Sigma = L L^T, scal[0] = 0.5 log det Sigma = sum log L_ii.
-int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st) {
+int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm) {
   if (int rc = reserve_d(W, D, st)) return rc;
   const long long dd = (long long)D * D;
-  const size_t bytes = sizeof(double) * (size_t)dd;
+  const int nblk = ((D + 31) / 32) * ((D + 31) / 32);
+  FrSched* sc = static_cast<FrSched*>(W->sched.p);
   hipLaunchKernelGGL(fr_unpack_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, lam, W->L.d());
   hipLaunchKernelGGL(fr_logdet_lam_kernel, dim3(1), dim3(1024), 0, st, D, lam, W->scal.d());
-  FR_HIP(gemm(mm(D, D, D, W->L.d(), false, W->L.d(), true, W->Sig.d()), st));
-  double* res = W->res.d();
-  const int KM = FrWork::kNSMax;
-  if (int rc = frob2(W, D, W->Sig.d(), 0.0, res + KM, st)) return rc;
-  // lambda_max estimate: 6 power steps (vectors in the sq / offd / w scratch)
   {
-    const unsigned nb = (unsigned)((D + 7) / 8);
-    double *xa = W->sq.d(), *xb = W->offd.d();
-    hipLaunchKernelGGL(fr_power_kernel, dim3(nb), dim3(256), 0, st, D, W->Sig.d(), nullptr, xa);
-    for (int p = 1; p < 5; ++p) {
-      hipLaunchKernelGGL(fr_power_kernel, dim3(nb), dim3(256), 0, st, D, W->Sig.d(), xa, xb);
-      std::swap(xa, xb);
-    }
-    hipLaunchKernelGGL(fr_power_kernel, dim3(nb), dim3(256), 0, st, D, W->Sig.d(), xa, xb);
-    hipLaunchKernelGGL(fr_norm2_kernel, dim3(1), dim3(256), 0, st, D, xb, res + KM + 1);
-  }
-  FR_HIP(W->nsY[0].reserve(bytes));
-  FR_HIP(W->nsZ[0].reserve(bytes));
-  hipLaunchKernelGGL(fr_ns_init_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, W->Sig.d(), res + KM,
-                     W->nsY[0].d(), W->nsZ[0].d(), res + KM + 2);
-  const int kmin = std::max(2, W->K_prev);
-  // ||I - Z Y||_F <= 1e-10 sqrt(D): S = sqrt(c) Y_K to ~1e-10 relative (the parity bar is
-  // 1e-5; the tests hold gradients to 1e-8 of the scipy sqrtm / solve_sylvester oracle)
-  const double tol = 1e-10 * std::sqrt((double)D), stall = 1e-8 * std::sqrt((double)D);
-  int K = -1;
-  for (int k = 0; k < KM; ++k) {
-    FR_HIP(W->nsT[k].reserve(bytes));
-    const size_t nblk = (size_t)((D + 31) / 32) * ((D + 31) / 32) * 4;
-    GemmOp g = mm(D, D, D, W->nsZ[k].d(), false, W->nsY[k].d(), false, W->nsT[k].d(), -1.0);
-    g.diag = 3.0;
-    g.sq_part = W->tpart.d() + nblk * k;   // ||T_k - 2I||_F^2 partials from the epilogue
-    g.sq_shift = 2.0;
+    GemmOp g = mm(D, D, D, W->L.d(), false, W->L.d(), true, W->Sig.d());
+    g.sq_part = W->fro_part.d();
     FR_HIP(gemm(g, st));
-    if (k >= kmin) {
-      // partials of T_{k-1} and T_k (contiguous) and the scale c, one synchronisation
-      FR_HIP(hipMemcpyAsync(W->host_tpart, W->tpart.d() + nblk * (k - 1), sizeof(double) * 2 * nblk,
-                            hipMemcpyDeviceToHost, st));
-      FR_HIP(hipMemcpyAsync(W->host_res + KM + 2, res + KM + 2, sizeof(double), hipMemcpyDeviceToHost, st));
-      FR_HIP(hipStreamSynchronize(st));
-      for (int kk = 0; kk < 2; ++kk) {
-        double t = 0.0;
-        for (size_t b = 0; b < nblk; ++b) t += W->host_tpart[kk * nblk + b];   // fixed order
-        W->host_res[k - 1 + kk] = t;
+  }
+  // power steps: Sigma x and Z_prev u (the previous root's vectors as start)
+  warm = warm && W->warm;
+  const bool hz = warm && W->have_z && W->Zf;
+  const int n_pow = warm ? 3 : 8;
+  const unsigned nb = (unsigned)((D + 7) / 8);
+  for (int p = 0; p < n_pow; ++p) {
+    const int a = W->pv_cur, b = 1 - a;
+    const bool xfirst = p == 0 && !warm, ufirst = p == 0 && !W->zv_init;
+    hipLaunchKernelGGL(fr_power2_kernel, dim3(nb, hz ? 2 : 1), dim3(256), 0, st, D, W->Sig.d(),
+                       xfirst ? nullptr : W->pv[a].d(), W->pv[b].d(), W->Zf,
+                       ufirst ? nullptr : W->pv[2 + a].d(), W->pv[2 + b].d());
+    W->pv_cur = b;
+  }
+  if (hz) W->zv_init = true;
+  // warm roots launch the learnt count (fr_info); others at least 12 (l_0 = 0.05
+  // needs ~9 at rounding level)
+  const int kmax = std::min(warm ? std::max(W->ns_kmax, 4) : std::max(W->ns_kmax, 12), kFrNSMax);
+  W->last_warm = warm;
+  hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(256), 0, st, D, kmax, W->fro_part.d(),
+                     4 * nblk, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), hz ? 1 : 0, 0.05,
+                     sc);
+  // iteration 0: Y_1 -> Yb[1], Z_1 -> Zb[1]
+  {
+    GemmOp g = mm(D, D, D, W->Sig.d(), false, W->Sig.d(), false, W->Yb[1].d());
+    g.ns0 = sc->ns0;
+    g.ns0_z = W->Zb[1].d();
+    FR_HIP(gemm(g, st));
+  }
+  for (int k = 1; k <= kmax; ++k) {
+    const double *Yk = W->Yb[k & 1].d(), *Zk = W->Zb[k & 1].d();
+    double* tp = W->tpart[k & 1].d();
+    GemmOp t = mm(D, D, D, Zk, false, Yk, false, W->T.d());
+    t.alpha_dev = &sc->nalpha2[k];
+    t.diag = 3.0;
+    t.sq_part = tp;
+    t.sq_shift_dev = &sc->shift[k];
+    t.skip_flag = &sc->ns_conv;
+    FR_HIP(gemm(t, st));
+    GemmOp yz[2] = {mm(D, D, D, Yk, false, W->T.d(), false, W->Yb[(k + 1) & 1].d()),
+                    mm(D, D, D, W->T.d(), false, Zk, false, W->Zb[(k + 1) & 1].d())};
+    for (int o = 0; o < 2; ++o) {
+      GemmOp& g = yz[o];
+      g.alpha_dev = &sc->halpha[k];
+      g.skip_flag = &sc->ns_conv;
+      g.copy_src = o == 0 ? Yk : Zk;
+      g.conv_part = tp;
+      g.conv_n = 4 * nblk;
+      g.conv_scale_dev = &sc->inv_a4[k];
+      g.conv_tol2 = 1e-20 * D;
+      if (k >= 2) {
+        g.conv_prev_part = W->tpart[(k - 1) & 1].d();
+        g.conv_prev_scale_dev = &sc->inv_a4[k - 1];
+        g.conv_stall_tol2 = 1e-16 * D;
       }
-      const double rk = std::sqrt(W->host_res[k]), rp = std::sqrt(W->host_res[k - 1]);
-      if (!(rk < 1e30))
-        return vb_set_error(-2, "Newton-Schulz square root of Sigma diverged (residual %g)", rk);
-      if (rk <= tol || (rk <= stall && rk >= 0.25 * rp)) {
-        K = k;
-        break;
-      }
+      g.conv_iter_out = &sc->ns_iter;
+      g.conv_iter = k;
     }
-    if (k + 1 >= KM) break;
-    FR_HIP(W->nsY[k + 1].reserve(bytes));
-    FR_HIP(W->nsZ[k + 1].reserve(bytes));
-    const GemmOp yz[2] = {mm(D, D, D, W->nsY[k].d(), false, W->nsT[k].d(), false, W->nsY[k + 1].d(), 0.5),
-                          mm(D, D, D, W->nsT[k].d(), false, W->nsZ[k].d(), false, W->nsZ[k + 1].d(), 0.5)};
     FR_HIP(gemm_group(yz, 2, st));
   }
-  if (K < 0)
-    return vb_set_error(-2, "Newton-Schulz square root of Sigma did not converge in %d iterations "
-                            "(Sigma too ill-conditioned)", KM);
-  W->K = K;
-  W->K_prev = K;
-  W->c = W->host_res[KM + 2];
+  W->Yf = W->Yb[(kmax + 1) & 1].d();
+  W->Zf = W->Zb[(kmax + 1) & 1].d();
+  W->have_z = true;
+  W->warm = true;
+  W->sqrt_pending = true;
   FR_HIP(hipGetLastError());
   return 0;
 }
 
-// Sylvester solve of autograd's sqrtm VJP, S X + X S = G_S + G_S^T, as the
-// forward-mode derivative of the Newton-Schulz iteration (the Frechet
-// derivative of sqrtm at a symmetric Sigma is self-adjoint), then
-// H = X + 2 c_inv Sigma^-1 (the symmetric Sigma cotangent, doubled).
-//   dT_k = -(dZ_k Y_k + Z_k dY_k)
-//   dY_{k+1} = (dY_k T_k + Y_k dT_k) / 2,  dZ_{k+1} = (dT_k Z_k + T_k dZ_k) / 2
-// with dY_0 = (G_S + G_S^T) / c, dZ_0 = 0; X = sqrt(c) dY_{K+1}.
-int fr_sylvester(FrWork* W, int D, double* H, hipStream_t st) {
-  const long long dd = (long long)D * D;
-  const int K = W->K;
-  const double* cdev = W->res.d() + FrWork::kNSMax + 2;
-  hipLaunchKernelGGL(fr_symscale_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, W->GS.d(), cdev,
-                     W->dY.d());
-  double *dY = W->dY.d(), *dZ = W->dZ.d(), *dYn = W->dYn.d(), *dZn = W->dZn.d(), *dT = W->dT.d();
-  // a dual product: alpha (A B + A2 B2), accumulated in one pass over K
-  auto dual = [&](const double* A, const double* B, const double* A2, const double* B2, double* C,
-                  double alpha) {
-    GemmOp g = mm(D, D, D, A, false, B, false, C, alpha);
-    g.A2 = A2;
-    g.B2 = B2;
-    g.alpha2 = alpha;
+// Preconditioned conjugate gradients for autograd's sqrtm VJP (see pcg_* above):
+// X = the symmetric solution of S X + X S = G_S + G_S^T, into W->Xs.
+int fr_pcg(FrWork* W, int D, hipStream_t st) {
+  FrSched* sc = static_cast<FrSched*>(W->sched.p);
+  const int nt = (D + kTile - 1) / kTile, nblk = nt * nt;
+  const dim3 tg(nt, nt);
+  hipLaunchKernelGGL(pcg_init_kernel, tg, dim3(256), 0, st, D, W->GS.d(), sc, W->Eh.d(),
+                     W->R.d(), W->Xs.d(), W->ee_part.d());
+  // P_0 = M^-1(R_0) from C2 = Z R_0, <R_0, Z R_0> in the epilogue
+  auto zr = [&](int it) {
+    GemmOp g = mm(D, D, D, W->Zf, false, W->R.d(), false, W->C2.d());
+    g.dot_with = W->R.d();
+    g.dot_part = W->rz_part.d();
+    g.skip_flag = &sc->pcg_done;
+    if (it >= 0) {   // converged when ||R||^2 <= 1e-22 ||E||^2 (relative residual 1e-11)
+      g.conv_part = W->rr_part.d();
+      g.conv_n = nblk;
+      g.conv_ref_dev = &sc->ee;
+      g.conv_tol2 = 1e-22;
+      g.conv_iter_out = &sc->pcg_iter;
+      g.conv_iter = it;
+    }
     return g;
   };
-  // k = 0: Z_0 = I, dZ_0 = 0, dT_0 = -dY_0
-  {
-    GemmOp g = dual(dY, W->nsT[0].d(), W->nsY[0].d(), dY, dYn, 0.5);
-    g.alpha2 = -0.5;
+  FR_HIP(gemm(zr(-1), st));
+  hipLaunchKernelGGL(pcg_p_kernel, tg, dim3(256), 0, st, D, -1, W->C2.d(), W->rz_part.d(),
+                     4 * nblk, W->ee_part.d(), nblk, sc, W->P.d());
+  // warm roots launch the learnt count (fr_info), others at least 16
+  const int kpcg = W->last_warm ? W->pcg_kmax : std::max(W->pcg_kmax, 16);
+  for (int it = 0; it < kpcg; ++it) {
+    GemmOp g = mm(D, D, D, W->Yf, false, W->P.d(), false, W->C1.d());
+    g.dot_with = W->P.d();
+    g.dot_part = W->pq_part.d();
+    g.skip_flag = &sc->pcg_done;
     FR_HIP(gemm(g, st));
-    hipLaunchKernelGGL(fr_axpby_kernel, dim3(blocks(dd)), dim3(256), 0, st, dd, -0.5, dY, dZn);
-    std::swap(dY, dYn);
-    std::swap(dZ, dZn);
+    hipLaunchKernelGGL(pcg_xr_kernel, tg, dim3(256), 0, st, D, it, W->C1.d(), W->P.d(),
+                       W->pq_part.d(), 4 * nblk, sc, W->Xs.d(), W->R.d(), W->rr_part.d());
+    FR_HIP(gemm(zr(it), st));
+    hipLaunchKernelGGL(pcg_p_kernel, tg, dim3(256), 0, st, D, it, W->C2.d(), W->rz_part.d(),
+                       4 * nblk, W->ee_part.d(), nblk, sc, W->P.d());
   }
-  for (int k = 1; k <= K; ++k) {
-    const double *Yk = W->nsY[k].d(), *Zk = W->nsZ[k].d(), *Tk = W->nsT[k].d();
-    FR_HIP(gemm(dual(dZ, Yk, Zk, dY, dT, -1.0), st));                 // dT
-    const GemmOp yz[2] = {dual(dY, Tk, Yk, dT, dYn, 0.5),              // dY_{k+1}
-                          dual(dT, Zk, Tk, dZ, dZn, 0.5)};             // dZ_{k+1}
-    FR_HIP(gemm_group(yz, k < K ? 2 : 1, st));
-    std::swap(dY, dYn);
-    std::swap(dZ, dZn);
-  }
-  // Sigma^-1 = Z_K^2 / c
-  FR_HIP(gemm(mm(D, D, D, W->nsZ[K].d(), false, W->nsZ[K].d(), false, W->SigInv.d(), 1.0 / W->c),
-              st));
-  hipLaunchKernelGGL(fr_h_kernel, dim3(blocks(dd)), dim3(256), 0, st, dd, std::sqrt(W->c), dY,
-                     W->SigInv.d(), W->scal.d(), H);
   FR_HIP(hipGetLastError());
   return 0;
 }
@@ -710,10 +917,11 @@ int fr_draw(FrWork* W, int D, long long n, double df, const double* host_eps, ui
   return 0;
 }
 
-// x = mu + (z S) / s, S = sqrt(c) Y_K  (after fr_sqrt)
+// x = mu + (z S) / s, S = sqrt(c) Y_final  (after fr_sqrt)
 int fr_transform(FrWork* W, int D, long long n, const double* mu, const double* s,
                  const double* z, double* x, hipStream_t st) {
-  GemmOp g = mm((int)n, D, D, z, false, W->nsY[W->K].d(), false, x, std::sqrt(W->c));
+  GemmOp g = mm((int)n, D, D, z, false, W->Yf, false, x);
+  g.alpha_dev = &static_cast<FrSched*>(W->sched.p)->sqrt_c;
   g.row_div = s;
   g.col_bias = mu;
   FR_HIP(gemm(g, st));
@@ -743,9 +951,9 @@ int fr_target(FrWork* W, int tgt, int D, long long n, const double* tparams, dou
 // and the value into *value (device pointers).
 int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* host_eps,
                   uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
-                  double* grad, hipStream_t st) {
+                  double* grad, hipStream_t st, bool warm) {
   const int D = f.D, N = f.N;
-  if (int rc = fr_sqrt(W, D, lam, st)) return rc;
+  if (int rc = fr_sqrt(W, D, lam, st, warm)) return rc;
   if (int rc = reserve_n(W, D, N)) return rc;
   const double *s, *z;
   if (int rc = fr_draw(W, D, N, f.df, host_eps, k0, k1, stream, step, &s, &z, st)) return rc;
@@ -771,12 +979,16 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
   FR_HIP(gemm(g, st));
   hipLaunchKernelGGL(fr_colsum_kernel, dim3(blocks(D, 64)), dim3(256), 0, st, N, D, W->r.d(),
                      W->G.d(), grad);
-  // Sylvester solve (sqrtm VJP) + entropy / log q term -> symmetric Sigma cotangent
-  if (int rc = fr_sylvester(W, D, W->M.d(), st)) return rc;
-  // G_L = H L, packed with the exp-diagonal chain rule
-  FR_HIP(gemm(mm(D, D, D, W->M.d(), false, W->L.d(), false, W->H.d()), st));
+  // Sylvester solve (sqrtm VJP): X, symmetric Sigma cotangent of the sample term
+  if (int rc = fr_pcg(W, D, st)) return rc;
+  // G_L = X L, packed with the exp-diagonal chain rule; the entropy / log q term
+  // 2 c Sigma^-1 contributes 2 c Sigma^-1 L = 2 c L^-T, whose lower triangle is
+  // diag(2 c / L_ii): 2 c on each packed (log) diagonal entry
+  FR_HIP(gemm(mm(D, D, D, W->Xs.d(), false, W->L.d(), false, W->H.d()), st));
+  const int nt = (D + kTile - 1) / kTile;
   hipLaunchKernelGGL(fr_pack_kernel, dim3(blocks((long long)D * D)), dim3(256), 0, st, D, W->H.d(),
-                     W->L.d(), grad);
+                     W->L.d(), W->scal.d(), static_cast<FrSched*>(W->sched.p), W->rr_part.d(),
+                     nt * nt, grad);
   FR_HIP(hipGetLastError());
   return 0;
 }
@@ -801,7 +1013,7 @@ int fr_log_weights(FrWork* W, const FrSpec& f, const double* lam, long long m,
                    const double* host_eps, uint32_t k0, uint32_t k1, uint32_t stream,
                    uint32_t step, double* lw, double* xs, hipStream_t st) {
   const int D = f.D;
-  if (int rc = fr_sqrt(W, D, lam, st)) return rc;
+  if (int rc = fr_sqrt(W, D, lam, st, false)) return rc;
   if (int rc = reserve_n(W, D, m)) return rc;
   const double *s, *z;
   if (int rc = fr_draw(W, D, m, f.df, host_eps, k0, k1, stream, step, &s, &z, st)) return rc;
@@ -1165,13 +1377,35 @@ int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, 
   return 0;
 }
 
+// Reads back (one synchronisation) the outcome of the device-side iterations
+// since the last call: dsyevd's info, and the sticky Newton-Schulz / PCG status;
+// adapts the iteration counts launched next (one spare Newton-Schulz
+// iteration, two PCG iterations over the largest count seen).
 int fr_info(FrWork* W, hipStream_t st) {
   int info = 0;
-  if (!W->info.p || !W->eig_pending) return 0;
+  const bool eig = W->info.p && W->eig_pending, sq = W->sched.p && W->sqrt_pending;
+  if (!eig && !sq) return 0;
   W->eig_pending = false;
-  FR_HIP(hipMemcpyAsync(&info, W->info.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  W->sqrt_pending = false;
+  if (eig) FR_HIP(hipMemcpyAsync(&info, W->info.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  if (sq) FR_HIP(hipMemcpyAsync(W->host_sched, W->sched.p, sizeof(FrSched), hipMemcpyDeviceToHost, st));
   FR_HIP(hipStreamSynchronize(st));
-  return info;
+  if (info) return vb_set_error(-2, "eigendecomposition of Sigma did not converge (info %d)", info);
+  if (!sq) return 0;
+  const FrSched& h = *W->host_sched;
+  FrSched* d = static_cast<FrSched*>(W->sched.p);
+  FR_HIP(hipMemsetAsync(&d->status, 0, 3 * sizeof(int), st));
+  if ((h.status & 1) || !h.ns_conv)
+    return vb_set_error(-2, "Newton-Schulz square root of Sigma did not converge in %d iterations "
+                            "(Sigma too ill-conditioned)", W->ns_kmax);
+  if (h.status & 2)
+    return vb_set_error(-2, "conjugate gradients for the sqrtm gradient did not converge in %d "
+                            "iterations", W->pcg_kmax);
+  if (W->last_warm && h.hint_ns > 0)
+    W->ns_kmax = std::min(kFrNSMax, std::max(h.hint_ns, h.ns_iter) + 1);
+  if (W->last_warm && h.hint_pcg >= 0)
+    W->pcg_kmax = std::min(40, std::max(h.hint_pcg, h.pcg_iter) + 3);
+  return 0;
 }
 
 }  // namespace vbk

@@ -43,6 +43,36 @@ struct GemmOp {
   // written outputs, 4 per block at sq_part[4 (by gridDim.x + bx) + wave]
   double* sq_part;
   double sq_shift;
+  // ---- device-resident scalars and control (the sync-free full-rank step) ----
+  const double* alpha_dev;     // alpha (and alpha2) *= *alpha_dev
+  const double* sq_shift_dev;  // overrides sq_shift
+  // skip: when *skip_flag != 0 the block copies copy_src into C (if given) or
+  // returns.  Convergence test run first by every block, in the same fixed
+  // order: s = conv_scale * sum(conv_part[0, conv_n)); if s <= conv_tol2 *
+  // (*conv_ref or 1) the block sets *skip_flag = 1 and writes conv_iter to
+  // *conv_iter_out (when the flag was clear on entry), then skips.
+  int* skip_flag;
+  const double* copy_src;
+  const double* conv_part;
+  int conv_n;
+  const double* conv_scale_dev;
+  const double* conv_ref_dev;
+  double conv_tol2;
+  // stall: also converged when s <= conv_stall_tol2 * ref and the previous
+  // iterate's sum s_prev (conv_prev_part, same count, same scale rule with
+  // conv_prev_scale_dev) satisfies s >= s_prev / 16 (rounding floor reached)
+  const double* conv_prev_part;
+  const double* conv_prev_scale_dev;
+  double conv_stall_tol2;
+  int* conv_iter_out;
+  int conv_iter;
+  // optional: per-wave partial sums of dot_with_ij * C_ij (before beta), 4 per block
+  const double* dot_with;
+  double* dot_part;
+  // Newton-Schulz iteration 0 (A = B = Sigma): C = ns0[0] Sigma^2 + ns0[1] Sigma and
+  // ns0_z = ns0[2] (3 I - ns0[3] Sigma), written for the same tile
+  const double* ns0;
+  double* ns0_z;
 };
 
 // Up to two independent GEMMs of equal shape / transposes in one launch
@@ -102,6 +132,53 @@ __device__ __forceinline__ double frag(const double* s, int r, int k) {
   return KCONTIG ? s[r * SR + k] : s[k * SK + r];
 }
 
+// Block-uniform skip decision (see GemmOp::skip_flag).  Every block sums the
+// partials in the same order, so all blocks decide alike.
+__device__ __forceinline__ bool gemm_skip(const GemmOp& g, double* red) {
+  if (!g.skip_flag) return false;
+  __shared__ int s_skip;
+  const int t = threadIdx.x;
+  if (g.conv_part) {
+    double a = 0.0, b = 0.0;
+    for (int i = t; i < g.conv_n; i += NTH) {
+      a += g.conv_part[i];
+      if (g.conv_prev_part) b += g.conv_prev_part[i];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      a += __shfl_xor(a, off, 64);
+      b += __shfl_xor(b, off, 64);
+    }
+    if ((t & 63) == 0) {
+      red[t >> 6] = a;
+      red[8 + (t >> 6)] = b;
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    int sk = *g.skip_flag != 0;
+    if (!sk && g.conv_part) {
+      double a = 0.0, b = 0.0;
+      for (int k = 0; k < NTH / 64; ++k) {
+        a += red[k];
+        b += red[8 + k];
+      }
+      if (g.conv_scale_dev) a *= *g.conv_scale_dev;
+      if (g.conv_prev_scale_dev) b *= *g.conv_prev_scale_dev;
+      const double ref = g.conv_ref_dev ? *g.conv_ref_dev : 1.0;
+      const bool stall = g.conv_prev_part && a <= g.conv_stall_tol2 * ref && a * 16.0 >= b;
+      if (a <= g.conv_tol2 * ref || stall) {
+        sk = 1;
+        *g.skip_flag = 1;
+        if (g.conv_iter_out) *g.conv_iter_out = g.conv_iter;
+      }
+    }
+    s_skip = sk;
+  }
+  __syncthreads();
+  return s_skip != 0;
+}
+
 template <bool TA, bool TB, bool KS, bool DUAL>
 __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   const GemmOp& g = gg.op[blockIdx.z];
@@ -110,6 +187,16 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   __shared__ double sA[2][BUF];
   __shared__ double sB[2][BUF];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (gemm_skip(g, sB[1])) {
+    if (g.copy_src) {
+      for (int e = t; e < BT * BT; e += NTH) {
+        const int row = blockIdx.y * BT + e / BT, col = blockIdx.x * BT + e % BT;
+        if (row < g.M && col < g.N)
+          g.C[(long long)row * g.ldc + col] = g.copy_src[(long long)row * g.ldc + col];
+      }
+    }
+    return;
+  }
   const int q = w & 3, h = w >> 2;           // output quadrant, k half of each tile
   const int wm = q >> 1, wn = q & 1;
   const int i0 = blockIdx.y * BT, j0 = blockIdx.x * BT;
@@ -198,19 +285,27 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   __syncthreads();
   if (h == 1) return;
   const int col = j0 + wn * 16 + (lane & 15);
-  double sq = 0.0;
+  double sq = 0.0, dt = 0.0;
+  const double alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
+  const double shift = g.sq_shift_dev ? *g.sq_shift_dev : g.sq_shift;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = i0 + wm * 16 + kq + 4 * r;
     if (row < g.M && col < g.N) {
-      double v = g.alpha * (r4[r] + red[(q * 4 + r) * 64 + lane]);
+      double v = alpha * (r4[r] + red[(q * 4 + r) * 64 + lane]);
       if (g.row_div) v = v / g.row_div[row];
       if (g.col_bias) v = g.col_bias[col] + v;
       if (row == col) v += g.diag;
+      if (g.ns0) {
+        const double a = g.A[(long long)row * g.lda + col];
+        v = fma(g.ns0[1], a, g.ns0[0] * (r4[r] + red[(q * 4 + r) * 64 + lane]));
+        g.ns0_z[(long long)row * g.ldc + col] = g.ns0[2] * ((row == col ? 3.0 : 0.0) - g.ns0[3] * a);
+      }
       double* c = g.C + (long long)row * g.ldc + col;
+      if (g.dot_with) dt = fma(g.dot_with[(long long)row * g.ldc + col], v, dt);
       if (g.beta != 0.0) v += g.beta * *c;
       *c = v;
-      const double e = row == col ? v - g.sq_shift : v;
+      const double e = row == col ? v - shift : v;
       sq += e * e;
     }
   }
@@ -218,6 +313,11 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off, 64);
     if (lane == 0) g.sq_part[4 * (blockIdx.y * gridDim.x + blockIdx.x) + q] = sq;
+  }
+  if (g.dot_part) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) dt += __shfl_xor(dt, off, 64);
+    if (lane == 0) g.dot_part[4 * (blockIdx.y * gridDim.x + blockIdx.x) + q] = dt;
   }
 }
 

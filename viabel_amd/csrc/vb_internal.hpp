@@ -186,7 +186,9 @@ struct FrSpec {
 
 // All return 0 or a VB_E* code (message via vb_set_error).
 int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st);  // eigh of Sigma
-int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st);     // Newton-Schulz sqrtm
+// Newton-Schulz sqrtm; warm: Sigma is close to the previous call's (optimisation run)
+int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm = false);
+constexpr int kFrNSMax = 40;  // Newton-Schulz iterations launched at most per root
 int fr_draw(FrWork* W, int D, long long n, double df, const double* host_eps, uint32_t k0,
             uint32_t k1, uint32_t stream, uint32_t step, const double** s_out,
             const double** z_out, hipStream_t st);
@@ -196,7 +198,7 @@ int fr_target(FrWork* W, int tgt, int D, long long n, const double* tparams, dou
               const double* x, double* logp, double* G, hipStream_t st);
 int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* host_eps,
                   uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
-                  double* grad, hipStream_t st);
+                  double* grad, hipStream_t st, bool warm = false);
 int fr_logdensity(FrWork* W, int D, double df, double t_const, const double* lam, const double* x,
                   long long n, double* out, hipStream_t st);
 int fr_log_weights(FrWork* W, const FrSpec& f, const double* lam, long long m,
@@ -226,6 +228,8 @@ int mf_wide_value_grad(FrWork* W, const MfSpec& f, const double* lam, const doub
 int mf_wide_log_weights(FrWork* W, const MfSpec& f, const double* lam, long long m,
                         const double* host_eps, uint32_t k0, uint32_t k1, uint32_t stream,
                         uint32_t step, double* lw, double* xs, hipStream_t st);
+// 0, or a VB_E* code with the message set (eigendecomposition / Newton-Schulz /
+// PCG failure since the last call); synchronises the stream.
 int fr_info(FrWork* W, hipStream_t st);
 hipError_t launch_fr_lw(int D, long long m, double df, double t_const, const double* logp,
                         const double* zz, const double* s, const double* scal, double* lw,
