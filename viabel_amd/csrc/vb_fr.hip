@@ -636,6 +636,7 @@ struct FrWork {
   bool zv_init = false;           // pv[2..3] hold a Z power vector
   bool last_warm = false;         // the last root was a warm one (iteration hints apply)
   int ns_kmax = 12, pcg_kmax = 14;  // iterations launched (device skips past convergence)
+  int last_kmax = 12;             // Newton-Schulz iterations the last root launched
   bool eig_pending = false;       // a dsyevd ran since the last fr_info
   bool sqrt_pending = false;      // a Newton-Schulz / PCG status to read at fr_info
   // N x D / N
@@ -798,10 +799,14 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm) {
     W->pv_cur = b;
   }
   if (hz) W->zv_init = true;
-  // warm roots launch the learnt count (fr_info); others at least 12 (l_0 = 0.05
-  // needs ~9 at rounding level)
-  const int kmax = std::min(warm ? std::max(W->ns_kmax, 4) : std::max(W->ns_kmax, 12), kFrNSMax);
+  // warm roots launch the learnt count (fr_info) plus two spare iterations (the
+  // count drifts by one as Sigma moves, and a launched-but-skipped iteration
+  // costs only its launch); others at least 12 (l_0 = 0.05 needs ~9 at rounding
+  // level)
+  const int kmax =
+      std::min(warm ? std::max(W->ns_kmax + 2, 6) : std::max(W->ns_kmax, 12), kFrNSMax);
   W->last_warm = warm;
+  W->last_kmax = kmax;
   hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(256), 0, st, D, kmax, W->fro_part.d(),
                      4 * nblk, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), hz ? 1 : 0, 0.05,
                      sc);
@@ -1397,7 +1402,7 @@ int fr_info(FrWork* W, hipStream_t st) {
   FR_HIP(hipMemsetAsync(&d->status, 0, 3 * sizeof(int), st));
   if ((h.status & 1) || !h.ns_conv)
     return vb_set_error(-2, "Newton-Schulz square root of Sigma did not converge in %d iterations "
-                            "(Sigma too ill-conditioned)", W->ns_kmax);
+                            "(Sigma too ill-conditioned)", W->last_kmax);
   if (h.status & 2)
     return vb_set_error(-2, "conjugate gradients for the sqrtm gradient did not converge in %d "
                             "iterations", W->pcg_kmax);

@@ -152,9 +152,18 @@ __device__ __forceinline__ double rsqrt_pos(double y) {
 // Per-step values: each lane keeps the last four steps' partial values in
 // registers and one reduce-scatter every fourth step sums all four (the
 // entropy term sum log s rides in the partial of the log-scale rep lanes).
+#ifdef VB_SEP_TS
+// per-wave step timestamps of the launch whose first step is VB_SEP_TS (slot =
+// blockIdx.x * 4 + wave; [0] step 0 ... [k] step 2^(k-1), [13] last step,
+// [14] PPW, [15] kernel entry), read back by vb_debug_sep_ts
+constexpr int kTsWaves = 8192;
+__device__ unsigned long long g_sep_ts[kTsWaves][16];
+#endif
+
 template <class TGT, bool TFAM, bool HOST, int PPW, bool REGRING>
 __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, int wave,
-                                         const double2* sct, const double2* ltab) {
+                                         const double2* sct, const double2* ltab,
+                                         unsigned long long t_entry = 0) {
   constexpr int LPP = 64 / PPW;       // lanes per column pair
   constexpr int SL = LPP / 4;         // slot lanes per parameter
 #ifdef VB_SEP_PROF
@@ -212,6 +221,10 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
   double pA = 0.0, pB = 0.0;
   if constexpr (PIPE)
     normal_pair_tab(rng.draw((uint32_t)w, (uint32_t)gl, (uint32_t)a.rng_step0, 0u), pA, pB, sct, ltab);
+#ifdef VB_SEP_PROF
+  const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
+  unsigned long long t_s0 = 0, t_s1 = 0, t_s2 = 0;
+#endif
 
   for (int s = 0; s < a.n_steps; ++s) {
     const long long i = a.step0 + s;
@@ -329,13 +342,35 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
     sB = group_bcast<PPW, 3>(s_own, grp);
     if (i >= a.hist_start && updater) a.hist[(i - a.hist_start) * P + own_idx] = lam_own;
     slot = (slot + 1 == W) ? 0 : slot + 1;
+#ifdef VB_SEP_TS
+    if (lane == 0 && a.step0 == VB_SEP_TS && ((s & (s - 1)) == 0 || s + 1 == a.n_steps)) {
+      const int wslot = blockIdx.x * 4 + (threadIdx.x >> 6);
+      const int k = s + 1 == a.n_steps ? 13 : (s == 0 ? 0 : 1 + __builtin_ctz(s));
+      if (wslot < kTsWaves) {
+        g_sep_ts[wslot][k] = __builtin_amdgcn_s_memrealtime();
+        if (s == 0) {
+          g_sep_ts[wslot][14] = PPW;
+          g_sep_ts[wslot][15] = t_entry;
+        }
+      }
+    }
+#endif
+#ifdef VB_SEP_PROF
+    if (s < 3) {
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      if (s == 0) t_s0 = t;
+      else if (s == 1) t_s1 = t;
+      else t_s2 = t;
+    }
+#endif
   }
 
 #ifdef VB_SEP_PROF
   if (lane == 0 && a.step0 == VB_SEP_PROF) {
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-    printf("SEPW %d %d %u %u %llu %llu\n", PPW, w, __builtin_amdgcn_s_getreg(63492),
-           __builtin_amdgcn_s_getreg(63508), t_start, t_end);
+    printf("SEPW %d %d %u %u %llu %llu %llu %llu %llu %llu %llu\n", PPW, w,
+           __builtin_amdgcn_s_getreg(63492), __builtin_amdgcn_s_getreg(63508), t_entry, t_start,
+           t_loop, t_end, t_s0, t_s1, t_s2);
   }
 #endif
   if (!a.emit_grad && own_ok) {
@@ -359,6 +394,11 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
 template <class TGT, bool TFAM, bool HOST, int PPW_BIG, bool REGRING>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(3)))
 void sep_kernel(SepArgs a) {
+#if defined(VB_SEP_PROF) || defined(VB_SEP_TS)
+  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
+#else
+  const unsigned long long t_entry = 0;
+#endif
   __shared__ double s_ring[REGRING ? 1 : 4][REGRING ? 1 : 64 * 4 * PPW_BIG];
   // Box-Muller tables (vb_tables.hpp) for the in-kernel Philox draws
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
@@ -372,11 +412,11 @@ void sep_kernel(SepArgs a) {
   if ((int)blockIdx.x < a.blocks2) {
     const int wave = blockIdx.x * 4 + wid;
     if (wave * PPW_BIG >= a.pairs2) return;
-    sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave, s_sct, s_lt);
+    sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave, s_sct, s_lt, t_entry);
   } else {
     const int pair = a.pairs2 + (blockIdx.x - a.blocks2) * 4 + wid;
     if (pair >= a.n_pairs) return;
-    sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair, s_sct, s_lt);
+    sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair, s_sct, s_lt, t_entry);
   }
 }
 
@@ -1362,6 +1402,15 @@ hipError_t launch_block(int fam, int tgt, bool host, const BlockArgs& a, int npr
     default: return hipErrorInvalidValue;
   }
 }
+
+#ifdef VB_SEP_TS
+extern "C" int vb_debug_sep_ts(unsigned long long* out, int n_waves) {
+  if (n_waves > kTsWaves) n_waves = kTsWaves;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sep_ts),
+                                  sizeof(unsigned long long) * 16 * n_waves, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 
 hipError_t launch_sep_values(const double* vpart, int n_steps, int n_waves, double c0,
                              double* values, hipStream_t s) {
