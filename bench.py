@@ -197,31 +197,13 @@ def cpu_baseline_cfg3(host, n=N, runs=5, steps=200, allcore_rounds=3):
 # ---------------------------------------------------------------------------
 # GPU legs
 # ---------------------------------------------------------------------------
-class Timer:
-    """Pre-created HIP events on the launch stream (creation stays outside the
-    timed region)."""
-
-    def __init__(self, torch, stream, n):
-        self.stream = stream
-        self.ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                   for _ in range(n)]
-        self.used = []
-
-    def __call__(self, k, hist_rows):
-        e = self.ev[len(self.used)]
-        self.used.append((k, hist_rows))
-        return e
-
-    def launches(self):
-        """[(steps, history rows written, seconds)] per launch."""
-        return [(k, h, a.elapsed_time(b) * 1e-3) for (k, h), (a, b) in zip(self.used, self.ev)]
-
-
 def run_cfg3(torch, stream, dev, n, steps, warmup, rank, dist):
     """Config 3 (mf-Gauss KLVI, isogauss D = 1e4, Philox) for `steps` timed
-    steps after `warmup` untimed ones; launches of CHUNK steps, each bracketed
-    by HIP events.  Returns (elapsed max over ranks, [(steps, history rows,
-    seconds) per launch], run)."""
+    steps after `warmup` untimed ones, in launches of at most CHUNK steps.  The
+    library brackets every launch (sep_kernel + its per-step value reduction)
+    with HIP events on the launch stream (vb_run_set_timing), so the timed
+    loop makes one host call per launch.  Returns (elapsed max over ranks,
+    [(steps, history rows, seconds) per timed launch], run)."""
     import numpy as np
     from viabel_amd import targets, vb
     fam = vb.mean_field_gaussian_variational_family(D, rng='philox')
@@ -229,20 +211,17 @@ def run_cfg3(torch, stream, dev, n, steps, warmup, rank, dist):
     init = np.concatenate([np.zeros(D), np.ones(D)])
     run = vb.DeviceRun(obj, warmup + steps, init[None, :], window=WINDOW, learning_rate=LR,
                        epsilon=EPS)
+    run.set_timing(True)
     seed, strm = 0, 1 + rank          # one restart per rank, independent Philox streams
-    timer = Timer(torch, stream, -(-steps // CHUNK))
     hist_start = 3 * (warmup + steps) // 4        # vb.py:375-376
     # the W warm-up steps take the same host path as the timed launches
-    wtimer = Timer(torch, stream, -(-warmup // CHUNK))
     done = 0
     while done < warmup:
         cs = min(CHUNK, warmup - done)
-        e0, e1 = wtimer(cs, 0)
-        e0.record(stream)
         run.advance_philox(cs, seed, strm, done)
-        e1.record(stream)
         done += cs
     torch.cuda.synchronize(dev)
+    run.launch_times()                            # drop the warm-up records
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -250,11 +229,7 @@ def run_cfg3(torch, stream, dev, n, steps, warmup, rank, dist):
     done = 0
     while done < steps:
         cs = min(CHUNK, steps - done)
-        s0 = warmup + done
-        e0, e1 = timer(cs, max(0, s0 + cs - max(s0, hist_start)))
-        e0.record(stream)
         run.advance_philox(cs, seed, strm, warmup + done)
-        e1.record(stream)
         done += cs
     torch.cuda.synchronize(dev)
     if dist:
@@ -265,7 +240,11 @@ def run_cfg3(torch, stream, dev, n, steps, warmup, rank, dist):
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    return elapsed, timer.launches(), run
+    launches, s0 = [], warmup
+    for k, sec in run.launch_times():
+        launches.append((k, max(0, s0 + k - max(s0, hist_start)), sec))
+        s0 += k
+    return elapsed, launches, run
 
 
 def load_traffic():

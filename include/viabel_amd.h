@@ -211,6 +211,15 @@ int vb_run_create(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,
  * [n_problems][n_steps][N][D]. */
 int vb_run_advance(vb_run* run, int64_t n_steps, const vb_noise* noise);
 int vb_run_steps_done(vb_run* run, int64_t* out);
+/* Launch timing (measurement support, no reference counterpart): with enable
+ * != 0 every later vb_run_advance brackets its device work with HIP events on
+ * the context's stream, one pair per kernel chunk (column-pair path) or per
+ * call (other paths).  vb_run_launch_times waits for that work, returns up to
+ * max (steps, milliseconds) records in launch order, n_out = their count, and
+ * forgets them. */
+int vb_run_set_timing(vb_run* run, int enable);
+int vb_run_launch_times(vb_run* run, int64_t max, int64_t* steps_out, float* ms_out,
+                        int64_t* n_out);
 /* Results (all nullable): lam_out [n_problems][P]; hist_out
  * [n_problems][n_hist][P] (n_hist per vb_adagrad_config); values_out [n_problems][n_iters];
  * smoothed_out [n_problems][P] = mean of the history rows (vb.py:386-387). */

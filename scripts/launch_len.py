@@ -44,6 +44,27 @@ def main():
         print(json.dumps({'k': k, 'span_us_median': round(out[k], 2),
                           'us_per_step': round(out[k] / k, 3),
                           'spans': [round(x, 1) for x in spans]}), flush=True)
+    # a 20-step launch right behind a heater launch of h steps (no synchronisation
+    # between): does a warm GPU run the short launch faster?
+    for h in (0, 5, 64, 256, 1024):
+        spans = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize(dev)
+            left = h
+            while left > 0:
+                c = min(256, left)
+                run.advance_philox(c, 0, 1, step)
+                step += c
+                left -= c
+            e0.record(stream)
+            run.advance_philox(20, 0, 1, step)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            step += 20
+            spans.append(e0.elapsed_time(e1) * 1e3)
+        print(json.dumps({'heater_steps': h, 'span20_us_median': round(float(np.median(spans)), 2),
+                          'spans': [round(x, 1) for x in spans]}), flush=True)
     # increments: marginal cost per added step between lengths
     ks = sorted(out)
     for a, b in zip(ks, ks[1:]):

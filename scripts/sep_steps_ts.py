@@ -36,11 +36,13 @@ def main():
     torch.cuda.synchronize(dev)
     span = e0.elapsed_time(e1) * 1e3
     nw = 8192
-    buf = (ctypes.c_ulonglong * (16 * nw))()
+    buf = (ctypes.c_ulonglong * (32 * nw))()
     rc = nat.lib().vb_debug_sep_ts(buf, nw)
     assert rc == 0, rc
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 16).astype(np.int64)
-    a = a[a[:, 15] > 0]
+    both = np.frombuffer(buf, dtype=np.uint64).reshape(2, nw, 16).astype(np.int64)
+    a, clk = both[0], both[1]
+    keep = a[:, 15] > 0
+    a, clk = a[keep], clk[keep]
     t0 = a[:, 15].min()
     print('launch of %d steps: event span %.1f us, waves %d' % (steps, span, len(a)))
     ks = [0] + [1 << j for j in range(12) if (1 << j) < steps - 1]
@@ -58,6 +60,10 @@ def main():
         for lab, md, mxx in zip(labels, med, mx):
             rate = '' if prev is None else ' | %.3f us/step since step %d' % (
                 (md - prev[1]) / (lab - prev[0]), prev[0])
+            if prev is not None:
+                c0, c1 = cols[labels.index(prev[0])], cols[labels.index(lab)]
+                ghz = np.median((clk[m, c1] - clk[m, c0]) / ((a[m, c1] - a[m, c0]) * 10.0))
+                rate += ', core clock %.3f GHz' % ghz
             print('   end of step %4d: p50 %8.2f us  max %8.2f us%s' % (lab, md, mxx, rate))
             prev = (lab, md)
 

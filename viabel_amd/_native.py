@@ -82,6 +82,9 @@ _SIGNATURES = {
                        ctypes.c_int64, c_double_p, P(ctypes.c_void_p)], ctypes.c_int),
     'vb_run_advance': ([ctypes.c_void_p, ctypes.c_int64, P(Noise)], ctypes.c_int),
     'vb_run_steps_done': ([ctypes.c_void_p, c_int64_p], ctypes.c_int),
+    'vb_run_set_timing': ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
+    'vb_run_launch_times': ([ctypes.c_void_p, ctypes.c_int64, c_int64_p,
+                             P(ctypes.c_float), c_int64_p], ctypes.c_int),
     'vb_run_result': ([ctypes.c_void_p, c_double_p, c_double_p, c_double_p, c_double_p],
                       ctypes.c_int),
     'vb_run_destroy': ([ctypes.c_void_p], ctypes.c_int),

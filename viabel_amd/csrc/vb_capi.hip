@@ -658,6 +658,32 @@ struct vb_run {
   vbk::FrSpec spec{};
   vbk::MfSpec mspec{};
   DevBuf tparams, grad;
+  // launch timing (vb_run_set_timing): event pairs, reused; `ev_used` recorded
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+  std::vector<long long> ev_steps;
+  size_t ev_used = 0;
+  ~vb_run() {
+    for (auto& e : evs) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+  }
+  // the pair for the next bracketed launch of k steps (nullptr: timing off)
+  int next_event(long long k, std::pair<hipEvent_t, hipEvent_t>** out) {
+    *out = nullptr;
+    if (!timing) return VB_OK;
+    if (ev_used == evs.size()) {
+      std::pair<hipEvent_t, hipEvent_t> e{};
+      VB_HIP(hipEventCreate(&e.first));
+      VB_HIP(hipEventCreate(&e.second));
+      evs.push_back(e);
+      ev_steps.push_back(0);
+    }
+    ev_steps[ev_used] = k;
+    *out = &evs[ev_used++];
+    return VB_OK;
+  }
 };
 
 extern "C" {
@@ -798,6 +824,11 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
   uint32_t k0, k1;
   key_of(noise->seed, &k0, &k1);
 
+  std::pair<hipEvent_t, hipEvent_t>* call_ev = nullptr;
+  if (!r->sep) {
+    VB_TRY(r->next_event(n_steps, &call_ev));
+    if (call_ev) VB_HIP(hipEventRecord(call_ev->first, c->stream));
+  }
   if (r->fr || r->wide) {
     vbk::FrWork* W;
     VB_TRY(fr_work(c, &W));
@@ -877,9 +908,13 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
       a.k0 = k0;
       a.k1 = k1;
       a.stream = noise->stream;
+      std::pair<hipEvent_t, hipEvent_t>* ev;
+      VB_TRY(r->next_event(cs, &ev));
+      if (ev) VB_HIP(hipEventRecord(ev->first, c->stream));
       VB_HIP(vbk::launch_sep(r->fi.kind, r->tgt, host, a, c->stream));
       VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, sep_c0(r->fi, a.pd != 0), r->values.d() + a.step0,
                                     c->stream));
+      if (ev) VB_HIP(hipEventRecord(ev->second, c->stream));
       off += cs;
     }
   } else {
@@ -917,6 +952,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
     a.stream_stride = noise->stream_stride ? noise->stream_stride : 1;
     VB_HIP(vbk::launch_block(r->fi.kind, r->tgt, host, a, (int)r->nprob, c->stream));
   }
+  if (call_ev) VB_HIP(hipEventRecord(call_ev->second, c->stream));
   r->done += n_steps;
   if (r->wide) return sync(c);
   if (r->fr) {
@@ -928,6 +964,30 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
   }
   // host noise staging buffer is reused by the next call: finish before returning
   if (host) return sync(c);
+  return VB_OK;
+}
+
+int vb_run_set_timing(vb_run* r, int enable) {
+  if (!r) return fail(VB_EINVAL, "null vb_run");
+  r->timing = enable != 0;
+  return VB_OK;
+}
+
+int vb_run_launch_times(vb_run* r, int64_t max, int64_t* steps_out, float* ms_out,
+                        int64_t* n_out) {
+  if (!r || !n_out || (max > 0 && (!steps_out || !ms_out)))
+    return fail(VB_EINVAL, "null argument");
+  VB_TRY(check_ctx(r->ctx));
+  const size_t n = std::min<size_t>(r->ev_used, (size_t)std::max<int64_t>(max, 0));
+  for (size_t k = 0; k < n; ++k) {
+    VB_HIP(hipEventSynchronize(r->evs[k].second));
+    float ms = 0.f;
+    VB_HIP(hipEventElapsedTime(&ms, r->evs[k].first, r->evs[k].second));
+    steps_out[k] = r->ev_steps[k];
+    ms_out[k] = ms;
+  }
+  *n_out = (int64_t)n;
+  r->ev_used = 0;
   return VB_OK;
 }
 

@@ -158,6 +158,7 @@ __device__ __forceinline__ double rsqrt_pos(double y) {
 // [14] PPW, [15] kernel entry), read back by vb_debug_sep_ts
 constexpr int kTsWaves = 8192;
 __device__ unsigned long long g_sep_ts[kTsWaves][16];
+__device__ unsigned long long g_sep_clk[kTsWaves][16];  // s_memtime (core clock) beside it
 #endif
 
 template <class TGT, bool TFAM, bool HOST, int PPW, bool REGRING>
@@ -348,6 +349,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
       const int k = s + 1 == a.n_steps ? 13 : (s == 0 ? 0 : 1 + __builtin_ctz(s));
       if (wslot < kTsWaves) {
         g_sep_ts[wslot][k] = __builtin_amdgcn_s_memrealtime();
+        g_sep_clk[wslot][k] = __builtin_amdgcn_s_memtime();
         if (s == 0) {
           g_sep_ts[wslot][14] = PPW;
           g_sep_ts[wslot][15] = t_entry;
@@ -422,9 +424,9 @@ void sep_kernel(SepArgs a) {
 
 // values[i] = -(c0 + sum_w vpart[s][w]), fixed-order tree reduction.  One
 // 1024-thread block per step; each thread issues kValU independent loads per
-// round (one round covers 4 096 pairs, D = 1e4 needs two), so the block waits
-// on ~2 load latencies instead of a dependent chain of n_waves / 256.
-constexpr int kValThreads = 1024, kValU = 4;
+// round (one round covers 8 192 pairs: D = 1e4 needs one), so the block waits
+// on one load latency instead of a dependent chain of n_waves / 256.
+constexpr int kValThreads = 1024, kValU = 8;
 __global__ __launch_bounds__(kValThreads) void sep_values_kernel(const double* vpart,
                                                                  int n_waves, double c0,
                                                                  double* values) {
@@ -443,7 +445,7 @@ __global__ __launch_bounds__(kValThreads) void sep_values_kernel(const double* v
 #pragma unroll
     for (int u = 0; u < kValU; ++u) acc[u] += v[u];
   }
-  double t = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  double t = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   t = wave_sum(t);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
   __syncthreads();
@@ -1406,9 +1408,13 @@ hipError_t launch_block(int fam, int tgt, bool host, const BlockArgs& a, int npr
 #ifdef VB_SEP_TS
 extern "C" int vb_debug_sep_ts(unsigned long long* out, int n_waves) {
   if (n_waves > kTsWaves) n_waves = kTsWaves;
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sep_ts),
-                                  sizeof(unsigned long long) * 16 * n_waves, 0,
-                                  hipMemcpyDeviceToHost);
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sep_ts),
+                                    sizeof(unsigned long long) * 16 * n_waves, 0,
+                                    hipMemcpyDeviceToHost);
+  if (e == hipSuccess)
+    e = hipMemcpyFromSymbol(out + 16 * n_waves, HIP_SYMBOL(g_sep_clk),
+                            sizeof(unsigned long long) * 16 * n_waves, 0, hipMemcpyDeviceToHost);
+  return (int)e;
 }
 #endif
 

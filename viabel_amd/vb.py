@@ -413,6 +413,20 @@ class DeviceRun:
         nat.check(self._advance(self.handle, int(n_steps), nz))
         self.done += int(n_steps)
 
+    def set_timing(self, enable=True):
+        """Bracket later advances' device work with HIP events (vb_run_set_timing)."""
+        nat.check(nat.lib().vb_run_set_timing(self.handle, 1 if enable else 0))
+
+    def launch_times(self, max_records=4096):
+        """[(steps, seconds)] of the bracketed launches since the last call."""
+        import ctypes
+        steps = (ctypes.c_int64 * max_records)()
+        ms = (ctypes.c_float * max_records)()
+        n = ctypes.c_int64()
+        nat.check(nat.lib().vb_run_launch_times(self.handle, max_records, steps, ms,
+                                                ctypes.byref(n)))
+        return [(int(steps[k]), float(ms[k]) * 1e-3) for k in range(n.value)]
+
     def advance_host(self, eps):
         """eps: [n_problems][n_steps][N][D] standardized draws."""
         eps = nat.as_f64(eps)
