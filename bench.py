@@ -697,4 +697,5 @@ if __name__ == '__main__':
     # the CPU-baseline legs are single-threaded numpy (set before numpy loads)
     for k in ('OMP_NUM_THREADS', 'OPENBLAS_NUM_THREADS', 'MKL_NUM_THREADS'):
         os.environ.setdefault(k, '1')
+    os.environ.setdefault('VIABEL_AMD_PROGRESS', '0')     # no progress bars in the legs
     main()

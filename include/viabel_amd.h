@@ -37,11 +37,13 @@
  *   vb_centered_moments    viabel/bounds.py:127-135 (wasserstein_bounds sample moments)
  *   vb_covariance          viabel/bounds.py:55-56 (np.cov(samples.T), ddof = 1)
  *   vb_weighted_covariance notebooks/experiments.py:83-85 (PSIS-weighted mean / np.cov)
+ *   vb_weighted_covariance_logw notebooks/experiments.py:80-85 (weights from log weights)
  *   vb_psislw              notebooks/psis.py:112-208 (psislw)
  *   vb_psislw_colmajor     notebooks/psis.py:112-208 (psislw, Fortran-ordered input)
  *   vb_gpdfit              notebooks/psis.py:211-331 (gpdfitnew)
  *   vb_gpinv               notebooks/psis.py:334-376 (gpinv)
  *   vb_sumlogs             notebooks/psis.py:379-395 (sumlogs)
+ *   vb_sumlogs_rows        notebooks/psis.py:379-395 (sumlogs with an axis)
  */
 #ifndef VIABEL_AMD_H
 #define VIABEL_AMD_H
@@ -291,6 +293,12 @@ int vb_covariance(vb_ctx* ctx, const double* x, int64_t n, int64_t d,
  * (notebooks/experiments.py:73-89) with the PSIS-smoothed weights. */
 int vb_weighted_covariance(vb_ctx* ctx, const double* x, int64_t n, int64_t d,
                            const double* w, int32_t ddof, double* mean_out, double* cov_out);
+/* vb_weighted_covariance with w = exp(log_w - max log_w), normalised on the
+ * device: improve_with_psis's weights from the smoothed log weights
+ * (notebooks/experiments.py:80-85). */
+int vb_weighted_covariance_logw(vb_ctx* ctx, const double* x, int64_t n, int64_t d,
+                                const double* log_w, int32_t ddof, double* mean_out,
+                                double* cov_out);
 
 /* ---- PSIS (psis.py:112-395) ------------------------------------------ */
 /* lw [n, m] C order (m columns of n log weights).  lw_out same layout.
@@ -313,6 +321,9 @@ int vb_gpdfit(vb_ctx* ctx, const double* x, int64_t n, double* k, double* sigma,
 int vb_gpinv(vb_ctx* ctx, const double* p, int64_t n, double k, double sigma,
              double* out);
 int vb_sumlogs(vb_ctx* ctx, const double* x, int64_t n, double* out);
+/* out[r] = sumlogs of row r of x [rows][n] (sumlogs with an axis, psis.py:379-395),
+ * all rows in one launch chain. */
+int vb_sumlogs_rows(vb_ctx* ctx, const double* x, int64_t rows, int64_t n, double* out);
 
 #ifdef __cplusplus
 }

@@ -60,7 +60,9 @@ def stochastic_iterate_averaging(estimate, start):
     """functions.py:68-77."""
     N = estimate.shape[0]
     if N - start <= 0:
-        raise ValueError('Start of stationary distribution must be lower than number of iterates')
+        # the reference raises a bare str (functions.py:70-71), which Python
+        # turns into a TypeError; same exception type here, with the message
+        raise TypeError('Start of stationary distribution must be lower than number of iterates')
     window_lengths = np.reshape(np.arange(start, N) - start + 1, [-1, 1])
     estimate_iters = np.cumsum(estimate[start:, :], axis=0) / window_lengths
     return estimate_iters, estimate_iters[-1]

@@ -10,6 +10,9 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line('markers', 'gpu: needs an MI355X (runs the HIP kernels)')
+    # adagrad_optimize's progress bar (vb.py:354) off in tests; tests that check it
+    # turn it back on
+    os.environ.setdefault('VIABEL_AMD_PROGRESS', '0')
     _build_missing()
 
 

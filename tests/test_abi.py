@@ -96,8 +96,13 @@ def test_api_argument_errors_without_gpu():
     fam = vb.mean_field_gaussian_variational_family(3)
     with pytest.raises(ValueError, match='only p = 2 or 4 supported'):
         fam.pth_moment(3, np.zeros(6))
+    # a callable torch cannot differentiate (vb.py:236-241 takes any autograd
+    # callable; only torch-differentiable ones can be wrapped here)
     with pytest.raises(TypeError, match='viabel_amd.targets'):
-        vb.black_box_klvi(fam, lambda x: -0.5 * np.sum(x ** 2, 1), 10)
+        vb.black_box_klvi(fam, lambda x: np.asarray(x).sum(1), 10)
+    # a torch-differentiable callable is wrapped as a host-callback target
+    obj = vb.black_box_klvi(fam, lambda x: -0.5 * (x ** 2).sum(1), 10)
+    assert obj.target.kind == targets.callback(lambda x: None, 3).kind
     with pytest.raises(ValueError, match='learning rate must be positive'):
         vb.adagrad_optimize(10, vb.black_box_klvi(fam, targets.isogauss(3), 5), np.zeros(6),
                             learning_rate=0)

@@ -201,6 +201,33 @@ def test_weighted_covariance_vs_numpy(n, d, weighted):
         np.testing.assert_allclose(c, np.cov(x.T, aweights=w, ddof=ddof), rtol=1e-10, atol=1e-12)
 
 
+@pytest.mark.parametrize('n,d', [(500, 3), (1_000_000, 2), (700, 300)])
+def test_weighted_covariance_log_weights(n, d):
+    """Weights from log weights on the device (improve_with_psis,
+    experiments.py:80-85): exp(lw - max) normalised, against numpy."""
+    from viabel_amd import experiments
+    rs = np.random.RandomState(n + d + 1)
+    x = rs.randn(n, d) + rs.randn(d)
+    lw = rs.randn(n) * 3.0 - 700.0         # exp(lw) alone would underflow
+    w = np.exp(lw - lw.max())
+    w /= w.sum()
+    m, c = experiments.weighted_mean_and_cov(x, log_weights=lw, ddof=0)
+    np.testing.assert_allclose(m, np.average(x, axis=0, weights=w), rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(c, np.cov(x.T, aweights=w, ddof=0), rtol=1e-9, atol=1e-12)
+    with pytest.raises(ValueError, match='weights sum to zero'):
+        experiments.weighted_mean_and_cov(x[:10], np.zeros(10))
+
+
+def test_sumlogs_axis_batched():
+    """sumlogs with an axis: all rows in one device call (psis.py:379-395)."""
+    from viabel_amd import psis
+    from oracle import psis_oracle
+    rs = np.random.RandomState(5)
+    x = rs.randn(7, 3000, 4) * 20
+    for axis in (0, 1, 2):
+        _close(psis.sumlogs(x, axis=axis), psis_oracle.sumlogs(x, axis=axis), rtol=1e-13)
+
+
 def test_all_bounds_samples_wide():
     """all_bounds with raw samples at d > 64 (np.cov on the MFMA GEMM path)."""
     import viabel_amd as va

@@ -52,7 +52,7 @@ def test_windows_halfway_and_averaging():
     oit, olast = fo.stochastic_iterate_averaging(chains[1, :, 2:5], 700)
     _close(it, oit, 1e-13)
     _close(last, olast, 1e-13)
-    with pytest.raises(ValueError, match='Start of stationary'):
+    with pytest.raises(TypeError, match='Start of stationary'):
         functions.stochastic_iterate_averaging(chains[0], 3000)
 
 

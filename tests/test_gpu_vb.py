@@ -332,3 +332,45 @@ def test_sep_layouts_agree(mode, kind, df, D, monkeypatch):
                        learning_rate=0.03, window=7)
     np.testing.assert_allclose(res[1], ores[1], rtol=1e-9, atol=1e-11)
     np.testing.assert_allclose(res[2], ores[2], rtol=1e-9, atol=1e-9)
+
+
+def test_adagrad_chunked_progress_and_interrupt(monkeypatch):
+    """adagrad_optimize runs the device loop in chunks (>= 1000 steps) with the
+    reference's progress bar between them; the result equals one unchunked
+    device run, and a KeyboardInterrupt returns the steps done so far
+    (vb.py:377-389)."""
+    vb, targets, vo, ro = _mods()
+    D, N, n_iters = 6, 64, 2400
+    monkeypatch.setenv('VIABEL_AMD_PROGRESS', '1')
+    fam = vb.mean_field_gaussian_variational_family(D, rng='philox')
+    init = np.concatenate([np.zeros(D), np.ones(D)])
+    obj = vb.black_box_klvi(fam, targets.funnel(D), N)
+    seed, stream, step0 = fam.seed, fam.stream, fam.step
+    res = vb.adagrad_optimize(n_iters, obj, init, learning_rate=0.02, learning_rate_end=0.005)
+    # the same run as one device launch chain
+    run = vb.DeviceRun(obj, n_iters, init[None, :], 10, 0.02, 0.1, 0.005)
+    run.advance_philox(n_iters, seed, stream, step0)
+    _, hist, vals, smooth = run.result()
+    np.testing.assert_array_equal(res[2], vals[0])
+    np.testing.assert_array_equal(res[1], hist[0])
+    np.testing.assert_array_equal(res[0], smooth[0])
+    # interrupt after the first chunk (1000 steps): partial results
+    calls = []
+    orig = vb.DeviceRun.advance_philox
+
+    def interrupting(self, *a, **k):
+        if calls:
+            raise KeyboardInterrupt
+        calls.append(1)
+        return orig(self, *a, **k)
+    monkeypatch.setattr(vb.DeviceRun, 'advance_philox', interrupting)
+    fam2 = vb.mean_field_gaussian_variational_family(D, rng='philox')
+    obj2 = vb.black_box_klvi(fam2, targets.funnel(D), N)
+    seed2, stream2, step2 = fam2.seed, fam2.stream, fam2.step
+    part = vb.adagrad_optimize(n_iters, obj2, init, learning_rate=0.02, learning_rate_end=0.005)
+    assert part[2].shape == (1000,) and part[3].shape == (1000,)
+    monkeypatch.setattr(vb.DeviceRun, 'advance_philox', orig)
+    run2 = vb.DeviceRun(obj2, n_iters, init[None, :], 10, 0.02, 0.1, 0.005)
+    run2.advance_philox(1000, seed2, stream2, step2)
+    np.testing.assert_array_equal(part[2], run2.values()[:1000])
+    assert part[1].shape == (0, 2 * D) and np.all(np.isnan(part[0]))

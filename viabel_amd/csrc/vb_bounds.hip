@@ -40,6 +40,8 @@ __device__ __forceinline__ double block_max1(double v, double* red) {
   return r;
 }
 
+__global__ void set_scalar_kernel(double* p, double v) { *p = v; }
+
 int red_grid(long long n) {
   long long g = (n + 2047) / 2048;
   if (g < 1) g = 1;
@@ -205,7 +207,8 @@ __global__ void divergence_final(const double* part, int nb, long long n, double
 // ---- column means of x [n][d] ---------------------------------------------
 // grid (row chunks, column tiles of 64); block = 64 columns x 4 row lanes
 __global__ __launch_bounds__(256) void col_sum_kernel(const double* x, long long n, long long d,
-                                                      long long rows_per_chunk, double* part) {
+                                                      long long rows_per_chunk, double* part,
+                                                      const double* w = nullptr) {
   __shared__ double red[4][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const long long col = (long long)blockIdx.y * 64 + cl;
@@ -213,20 +216,22 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const double* x, long long
   const long long r1 = min(n, r0 + rows_per_chunk);
   double s = 0.0;
   if (col < d)
-    for (long long r = r0 + rl; r < r1; r += 4) s += x[r * d + col];
+    for (long long r = r0 + rl; r < r1; r += 4) s += w ? w[r] * x[r * d + col] : x[r * d + col];
   red[rl][cl] = s;
   __syncthreads();
   if (rl == 0 && col < d)
     part[(long long)blockIdx.x * d + col] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
 }
 
+// mean = column sums / n, or / *sw (the weight sum on the device)
 __global__ __launch_bounds__(256) void col_final_kernel(const double* part, int nchunk,
-                                                        long long n, long long d, double* mean) {
+                                                        long long n, long long d, double* mean,
+                                                        const double* sw = nullptr) {
   const long long col = (long long)blockIdx.x * 256 + threadIdx.x;
   if (col >= d) return;
   double s = 0.0;
   for (int k = 0; k < nchunk; ++k) s += part[(long long)k * d + col];
-  mean[col] = s / (double)n;
+  mean[col] = s / (sw ? *sw : (double)n);
 }
 
 // 1-D fast path: mean of x[n]
@@ -274,7 +279,7 @@ __global__ __launch_bounds__(256) void cpow_kernel(const double* x, long long n,
 // ---- covariance: one block row per (chunk, pair) ----------------------------
 __global__ __launch_bounds__(256) void cov_kernel(const double* x, long long n, long long d,
                                                   const double* mean, long long rows_per_chunk,
-                                                  double* part) {
+                                                  double* part, const double* w = nullptr) {
   __shared__ double red[4];
   const int pair = blockIdx.y;
   // pair -> (i, j), i <= j, row-major upper triangle
@@ -288,14 +293,18 @@ __global__ __launch_bounds__(256) void cov_kernel(const double* x, long long n, 
   const long long r1 = min(n, r0 + rows_per_chunk);
   const double mi = mean[i], mj = mean[j];
   double s = 0.0;
-  for (long long r = r0 + threadIdx.x; r < r1; r += 256)
-    s += (x[r * d + i] - mi) * (x[r * d + j] - mj);
+  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
+    const double c = (x[r * d + i] - mi) * (x[r * d + j] - mj);
+    s += w ? w[r] * c : c;
+  }
   s = block_sum1(s, red);
   if (threadIdx.x == 0) part[(long long)blockIdx.x * gridDim.y + pair] = s;
 }
 
+// cov = pair sums / (n - 1), or / *fact (np.cov's aweights normaliser, device)
 __global__ __launch_bounds__(256) void cov_final_kernel(const double* part, int nchunk, int npairs,
-                                                        long long n, long long d, double* cov) {
+                                                        long long n, long long d, double* cov,
+                                                        const double* fact = nullptr) {
   const int pair = blockIdx.x * 256 + threadIdx.x;
   if (pair >= npairs) return;
   int i = 0, rem = pair;
@@ -306,7 +315,7 @@ __global__ __launch_bounds__(256) void cov_final_kernel(const double* part, int 
   const int j = i + rem;
   double s = 0.0;
   for (int k = 0; k < nchunk; ++k) s += part[(long long)k * npairs + pair];
-  const double c = s / (double)(n - 1);
+  const double c = s / (fact ? *fact : (double)(n - 1));
   cov[(long long)i * d + j] = c;
   cov[(long long)j * d + i] = c;
 }
@@ -390,51 +399,150 @@ hipError_t bounds_centered_moments(const double* x, long long n, long long d, do
 }
 
 namespace {
-// mean_j = sum_n w_n x_nj / sw  (w null: plain mean); 4 waves split the rows
-__global__ __launch_bounds__(256) void wmean_kernel(const double* x, long long n, long long d,
-                                                    const double* w, double sw, double* mean) {
-  __shared__ double part[4][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long long j = (long long)blockIdx.x * 64 + lane;
-  double a = 0.0;
-  if (j < d)
-    for (long long r = wv; r < n; r += 4) a += (w ? w[r] : 1.0) * x[r * d + j];
-  part[wv][lane] = a;
-  __syncthreads();
-  if (wv == 0 && j < d) mean[j] = ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane])) / sw;
-}
-
 __global__ __launch_bounds__(256) void center_kernel(const double* x, long long n, long long d,
                                                      const double* mean, double* xc) {
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
   if (idx < n * d) xc[idx] = x[idx] - mean[idx % d];
 }
+
+// weights for np.cov(aweights) / np.average: with LOGW, w_i = exp(lw_i - max lw)
+// (improve_with_psis, notebooks/experiments.py:80-82) written to wout after a
+// max pass; partial sums of w and w^2 per block
+template <bool LOGW>
+__global__ __launch_bounds__(256) void wsum_kernel(const double* w, long long n, const double* mx,
+                                                   double* wout, double* part) {
+  __shared__ double red[4];
+  const double m = LOGW ? *mx : 0.0;
+  double a = 0.0, b = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    double v = w[i];
+    if (LOGW) {
+      v = exp(v - m);
+      wout[i] = v;
+    }
+    a += v;
+    b += v * v;
+  }
+  a = block_sum1(a, red);
+  b = block_sum1(b, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = a;
+    part[2 * blockIdx.x + 1] = b;
+  }
+}
+
+// sc[0] = sum w, sc[1] = fact (np.cov: sw - ddof sw2 / sw, or sw at ddof 0),
+// sc[2] = 1 / fact, sc[3] = 1 when sum w > 0 (else the caller reports an error)
+__global__ __launch_bounds__(256) void wsum_final(const double* part, int nb, int ddof,
+                                                  double* sc) {
+  __shared__ double red[4];
+  double a = 0.0, b = 0.0;
+  for (int k = threadIdx.x; k < nb; k += 256) {
+    a += part[2 * k];
+    b += part[2 * k + 1];
+  }
+  a = block_sum1(a, red);
+  b = block_sum1(b, red);
+  if (threadIdx.x == 0) {
+    const double fact = ddof == 0 ? a : a - ddof * b / a;
+    sc[0] = a;
+    sc[1] = fact;
+    sc[2] = 1.0 / fact;
+    sc[3] = a > 0.0 ? 1.0 : 0.0;
+  }
+}
+
+// max of lw (one value) for the LOGW weights
+__global__ __launch_bounds__(256) void max_part_kernel(const double* x, long long n, double* part) {
+  __shared__ double red[4];
+  double m = -INFINITY;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256)
+    m = fmax(m, x[i]);
+  m = block_max1(m, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = m;
+}
+
+__global__ __launch_bounds__(256) void max_final_kernel(const double* part, int nb, double* out) {
+  __shared__ double red[4];
+  double m = -INFINITY;
+  for (int k = threadIdx.x; k < nb; k += 256) m = fmax(m, part[k]);
+  m = block_max1(m, red);
+  if (threadIdx.x == 0) *out = m;
+}
 }  // namespace
 
-// np.cov(x.T, aweights=w, ddof=ddof): mean [d], cov [d][d] = Xc^T diag(w) Xc / fact,
-// fact = sw - ddof * sw2 / sw (aweights) or n - ddof; the product on fp64 MFMA.
+size_t bounds_wcov_scratch_doubles(long long n, long long d) {
+  return bounds_scratch_doubles(n, d) + (size_t)n * (size_t)d + (size_t)n + 2 * kRedBlocks + 64;
+}
+
+// np.average(x.T, axis=1, weights=w) and np.cov(x.T, aweights=w, ddof=ddof) for x
+// [n][d], everything on the device: w (raw weights, or log weights with logw:
+// exp(lw - max lw)) -> weight sums and np.cov's normaliser in device scalars ->
+// weighted column means (row-chunked partials) -> centred weighted products
+// (pairwise chunked reduction for d <= kCovDMax, else Xc^T diag(w) Xc on the
+// fp64 MFMA GEMM).  w null: the unweighted np.cov with ddof.  sc_out[4] (device)
+// receives the scalars (sc_out[3] = 0 when the weights sum to zero).
 hipError_t bounds_weighted_covariance(const double* x, long long n, long long d, const double* w,
-                                      double sw, double fact, double* xc_scratch, double* mean,
-                                      double* cov, hipStream_t s) {
-  hipLaunchKernelGGL(wmean_kernel, dim3((unsigned)((d + 63) / 64)), dim3(256), 0, s, x, n, d, w, sw,
-                     mean);
+                                      bool logw, int ddof, double* scratch, double* sc_out,
+                                      double* mean, double* cov, hipStream_t s) {
+  long long rpc;
+  const int nc = col_chunks(n, &rpc);
+  double* part = scratch;                                   // reductions
+  double* wbuf = scratch + bounds_scratch_doubles(n, d);    // [n] exp weights
+  double* xc = wbuf + n;                                    // [n][d] centred x (GEMM path)
+  double* red = xc + (size_t)n * d;                         // [2 kRedBlocks + 8]
+  const double* wv = w;
+  const int g = red_grid(n);
+  if (w) {
+    if (logw) {
+      hipLaunchKernelGGL(max_part_kernel, dim3(g), dim3(256), 0, s, w, n, red);
+      hipLaunchKernelGGL(max_final_kernel, dim3(1), dim3(256), 0, s, red, g, red + 2 * kRedBlocks);
+      hipLaunchKernelGGL(wsum_kernel<true>, dim3(g), dim3(256), 0, s, w, n,
+                         red + 2 * kRedBlocks, wbuf, red);
+      wv = wbuf;
+    } else {
+      hipLaunchKernelGGL(wsum_kernel<false>, dim3(g), dim3(256), 0, s, w, n, nullptr, nullptr, red);
+    }
+    hipLaunchKernelGGL(wsum_final, dim3(1), dim3(256), 0, s, red, g, ddof, sc_out);
+  }
+  const double* sw = w ? sc_out : nullptr;
+  const double* fact = w ? sc_out + 1 : nullptr;
+  hipLaunchKernelGGL(col_sum_kernel, dim3(nc, (unsigned)((d + 63) / 64)), dim3(256), 0, s, x, n, d,
+                     rpc, part, wv);
+  hipLaunchKernelGGL(col_final_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, s, part, nc,
+                     n, d, mean, sw);
+  if (d <= kCovDMax) {
+    const int npairs = (int)(d * (d + 1) / 2);
+    hipLaunchKernelGGL(cov_kernel, dim3(nc, npairs), dim3(256), 0, s, x, n, d, mean, rpc, part, wv);
+    if (!w) {
+      // unweighted with ddof: the (n - ddof) normaliser from a device scalar
+      hipLaunchKernelGGL(set_scalar_kernel, dim3(1), dim3(1), 0, s, sc_out + 1, (double)(n - ddof));
+      fact = sc_out + 1;
+    }
+    hipLaunchKernelGGL(cov_final_kernel, dim3((npairs + 255) / 256), dim3(256), 0, s, part, nc,
+                       npairs, n, d, cov, fact);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(center_kernel, dim3((unsigned)((n * d + 255) / 256)), dim3(256), 0, s, x, n, d,
-                     mean, xc_scratch);
-  GemmOp g{};
-  g.ta = true;
-  g.tb = false;
-  g.M = (int)d;
-  g.N = (int)d;
-  g.K = (int)n;
-  g.A = xc_scratch;
-  g.lda = d;
-  g.B = xc_scratch;
-  g.ldb = d;
-  g.C = cov;
-  g.ldc = d;
-  g.alpha = 1.0 / fact;
-  g.kscale = w;
-  hipError_t e = gemm(g, s);
+                     mean, xc);
+  GemmOp gm{};
+  gm.ta = true;
+  gm.tb = false;
+  gm.M = (int)d;
+  gm.N = (int)d;
+  gm.K = (int)n;
+  gm.A = xc;
+  gm.lda = d;
+  gm.B = xc;
+  gm.ldb = d;
+  gm.C = cov;
+  gm.ldc = d;
+  gm.alpha = w ? 1.0 : 1.0 / (double)(n - ddof);
+  gm.alpha_dev = w ? sc_out + 2 : nullptr;
+  gm.kscale = wv;
+  hipError_t e = gemm(gm, s);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }

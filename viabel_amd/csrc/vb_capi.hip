@@ -44,16 +44,34 @@ int fail(int code, const char* fmt, ...) {
     if (rc_ != VB_OK) return rc_; \
   } while (0)
 
-bool is_device_ptr(const void* p) {
-  if (!p) return false;
+// 0: host memory (staged through the context's buffers); 1: device memory the
+// context's GPU can use in place; -1: device memory of another GPU (rejected:
+// the kernels would read or write it across devices).  Entry points select the
+// context's device first (check_ctx), so hipGetDevice names it.
+int ptr_class(const void* p) {
+  if (!p) return 0;
   hipPointerAttribute_t at;
   hipError_t e = hipPointerGetAttributes(&at, p);
   if (e != hipSuccess) {
     (void)hipGetLastError();
-    return false;
+    return 0;
   }
-  return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged ||
-         at.type == hipMemoryTypeUnified;
+  if (at.type == hipMemoryTypeManaged || at.type == hipMemoryTypeUnified) return 1;
+  if (at.type != hipMemoryTypeDevice) return 0;
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess) return 1;
+  return at.device == cur ? 1 : -1;
+}
+
+bool is_device_ptr(const void* p) { return ptr_class(p) == 1; }
+
+int foreign_ptr_error(const void* p) {
+  hipPointerAttribute_t at;
+  int cur = -1;
+  (void)hipPointerGetAttributes(&at, p);
+  (void)hipGetDevice(&cur);
+  return fail(VB_EINVAL, "device pointer %p is on GPU %d but the context is on GPU %d", p,
+              at.device, cur);
 }
 
 struct DevBuf {
@@ -110,7 +128,9 @@ struct In {
       d = p;
       return VB_OK;
     }
-    if (is_device_ptr(p)) {
+    const int pc = ptr_class(p);
+    if (pc < 0) return foreign_ptr_error(p);
+    if (pc == 1) {
       d = p;
       return VB_OK;
     }
@@ -136,7 +156,9 @@ struct OutT {
       d = p;
       return VB_OK;
     }
-    if (is_device_ptr(p)) {
+    const int pc = ptr_class(p);
+    if (pc < 0) return foreign_ptr_error(p);
+    if (pc == 1) {
       d = p;
       return VB_OK;
     }
@@ -431,6 +453,7 @@ int vb_family_sample(vb_ctx* c, const vb_family* fam, const double* lam, int64_t
   VB_TRY(dl.stage(c, 0, lam, 2 * (size_t)fi.D));
   if (noise->kind == VB_NOISE_HOST) {
     if (!noise->eps) return fail(VB_EINVAL, "host noise requires eps");
+    if (ptr_class(noise->eps) < 0) return foreign_ptr_error(noise->eps);
     VB_TRY(dn.stage(c, 1, noise->eps, nd));
   }
   VB_TRY(dx.stage(c, 2, x_out, nd));
@@ -810,6 +833,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
   const size_t per_step = (size_t)N * D + (r->fr ? (size_t)N : 0);
   if (host) {
     if (!noise->eps) return fail(VB_EINVAL, "host noise requires eps");
+    if (ptr_class(noise->eps) < 0) return foreign_ptr_error(noise->eps);
     const size_t tot = per_step * n_steps * r->nprob;
     if (is_device_ptr(noise->eps)) {
       // used in place
@@ -1224,41 +1248,49 @@ int vb_centered_moments(vb_ctx* c, const double* x, int64_t n, int64_t d, double
   return VB_OK;
 }
 
-int vb_weighted_covariance(vb_ctx* c, const double* x, int64_t n, int64_t d, const double* w,
-                           int32_t ddof, double* mean_out, double* cov_out) {
+}  // extern "C"
+
+// np.cov(x.T, aweights=w, ddof) / np.average with w raw weights or (logw) log
+// weights normalised on the device as exp(lw - max lw); no O(n) host work
+static int weighted_cov_impl(vb_ctx* c, const double* x, int64_t n, int64_t d, const double* w,
+                             bool logw, int32_t ddof, double* mean_out, double* cov_out) {
   VB_TRY(check_ctx(c));
   if (!x || !cov_out || n < 1 || d < 1) return fail(VB_EINVAL, "invalid argument");
   if (d > (1LL << 30) || n > (1LL << 31)) return fail(VB_EINVAL, "sizes out of range");
   In dx, dw;
   VB_TRY(dx.stage(c, 0, x, (size_t)n * d));
-  double sw = (double)n, fact = (double)(n - ddof);
-  if (w) {
-    // weight sums on the host copy (n values; the caller's vector)
-    std::vector<double> hw((size_t)n);
-    VB_HIP(hipMemcpyAsync(hw.data(), w, sizeof(double) * n, hipMemcpyDefault, c->stream));
-    VB_TRY(sync(c));
-    double s1 = 0.0, s2 = 0.0;
-    for (double v : hw) {
-      s1 += v;
-      s2 += v * v;
-    }
-    if (!(s1 > 0)) return fail(VB_EINVAL, "weights sum to zero");
-    sw = s1;
-    fact = ddof == 0 ? s1 : s1 - ddof * s2 / s1;   // numpy.cov with aweights
-    VB_TRY(dw.stage(c, 6, w, (size_t)n));
-  }
-  VB_TRY(c->slot[1].reserve(sizeof(double) * (size_t)n * d));
-  VB_TRY(c->slot[4].reserve(sizeof(double) * d));
+  if (w) VB_TRY(dw.stage(c, 6, w, (size_t)n));
+  VB_TRY(c->slot[1].reserve(sizeof(double) * vbk::bounds_wcov_scratch_doubles(n, d)));
+  VB_TRY(c->slot[4].reserve(sizeof(double) * ((size_t)d + 8)));
   double* mdev = c->slot[4].d();
+  double* sc = mdev + d;
   Out dm, dc;
   VB_TRY(dm.stage(c, 5, mean_out, mean_out ? (size_t)d : 0));
   VB_TRY(dc.stage(c, 2, cov_out, (size_t)d * d));
-  VB_HIP(vbk::bounds_weighted_covariance(dx.d, n, d, w ? dw.d : nullptr, sw, fact, c->slot[1].d(),
-                                         mdev, dc.d, c->stream));
+  VB_HIP(vbk::bounds_weighted_covariance(dx.d, n, d, w ? dw.d : nullptr, logw, ddof,
+                                         c->slot[1].d(), sc, mdev, dc.d, c->stream));
   if (mean_out) VB_HIP(hipMemcpyAsync(dm.d, mdev, sizeof(double) * d, hipMemcpyDeviceToDevice, c->stream));
+  double hsc[4] = {0.0, 0.0, 0.0, 1.0};
+  if (w) VB_HIP(hipMemcpyAsync(hsc, sc, sizeof(hsc), hipMemcpyDeviceToHost, c->stream));
   VB_TRY(dm.finish(c));
   VB_TRY(dc.finish(c));
-  return sync(c);
+  VB_TRY(sync(c));
+  if (!(hsc[3] > 0)) return fail(VB_EINVAL, "weights sum to zero");
+  return VB_OK;
+}
+
+extern "C" {
+
+int vb_weighted_covariance(vb_ctx* c, const double* x, int64_t n, int64_t d, const double* w,
+                           int32_t ddof, double* mean_out, double* cov_out) {
+  return weighted_cov_impl(c, x, n, d, w, false, ddof, mean_out, cov_out);
+}
+
+int vb_weighted_covariance_logw(vb_ctx* c, const double* x, int64_t n, int64_t d,
+                                const double* log_w, int32_t ddof, double* mean_out,
+                                double* cov_out) {
+  if (!log_w) return fail(VB_EINVAL, "null log weights");
+  return weighted_cov_impl(c, x, n, d, log_w, true, ddof, mean_out, cov_out);
 }
 
 int vb_covariance(vb_ctx* c, const double* x, int64_t n, int64_t d, double* mean_out,
@@ -1437,6 +1469,19 @@ int vb_iterate_average(vb_ctx* c, const double* x, int64_t n, int64_t ld, int64_
   Out dout;
   VB_TRY(dout.stage(c, 1, out, (size_t)(n - start) * cols));
   VB_HIP(vbk::launch_iterate_average(dx.d, n, ld, cols, start, dout.d, c->stream));
+  VB_TRY(dout.finish(c));
+  return sync(c);
+}
+
+int vb_sumlogs_rows(vb_ctx* c, const double* x, int64_t rows, int64_t n, double* out) {
+  VB_TRY(check_ctx(c));
+  if (!x || !out || n < 1 || rows < 1) return fail(VB_EINVAL, "invalid argument");
+  In dx;
+  VB_TRY(dx.stage(c, 0, x, (size_t)rows * n));
+  VB_TRY(c->slot[3].reserve(vbk::psis_sumlogs_rows_scratch_bytes(rows, n)));
+  Out dout;
+  VB_TRY(dout.stage(c, 1, out, (size_t)rows));
+  VB_HIP(vbk::psis_sumlogs_rows(dx.d, rows, n, c->slot[3].p, dout.d, c->stream));
   VB_TRY(dout.finish(c));
   return sync(c);
 }

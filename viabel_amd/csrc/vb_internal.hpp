@@ -131,9 +131,10 @@ hipError_t bounds_centered_moments(const double* x, long long n, long long d,
 hipError_t bounds_covariance(const double* x, long long n, long long d, double* dev_scratch,
                              double* mean_dev, double* cov_dev, hipStream_t s);
 size_t bounds_scratch_doubles(long long n, long long d);
+size_t bounds_wcov_scratch_doubles(long long n, long long d);
 hipError_t bounds_weighted_covariance(const double* x, long long n, long long d, const double* w,
-                                      double sw, double fact, double* xc_scratch, double* mean,
-                                      double* cov, hipStream_t s);
+                                      bool logw, int ddof, double* scratch, double* sc_out,
+                                      double* mean, double* cov, hipStream_t s);
 constexpr int kCovDMax = 64;
 
 // PSIS (vb_psis.hip)
@@ -148,6 +149,9 @@ hipError_t psis_gpdfit(const double* x, long long n, void* scratch, double* out4
                        double* ks_out, double* w_out, hipStream_t s);
 hipError_t psis_gpinv(const double* p, long long n, double k, double sigma, double* out,
                       hipStream_t s);
+size_t psis_sumlogs_rows_scratch_bytes(long long rows, long long n);
+hipError_t psis_sumlogs_rows(const double* x, long long rows, long long n, void* scratch,
+                             double* out, hipStream_t s);
 hipError_t psis_sumlogs(const double* x, long long n, void* scratch, double* out, hipStream_t s);
 
 }  // namespace vbk

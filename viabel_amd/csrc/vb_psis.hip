@@ -21,6 +21,8 @@
 #include "vb_device.hpp"
 #include "vb_internal.hpp"
 
+#include <algorithm>
+
 #include <hipcub/hipcub.hpp>
 
 #include <cfloat>
@@ -755,6 +757,42 @@ hipError_t psis_gpinv(const double* p, long long n, double k, double sigma, doub
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(gpinv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, n, k,
                      sigma, out);
+  return hipGetLastError();
+}
+
+// sumlogs of `rows` contiguous rows of n values (row r at x + r n) in one launch
+// chain: every kernel takes its row from blockIdx.y; per-row scratch (partials +
+// max) sb bytes apart; out[r] dense
+__global__ __launch_bounds__(256) void lse_rows_final_kernel(const double* part, int nb,
+                                                             const double* mx, double* out,
+                                                             long long sb) {
+  __shared__ double red[16];
+  part = colp(part, sb);
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 256) s += part[b];
+  s = bsum(s, red);
+  if (threadIdx.x == 0) out[blockIdx.y] = log(s) + *colp(mx, sb);
+}
+
+size_t psis_sumlogs_rows_scratch_bytes(long long rows, long long n) {
+  return (size_t)rows * (size_t)(psis_grid(n) + 8) * sizeof(double);
+}
+
+hipError_t psis_sumlogs_rows(const double* x, long long rows, long long n, void* scratch,
+                             double* out, hipStream_t s) {
+  const int g = psis_grid(n);
+  const long long sb = (long long)(g + 8) * (long long)sizeof(double);
+  double* part = static_cast<double*>(scratch);
+  double* mx = part + g;
+  for (long long r0 = 0; r0 < rows; r0 += 65535) {
+    const unsigned R = (unsigned)std::min<long long>(65535, rows - r0);
+    const double* xr = x + r0 * n;
+    hipLaunchKernelGGL(col_max_kernel, dim3(g, R), dim3(256), 0, s, xr, n, 1LL, n, part, sb);
+    hipLaunchKernelGGL(max_final_kernel, dim3(1, R), dim3(256), 0, s, part, g, mx, sb);
+    hipLaunchKernelGGL(sumexp_kernel, dim3(g, R), dim3(256), 0, s, xr, n, 1LL, n, mx, part, sb);
+    hipLaunchKernelGGL(lse_rows_final_kernel, dim3(1, R), dim3(256), 0, s, part, g, mx, out + r0,
+                       sb);
+  }
   return hipGetLastError();
 }
 

@@ -1,6 +1,7 @@
 """Log-weight producer of the reference's experiment harness, on the device.
 
   check_accuracy                notebooks/experiments.py:26-48 (host algebra on d x d)
+  check_approx_accuracy         notebooks/experiments.py:51-55
   get_samples_and_log_weights   notebooks/experiments.py:60-63
   psis_correction               notebooks/experiments.py:66-70
   improve_with_psis             notebooks/experiments.py:73-89
@@ -16,7 +17,7 @@ from .psis import psislw
 from .targets import Target
 
 __all__ = ['get_samples_and_log_weights', 'psis_correction', 'log_weights', 'check_accuracy',
-           'improve_with_psis', 'weighted_mean_and_cov']
+           'check_approx_accuracy', 'improve_with_psis', 'weighted_mean_and_cov']
 
 
 def log_weights(logdensity, var_family, var_param, n_samples, return_samples=True,
@@ -57,14 +58,23 @@ def psis_correction(logdensity, var_family, var_param, n_samples):
     return samples.T, smoothed_log_weights, khat
 
 
-def weighted_mean_and_cov(samples, weights=None, ddof=1):
+def weighted_mean_and_cov(samples, weights=None, ddof=1, log_weights=None):
     """Device np.average(samples.T, axis=1, weights) and np.cov(samples.T,
-    aweights=weights, ddof=ddof) for samples [n, d]."""
+    aweights=weights, ddof=ddof) for samples [n, d].  `log_weights` instead of
+    `weights`: the weights are exp(log_weights - max), formed on the device."""
     x = nat.as_f64(np.atleast_2d(np.asarray(samples, dtype=float).T).T)
     n, d = x.shape
-    w = None if weights is None else nat.as_f64(np.ravel(weights))
     mean = np.empty(d)
     cov = np.empty((d, d))
+    if log_weights is not None:
+        if weights is not None:
+            raise ValueError('give weights or log_weights, not both')
+        lw = nat.as_f64(np.ravel(log_weights))
+        nat.check(nat.lib().vb_weighted_covariance_logw(nat.context().handle, nat.dptr(x), n, d,
+                                                        nat.dptr(lw), int(ddof), nat.dptr(mean),
+                                                        nat.dptr(cov)))
+        return mean, cov
+    w = None if weights is None else nat.as_f64(np.ravel(weights))
     nat.check(nat.lib().vb_weighted_covariance(nat.context().handle, nat.dptr(x), n, d,
                                                nat.dptr(w), int(ddof), nat.dptr(mean),
                                                nat.dptr(cov)))
@@ -95,6 +105,11 @@ def check_accuracy(true_mean, true_cov, approx_mean, approx_cov, verbose=False, 
     return results
 
 
+def check_approx_accuracy(var_family, var_param, true_mean, true_cov, verbose=False, name=None):
+    """experiments.py:51-55: check_accuracy of the family's (mean, cov) at var_param."""
+    return check_accuracy(true_mean, true_cov, *var_family.mean_and_cov(var_param), verbose, name)
+
+
 def improve_with_psis(logdensity, var_family, var_param, n_samples, true_mean, true_cov,
                       transform=None, verbose=False):
     """experiments.py:73-89: PSIS-reweighted mean and covariance (ddof 0) of
@@ -106,10 +121,9 @@ def improve_with_psis(logdensity, var_family, var_param, n_samples, true_mean, t
         print()
     if transform is not None:
         samples = transform(samples)
-    slw = slw - np.max(slw)
-    wts = np.exp(slw)
-    wts /= np.sum(wts)
-    approx_mean, approx_cov = weighted_mean_and_cov(np.asarray(samples).T, wts, ddof=0)
+    # weights exp(slw - max slw) / sum (experiments.py:80-82) are formed on the device
+    approx_mean, approx_cov = weighted_mean_and_cov(np.asarray(samples).T, log_weights=slw,
+                                                    ddof=0)
     res = check_accuracy(true_mean, true_cov, approx_mean, approx_cov, verbose)
     res['khat'] = khat
     return res, approx_mean, approx_cov

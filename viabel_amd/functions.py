@@ -94,7 +94,9 @@ def stochastic_iterate_averaging(estimate, start):
     N, cols = x.shape
     start = int(start)
     if N - start <= 0:
-        raise ValueError('Start of stationary distribution must be lower than number of iterates')
+        # the reference raises a bare str (functions.py:70-71), which Python
+        # turns into a TypeError; same exception type here, with the message
+        raise TypeError('Start of stationary distribution must be lower than number of iterates')
     out = np.empty((N - start, cols))
     nat.check(nat.lib().vb_iterate_average(nat.context().handle, nat.dptr(x), N, cols, cols, start,
                                            nat.dptr(out)))

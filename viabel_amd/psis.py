@@ -152,8 +152,11 @@ def sumlogs(x, axis=None, out=None):
         res = _sumlogs_1d(x.ravel())
     else:
         moved = np.moveaxis(x, axis, -1)
-        flat = moved.reshape(-1, moved.shape[-1])
-        res = np.array([_sumlogs_1d(row) for row in flat]).reshape(moved.shape[:-1])
+        flat = nat.as_f64(moved.reshape(-1, moved.shape[-1]))
+        res = np.empty(flat.shape[0])
+        nat.check(nat.lib().vb_sumlogs_rows(nat.context().handle, nat.dptr(flat), flat.shape[0],
+                                            flat.shape[1], nat.dptr(res)))
+        res = res.reshape(moved.shape[:-1])
     if out is not None:
         out[...] = res
         return out

@@ -27,7 +27,7 @@ import numpy as np
 from . import _native as nat
 
 __all__ = ['Target', 'isogauss', 'mixture', 'funnel', 'eight_schools_ncp', 'corr_gauss',
-           'callback', 'from_stan', 'torch_target']
+           'callback', 'from_stan', 'torch_target', 'as_target']
 
 
 class Target:
@@ -156,3 +156,30 @@ def torch_target(logdensity, dim=None, device=None):
         g, = torch.autograd.grad(lp.sum(), xt)
         return lp.detach().cpu().numpy(), g.cpu().numpy()
     return callback(f, dim, 'torch')
+
+
+def as_target(logdensity, dim):
+    """The reference accepts any differentiable callable as logdensity
+    (vb.py:236-241, 249-253).  A device target passes through; a plain callable
+    that torch can differentiate (logdensity(x: tensor (n, dim)) -> tensor (n,)
+    with a grad_fn) is wrapped with torch_target; anything else -- e.g. an
+    autograd.numpy function, whose derivatives only autograd can take -- raises
+    TypeError."""
+    if isinstance(logdensity, Target):
+        return logdensity
+    msg = ('logdensity must be a viabel_amd.targets target, a user model wrapped with '
+           'targets.callback / targets.from_stan, or a callable that torch can differentiate '
+           '(x: tensor (n, dim) -> tensor (n,)); got %r' % (logdensity,))
+    if not callable(logdensity) or dim is None:
+        raise TypeError(msg)
+    try:
+        import torch
+        dev = torch.device('cuda' if torch.cuda.is_available() else 'cpu')
+        x = torch.zeros((2, int(dim)), dtype=torch.float64, device=dev, requires_grad=True)
+        out = logdensity(x)
+        ok = (isinstance(out, torch.Tensor) and out.requires_grad and tuple(out.shape) == (2,))
+    except Exception as e:       # the probe failed: not a torch-differentiable callable
+        raise TypeError(msg + ' (probe: %s: %s)' % (type(e).__name__, e)) from None
+    if not ok:
+        raise TypeError(msg)
+    return torch_target(logdensity, int(dim))

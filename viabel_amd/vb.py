@@ -36,6 +36,7 @@ from collections import namedtuple
 import numpy as np
 
 from . import _native as nat
+from . import targets as _targets
 from .targets import Target
 
 __all__ = [
@@ -274,13 +275,9 @@ class NativeObjective:
     def __init__(self, kind, var_family, logdensity, n_samples, alpha=None):
         if not isinstance(var_family, NativeVariationalFamily):
             raise TypeError('var_family must come from viabel_amd.vb')
-        if not isinstance(logdensity, Target):
-            raise TypeError(
-                'the device estimator needs a viabel_amd.targets target as logdensity: a '
-                'built-in device target, or a user model wrapped with targets.callback / '
-                'targets.from_stan / targets.torch_target (an autograd callable cannot be '
-                'differentiated here); got %r' % (logdensity,))
-        logdensity = logdensity.bind(var_family.dim)
+        # device targets pass through; torch-differentiable callables are wrapped
+        # (targets.as_target); anything else raises TypeError
+        logdensity = _targets.as_target(logdensity, var_family.dim).bind(var_family.dim)
         if logdensity.dim != var_family.dim:
             raise ValueError('target dimension %d != family dimension %d'
                              % (logdensity.dim, var_family.dim))
@@ -448,6 +445,13 @@ class DeviceRun:
                                           nat.dptr(vals), nat.dptr(smooth)))
         return lam, hist, vals, smooth
 
+    def values(self):
+        """Objective values of problem 0 so far ([n_iters], steps not yet run are
+        undefined)."""
+        vals = np.empty((self.n_problems, self.n_iters))
+        nat.check(nat.lib().vb_run_result(self.handle, None, None, nat.dptr(vals), None))
+        return vals[0]
+
     def synchronize(self):
         nat.context().synchronize()
 
@@ -459,25 +463,60 @@ class DeviceRun:
             pass
 
 
+def _progress(n_iters):
+    """The reference's tqdm.trange progress bar (vb.py:354), or None without
+    tqdm; VIABEL_AMD_PROGRESS=0 turns it off."""
+    if os.environ.get('VIABEL_AMD_PROGRESS', '1') == '0':
+        return None
+    try:
+        import tqdm
+    except ImportError:
+        return None
+    return tqdm.tqdm(total=n_iters)
+
+
 def _native_adagrad(n_iters, obj, init_param, window, learning_rate, epsilon,
                     learning_rate_end):
+    """The device-resident loop in chunks of about a tenth of the run (>= 1000
+    steps): between chunks the progress bar shows the reference's 'Average Loss'
+    (mean of the last 1000 values, vb.py:378-381), and a KeyboardInterrupt stops
+    the run with the steps done so far, like the reference's (vb.py:382-389)."""
     fam = obj.family
     run = DeviceRun(obj, n_iters, init_param[None, :], window, learning_rate, epsilon,
                     learning_rate_end)
-    if fam.rng == 'philox':
-        run.advance_philox(n_iters, fam.seed, fam.stream, fam.step)
-        fam.step += n_iters
-    else:
+    chunk = max(1000, -(-n_iters // 10))
+    if fam.rng != 'philox':
         per_step = obj.n_samples * (fam.dim + 1)
-        chunk = max(1, min(n_iters, _HOST_CHUNK_ELEMS // max(per_step, 1)))
-        done = 0
+        chunk = max(1, min(chunk, _HOST_CHUNK_ELEMS // max(per_step, 1)))
+    bar = _progress(n_iters)
+    done = 0
+    try:
         while done < n_iters:
             cs = min(chunk, n_iters - done)
-            eps = np.stack([obj._eps_one_call() for _ in range(cs)])
-            run.advance_host(eps[None])
+            if fam.rng == 'philox':
+                run.advance_philox(cs, fam.seed, fam.stream, fam.step)
+                fam.step += cs
+            else:
+                run.advance_host(np.stack([obj._eps_one_call() for _ in range(cs)])[None])
             done += cs
+            if bar is not None:
+                vals = run.values()
+                bar.update(cs)
+                bar.set_description('Average Loss = {:,.5g}'.format(
+                    np.mean(vals[max(0, done - 1 - 1000):done])))
+    except KeyboardInterrupt:
+        pass
+    finally:
+        if bar is not None:
+            bar.close()
     _, hist, vals, smooth = run.result()
-    return smooth[0], hist[0], vals[0], np.zeros(n_iters)
+    if done == n_iters:
+        return smooth[0], hist[0], vals[0], np.zeros(n_iters)
+    # interrupted: what the reference returns at that point
+    rows = max(0, done - 3 * n_iters // 4)
+    hist = hist[0, :rows]
+    smoothed = np.mean(hist, axis=0) if rows else np.full(run.P, np.nan)
+    return smoothed, hist, vals[0, :done], np.zeros(done)
 
 
 def _foreign_adagrad(n_iters, objective_and_grad, init_param, has_log_norm, window,
