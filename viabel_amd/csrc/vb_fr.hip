@@ -210,19 +210,25 @@ __global__ __launch_bounds__(1024) void fr_weights_kernel(int N, int D, int chiv
   }
 }
 
-// gmu[j] = sum_n r_n G[n][j]: 64 columns per block, the 4 waves take every
-// 4th row, fixed-order combine in LDS
-__global__ __launch_bounds__(256) void fr_colsum_kernel(int N, int D, const double* r,
-                                                        const double* G, double* out) {
-  __shared__ double part[4][64];
+// gmu[j] = sum_n r_n G[n][j]: 64 columns per block, the 16 waves take every
+// 16th row, fixed-order combine in LDS
+__global__ __launch_bounds__(1024) void fr_colsum_kernel(int N, int D, const double* r,
+                                                         const double* G, double* out) {
+  __shared__ double part[16][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + lane;
   double a = 0.0;
   if (j < D)
-    for (int n = wv; n < N; n += 4) a += r[n] * G[(long long)n * D + j];
+    for (int n = wv; n < N; n += 16) a += r[n] * G[(long long)n * D + j];
   part[wv][lane] = a;
   __syncthreads();
-  if (wv == 0 && j < D) out[j] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  if (wv == 0 && j < D) {
+    double t[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      t[q] = (part[4 * q][lane] + part[4 * q + 1][lane]) + (part[4 * q + 2][lane] + part[4 * q + 3][lane]);
+    out[j] = (t[0] + t[1]) + (t[2] + t[3]);
+  }
 }
 
 // grad[D + i(i+1)/2 + j] = G_L[i][j] (j < i), G_L[i][i] L[i][i] + 2 scal[1] (exp on
@@ -235,7 +241,7 @@ __global__ __launch_bounds__(256) void fr_pack_kernel(int D, const double* GL, c
                                                       double* grad) {
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
   if (idx == 0) {
-    if (!sc->ns_conv) sc->status |= 1;
+    if (!sc->ns_conv && !sc->ns_fin) sc->status |= 1;
     if (!sc->pcg_done) {
       double rr = 0.0;
       for (int k = 0; k < n_rr; ++k) rr += rr_part[k];
@@ -279,16 +285,6 @@ __global__ __launch_bounds__(256) void fr_logq_kernel(int D, long long n, const 
   }
   a = wave_sum(a);
   if (lane == 0) out[row] = (t_const - scal[0]) - 0.5 * (df + D) * log(1.0 + a / df);
-}
-
-// 0.5 log det Sigma = sum_i log L_ii = the sum of the free log-diagonal entries
-__global__ __launch_bounds__(1024) void fr_logdet_lam_kernel(int D, const double* lam,
-                                                             double* scal) {
-  __shared__ double red[16];
-  double a = 0.0;
-  for (int i = threadIdx.x; i < D; i += blockDim.x) a += lam[D + (long long)i * (i + 1) / 2 + i];
-  a = block_sum(a, red);
-  if (threadIdx.x == 0) scal[0] = a;
 }
 
 // *out = ||X - shift I||_F^2 for an n x n X.  Per-block partials; the last block
@@ -385,6 +381,7 @@ struct FrSched {
   double rz[2], ee;              // PCG: <R, M^-1 R> (by iteration parity), ||E||^2
   double l0, lmax_est;
   int ns_conv, ns_iter, pcg_done, pcg_iter;
+  int ns_fin;                    // the last Newton-Schulz update was final (see fr_sqrt)
   int status;                    // sticky: 1 NS not converged, 2 PCG not converged
   int hint_ns, hint_pcg;         // sticky maxima of the iteration counts
   int warm_step;                 // this root was warm-started (its count feeds hint_ns)
@@ -422,23 +419,29 @@ __global__ __launch_bounds__(256) void fr_power2_kernel(int D, const double* Sig
 __device__ double ns_alpha(double l) { return sqrt(3.0 / (1.0 + l + l * l)); }
 
 // One block: c, l_0 and the whole schedule; resets the per-step flags.
+// Also scal[0] = 0.5 log det Sigma = sum_i log L_ii, the free log-diagonal of lam.
 __global__ __launch_bounds__(256) void fr_sched_kernel(int D, int kmax, const double* fro_part,
                                                        int n_part, const double* y,
                                                        const double* v, int has_z,
-                                                       double l_default, FrSched* sc) {
+                                                       double l_default, FrSched* sc,
+                                                       const double* lam, double* scal) {
   __shared__ double red[16];
-  double f = 0.0, ly = 0.0, lv = 0.0;
+  double f = 0.0, ly = 0.0, lv = 0.0, ld = 0.0;
   for (int i = threadIdx.x; i < n_part; i += 256) f += fro_part[i];
   for (int i = threadIdx.x; i < D; i += 256) {
     ly += y[i] * y[i];
     if (has_z) lv += v[i] * v[i];
+    ld += lam[D + (long long)i * (i + 1) / 2 + i];
   }
   f = block_sum(f, red);
   __syncthreads();
   ly = block_sum(ly, red);
   __syncthreads();
   lv = block_sum(lv, red);
+  __syncthreads();
+  ld = block_sum(ld, red);
   if (threadIdx.x != 0) return;
+  scal[0] = ld;
   const double lmax = sqrt(ly);                  // ||Sigma x|| for unit x <= lambda_max
   const double c = fmin(1.25 * lmax, sqrt(f));   // ||Sigma||_F >= lambda_max
   double l = l_default;
@@ -469,6 +472,7 @@ __global__ __launch_bounds__(256) void fr_sched_kernel(int D, int kmax, const do
     l = fmin(0.5 * a * l * (3.0 - a2 * l * l), 1.0);
   }
   sc->ns_conv = 0;
+  sc->ns_fin = 0;
   sc->ns_iter = -1;
   sc->warm_step = has_z;
   sc->pcg_done = 0;
@@ -779,7 +783,6 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm) {
   const int nblk = ((D + 31) / 32) * ((D + 31) / 32);
   FrSched* sc = static_cast<FrSched*>(W->sched.p);
   hipLaunchKernelGGL(fr_unpack_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, lam, W->L.d());
-  hipLaunchKernelGGL(fr_logdet_lam_kernel, dim3(1), dim3(1024), 0, st, D, lam, W->scal.d());
   {
     GemmOp g = mm(D, D, D, W->L.d(), false, W->L.d(), true, W->Sig.d());
     g.sq_part = W->fro_part.d();
@@ -804,12 +807,12 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm) {
   // costs only its launch); others at least 12 (l_0 = 0.05 needs ~9 at rounding
   // level)
   const int kmax =
-      std::min(warm ? std::max(W->ns_kmax + 2, 6) : std::max(W->ns_kmax, 12), kFrNSMax);
+      std::min(warm ? std::max(W->ns_kmax + 2, 6) : std::max(W->ns_kmax + 1, 12), kFrNSMax);
   W->last_warm = warm;
   W->last_kmax = kmax;
   hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(256), 0, st, D, kmax, W->fro_part.d(),
                      4 * nblk, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), hz ? 1 : 0, 0.05,
-                     sc);
+                     sc, lam, W->scal.d());
   // iteration 0: Y_1 -> Yb[1], Z_1 -> Zb[1]
   {
     GemmOp g = mm(D, D, D, W->Sig.d(), false, W->Sig.d(), false, W->Yb[1].d());
@@ -826,6 +829,7 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm) {
     t.sq_part = tp;
     t.sq_shift_dev = &sc->shift[k];
     t.skip_flag = &sc->ns_conv;
+    t.skip_flag2 = &sc->ns_fin;
     FR_HIP(gemm(t, st));
     GemmOp yz[2] = {mm(D, D, D, Yk, false, W->T.d(), false, W->Yb[(k + 1) & 1].d()),
                     mm(D, D, D, W->T.d(), false, Zk, false, W->Zb[(k + 1) & 1].d())};
@@ -833,11 +837,20 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm) {
       GemmOp& g = yz[o];
       g.alpha_dev = &sc->halpha[k];
       g.skip_flag = &sc->ns_conv;
-      g.copy_src = o == 0 ? Yk : Zk;
+      // the root ends in buffer (kmax + 1) & 1: the first skipped launch copies
+      // it there when it sits in the other one
+      g.copy_src = ((k & 1) != ((kmax + 1) & 1)) ? (o == 0 ? Yk : Zk) : nullptr;
+      g.copy_if_iter = k;
       g.conv_part = tp;
       g.conv_n = 4 * nblk;
       g.conv_scale_dev = &sc->inv_a4[k];
       g.conv_tol2 = 1e-20 * D;
+      // ||I - Z_k Y_k||_F <= 1e-5: the residual after this update is at most
+      // 0.75 ||E||_F ||E||_2 <= 7.5e-11 (e' = (3 e^2 + e^3) / 4 per eigenvalue),
+      // below the 1e-10 sqrt(D) bar, so this update is the last one (saves the
+      // detection-only T_{k+1} product; the root is the same iterate)
+      g.fin_flag = &sc->ns_fin;
+      g.conv_fin_tol2 = 1e-10;
       if (k >= 2) {
         g.conv_prev_part = W->tpart[(k - 1) & 1].d();
         g.conv_prev_scale_dev = &sc->inv_a4[k - 1];
@@ -982,7 +995,7 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
   GemmOp g = mm(D, D, N, z, true, W->G.d(), false, W->GS.d());
   g.kscale = W->rk.d();
   FR_HIP(gemm(g, st));
-  hipLaunchKernelGGL(fr_colsum_kernel, dim3(blocks(D, 64)), dim3(256), 0, st, N, D, W->r.d(),
+  hipLaunchKernelGGL(fr_colsum_kernel, dim3(blocks(D, 64)), dim3(1024), 0, st, N, D, W->r.d(),
                      W->G.d(), grad);
   // Sylvester solve (sqrtm VJP): X, symmetric Sigma cotangent of the sample term
   if (int rc = fr_pcg(W, D, st)) return rc;
@@ -1400,16 +1413,16 @@ int fr_info(FrWork* W, hipStream_t st) {
   const FrSched& h = *W->host_sched;
   FrSched* d = static_cast<FrSched*>(W->sched.p);
   FR_HIP(hipMemsetAsync(&d->status, 0, 3 * sizeof(int), st));
-  if ((h.status & 1) || !h.ns_conv)
+  if ((h.status & 1) || (!h.ns_conv && !h.ns_fin))
     return vb_set_error(-2, "Newton-Schulz square root of Sigma did not converge in %d iterations "
                             "(Sigma too ill-conditioned)", W->last_kmax);
   if (h.status & 2)
     return vb_set_error(-2, "conjugate gradients for the sqrtm gradient did not converge in %d "
                             "iterations", W->pcg_kmax);
   if (W->last_warm && h.hint_ns > 0)
-    W->ns_kmax = std::min(kFrNSMax, std::max(h.hint_ns, h.ns_iter) + 1);
+    W->ns_kmax = std::min(kFrNSMax, std::max(h.hint_ns, h.ns_iter));
   if (W->last_warm && h.hint_pcg >= 0)
-    W->pcg_kmax = std::min(40, std::max(h.hint_pcg, h.pcg_iter) + 3);
+    W->pcg_kmax = std::min(40, std::max(h.hint_pcg, h.pcg_iter) + 2);
   return 0;
 }
 

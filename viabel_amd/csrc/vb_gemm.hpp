@@ -66,6 +66,16 @@ struct GemmOp {
   double conv_stall_tol2;
   int* conv_iter_out;
   int conv_iter;
+  // finish-after-update (Newton-Schulz): when the test sum s <= conv_fin_tol2 *
+  // ref (and the skip test failed) the block computes its tile as usual and sets
+  // *fin_flag = 1 and *conv_iter_out = conv_iter + 1: the next iterate is final.
+  // Later launches name fin_flag as skip_flag2: they skip (setting *skip_flag).
+  int* fin_flag;
+  double conv_fin_tol2;
+  const int* skip_flag2;
+  // copy_src applies only when *conv_iter_out == copy_if_iter (-1: always), i.e.
+  // only in the first skipped launch after convergence
+  int copy_if_iter;
   // optional: per-wave partial sums of dot_with_ij * C_ij (before beta), 4 per block
   const double* dot_with;
   double* dot_part;
@@ -86,13 +96,17 @@ namespace gemm_detail {
 using d4 = double __attribute__((ext_vector_type(4)));
 constexpr int BT = 32;   // block tile (rows and columns)
 #ifndef VB_GEMM_KT
-#define VB_GEMM_KT 64
+#define VB_GEMM_KT 32
 #endif
 constexpr int KT = VB_GEMM_KT;  // k tile
 constexpr int SR = KT + 4;      // [row][k] stride
 constexpr int SK = BT + 16;     // [k][row] stride
 constexpr int BUF = (BT * SR > KT * SK) ? BT * SR : KT * SK;  // doubles per operand buffer
-constexpr int NTH = 512;                                       // 8 waves
+#ifndef VB_GEMM_KSPLIT
+#define VB_GEMM_KSPLIT 2
+#endif
+constexpr int KS_ = VB_GEMM_KSPLIT;                            // k parts of each tile
+constexpr int NTH = 256 * KS_;                                 // 4 quadrants x KS_ waves
 constexpr int PER = BT * KT / NTH;                             // elements per thread per tile
 
 // One operand tile (BT rows x KT k) of a row-major matrix X with leading
@@ -151,17 +165,21 @@ __device__ __forceinline__ bool gemm_skip(const GemmOp& g, double* red) {
     }
     if ((t & 63) == 0) {
       red[t >> 6] = a;
-      red[8 + (t >> 6)] = b;
+      red[NTH / 64 + (t >> 6)] = b;
     }
   }
   __syncthreads();
   if (t == 0) {
     int sk = *g.skip_flag != 0;
+    if (!sk && g.skip_flag2 && *g.skip_flag2 != 0) {
+      sk = 1;
+      *g.skip_flag = 1;
+    }
     if (!sk && g.conv_part) {
       double a = 0.0, b = 0.0;
       for (int k = 0; k < NTH / 64; ++k) {
         a += red[k];
-        b += red[8 + k];
+        b += red[NTH / 64 + k];
       }
       if (g.conv_scale_dev) a *= *g.conv_scale_dev;
       if (g.conv_prev_scale_dev) b *= *g.conv_prev_scale_dev;
@@ -171,6 +189,9 @@ __device__ __forceinline__ bool gemm_skip(const GemmOp& g, double* red) {
         sk = 1;
         *g.skip_flag = 1;
         if (g.conv_iter_out) *g.conv_iter_out = g.conv_iter;
+      } else if (g.fin_flag && a <= g.conv_fin_tol2 * ref) {
+        *g.fin_flag = 1;
+        if (g.conv_iter_out) *g.conv_iter_out = g.conv_iter + 1;
       }
     }
     s_skip = sk;
@@ -179,27 +200,18 @@ __device__ __forceinline__ bool gemm_skip(const GemmOp& g, double* red) {
   return s_skip != 0;
 }
 
+// One BT x BT output tile (bx, by) of g (the whole block, NTH threads).  ntx =
+// tiles per row (partial-sum index).  sA / sB: the block's LDS operand buffers.
+// Ends with a barrier, so a caller may run further tiles on the same buffers.
 template <bool TA, bool TB, bool KS, bool DUAL>
-__global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
-  const GemmOp& g = gg.op[blockIdx.z];
+__device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int ntx,
+                                          double (*sA)[BUF], double (*sB)[BUF]) {
   // A is k-contiguous when not transposed; B is k-contiguous when transposed.
   constexpr bool AK = !TA, BK = TB;
-  __shared__ double sA[2][BUF];
-  __shared__ double sB[2][BUF];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (gemm_skip(g, sB[1])) {
-    if (g.copy_src) {
-      for (int e = t; e < BT * BT; e += NTH) {
-        const int row = blockIdx.y * BT + e / BT, col = blockIdx.x * BT + e % BT;
-        if (row < g.M && col < g.N)
-          g.C[(long long)row * g.ldc + col] = g.copy_src[(long long)row * g.ldc + col];
-      }
-    }
-    return;
-  }
-  const int q = w & 3, h = w >> 2;           // output quadrant, k half of each tile
+  const int q = w & 3, h = w >> 2;           // output quadrant, k part of each tile
   const int wm = q >> 1, wn = q & 1;
-  const int i0 = blockIdx.y * BT, j0 = blockIdx.x * BT;
+  const int i0 = by * BT, j0 = bx * BT;
   const int nt1 = (g.K + KT - 1) / KT;
   const int nt = DUAL ? 2 * nt1 : nt1;   // the second product's tiles follow the first's
   // tile `it` of the virtual k range: operands and k offset
@@ -227,11 +239,11 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
 #pragma unroll
   for (int c = 0; c < (DUAL ? 4 : 1); ++c) acc2[c] = d4{0.0, 0.0, 0.0, 0.0};
   const int ra = wm * 16 + (lane & 15), cb = wn * 16 + (lane & 15), kq = lane >> 4;
-  const int kb = h * (KT / 2);
+  const int kb = h * (KT / KS_);
   auto mma = [&](const double* a_s, const double* b_s, int it) {
     if (DUAL && it >= nt1) {
 #pragma unroll
-      for (int s = 0; s < KT / 8; ++s) {
+      for (int s = 0; s < KT / (4 * KS_); ++s) {
         const int kk = kb + 4 * s;
         const double a = frag<AK>(a_s, ra, kk + kq);
         const double b = frag<BK>(b_s, cb, kk + kq);
@@ -240,7 +252,7 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
       return;
     }
 #pragma unroll
-    for (int s = 0; s < KT / 8; ++s) {
+    for (int s = 0; s < KT / (4 * KS_); ++s) {
       const int kk = kb + 4 * s;
       const double a = frag<AK>(a_s, ra, kk + kq);
       const double b = frag<BK>(b_s, cb, kk + kq);
@@ -276,49 +288,76 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
     // combine here so the epilogue's alpha applies to both: alpha r + alpha2 r2
     r4 = r4 + (g.alpha2 / g.alpha) * r2;
   }
-  // k-half 1 hands its partial tile to k-half 0 through LDS
+  // k parts 1.. hand their partial tiles to part 0 through LDS (fixed order)
   double* red = sA[0];
-  if (h == 1) {
+  if (h >= 1) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(q * 4 + r) * 64 + lane] = r4[r];
+    for (int r = 0; r < 4; ++r) red[((h - 1) * 16 + q * 4 + r) * 64 + lane] = r4[r];
   }
   __syncthreads();
-  if (h == 1) return;
-  const int col = j0 + wn * 16 + (lane & 15);
-  double sq = 0.0, dt = 0.0;
-  const double alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
-  const double shift = g.sq_shift_dev ? *g.sq_shift_dev : g.sq_shift;
+  if (h == 0) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = i0 + wm * 16 + kq + 4 * r;
-    if (row < g.M && col < g.N) {
-      double v = alpha * (r4[r] + red[(q * 4 + r) * 64 + lane]);
-      if (g.row_div) v = v / g.row_div[row];
-      if (g.col_bias) v = g.col_bias[col] + v;
-      if (row == col) v += g.diag;
-      if (g.ns0) {
-        const double a = g.A[(long long)row * g.lda + col];
-        v = fma(g.ns0[1], a, g.ns0[0] * (r4[r] + red[(q * 4 + r) * 64 + lane]));
-        g.ns0_z[(long long)row * g.ldc + col] = g.ns0[2] * ((row == col ? 3.0 : 0.0) - g.ns0[3] * a);
+    for (int r = 0; r < 4; ++r) {
+      double p = red[(q * 4 + r) * 64 + lane];
+#pragma unroll
+      for (int hh = 2; hh < KS_; ++hh) p += red[((hh - 1) * 16 + q * 4 + r) * 64 + lane];
+      r4[r] += p;
+    }
+    const int col = j0 + wn * 16 + (lane & 15);
+    double sq = 0.0, dt = 0.0;
+    const double alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
+    const double shift = g.sq_shift_dev ? *g.sq_shift_dev : g.sq_shift;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = i0 + wm * 16 + kq + 4 * r;
+      if (row < g.M && col < g.N) {
+        double v = alpha * r4[r];
+        if (g.row_div) v = v / g.row_div[row];
+        if (g.col_bias) v = g.col_bias[col] + v;
+        if (row == col) v += g.diag;
+        if (g.ns0) {
+          const double a = g.A[(long long)row * g.lda + col];
+          v = fma(g.ns0[1], a, g.ns0[0] * r4[r]);
+          g.ns0_z[(long long)row * g.ldc + col] = g.ns0[2] * ((row == col ? 3.0 : 0.0) - g.ns0[3] * a);
+        }
+        double* c = g.C + (long long)row * g.ldc + col;
+        if (g.dot_with) dt = fma(g.dot_with[(long long)row * g.ldc + col], v, dt);
+        if (g.beta != 0.0) v += g.beta * *c;
+        *c = v;
+        const double e = row == col ? v - shift : v;
+        sq += e * e;
       }
-      double* c = g.C + (long long)row * g.ldc + col;
-      if (g.dot_with) dt = fma(g.dot_with[(long long)row * g.ldc + col], v, dt);
-      if (g.beta != 0.0) v += g.beta * *c;
-      *c = v;
-      const double e = row == col ? v - shift : v;
-      sq += e * e;
+    }
+    if (g.sq_part) {
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off, 64);
+      if (lane == 0) g.sq_part[4 * (by * ntx + bx) + q] = sq;
+    }
+    if (g.dot_part) {
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) dt += __shfl_xor(dt, off, 64);
+      if (lane == 0) g.dot_part[4 * (by * ntx + bx) + q] = dt;
     }
   }
-  if (g.sq_part) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off, 64);
-    if (lane == 0) g.sq_part[4 * (blockIdx.y * gridDim.x + blockIdx.x) + q] = sq;
+  __syncthreads();
+}
+
+template <bool TA, bool TB, bool KS, bool DUAL>
+__global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
+  const GemmOp& g = gg.op[blockIdx.z];
+  __shared__ double sA[2][BUF];
+  __shared__ double sB[2][BUF];
+  if (gemm_skip(g, sB[1])) {
+    if (g.copy_src && (g.copy_if_iter < 0 || *g.conv_iter_out == g.copy_if_iter)) {
+      for (int e = threadIdx.x; e < BT * BT; e += NTH) {
+        const int row = blockIdx.y * BT + e / BT, col = blockIdx.x * BT + e % BT;
+        if (row < g.M && col < g.N)
+          g.C[(long long)row * g.ldc + col] = g.copy_src[(long long)row * g.ldc + col];
+      }
+    }
+    return;
   }
-  if (g.dot_part) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) dt += __shfl_xor(dt, off, 64);
-    if (lane == 0) g.dot_part[4 * (blockIdx.y * gridDim.x + blockIdx.x) + q] = dt;
-  }
+  gemm_tile<TA, TB, KS, DUAL>(g, blockIdx.x, blockIdx.y, gridDim.x, sA, sB);
 }
 
 }  // namespace gemm_detail
