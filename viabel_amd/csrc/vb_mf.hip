@@ -661,16 +661,10 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
     const bool rows = RO == 1 || (RO == 0 && row_wave);
     const long long i = a.step0 + s;
     const long long ri = a.rng_step0 + s;
-    double mu[DMAX], sg[DMAX];
     double sl = 0.0;  // sum_d log sigma_d of the pre-update lam
-    // unconditional LDS loads (every index is inside the arrays) then selects:
-    // a load guarded by d < D compiles to a branch per coordinate, each waiting
-    // on its own loads (and, at DMAX = 10, on a scratch reload of the guard)
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
-      const double m = s_lam[d], g = s_sg[d], l = s_lam[D + d];
-      mu[d] = d < D ? m : 0.0;
-      sg[d] = d < D ? g : 0.0;
+      const double l = s_lam[D + d];
       sl += d < D ? l : 0.0;
     }
     double acc[K];
@@ -689,9 +683,12 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
 
     auto row_of = [&](const double* e, double lqs) {
       double x[DMAX], g[DMAX];
+      // mu and sigma straight from LDS (broadcast reads): one sample per thread
+      // per step, so holding them in registers across the step buys nothing
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
-        x[d] = e[d] * sg[d] + mu[d];
+        const double m = s_lam[d], sgd = s_sg[d];
+        x[d] = d < D ? e[d] * sgd + m : 0.0;
         g[d] = 0.0;
       }
       double lp = Row::template row<DMAX>(x, g, D);
