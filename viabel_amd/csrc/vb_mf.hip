@@ -899,10 +899,10 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
     for (int s = 0; s < a.n_steps; ++s) step(s, std::integral_constant<int, 0>{});
   }
 #ifdef VB_BLOCK_PROF
-  if (prob == 0 && tid == 0) {
+  if (prob == 0 && (tid == 0 || tid == RT)) {  // a row wave and the first draw wave
     const unsigned long long tw = wall_clock64() - tw0, tc = clock64() - tc0;
-    printf("BLOCKPROF D=%d N=%d NT=%d RW=%d pipe=%d steps=%d wall_ticks=%llu cycles=%llu | exp %llu draw %llu row %llu chivi %llu bsum %llu upd %llu bar %llu\n",
-           D, N, NT, RW, L.pipe, a.n_steps, tw, tc, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6]);
+    printf("BLOCKPROF tid=%d D=%d N=%d NT=%d RW=%d pipe=%d steps=%d wall_ticks=%llu cycles=%llu | exp %llu draw %llu row %llu chivi %llu bsum %llu upd %llu bar %llu\n",
+           tid, D, N, NT, RW, L.pipe, a.n_steps, tw, tc, ph[0], ph[1], ph[2], ph[3], ph[4], ph[5], ph[6]);
   }
 #endif
 #undef VB_PH
