@@ -374,3 +374,55 @@ def test_adagrad_chunked_progress_and_interrupt(monkeypatch):
     run2.advance_philox(1000, seed2, stream2, step2)
     np.testing.assert_array_equal(part[2], run2.values()[:1000])
     assert part[1].shape == (0, 2 * D) and np.all(np.isnan(part[0]))
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize('objective', ['klvi', 'chivi', 'klvi_pd'])
+@pytest.mark.parametrize('target,D,N,nprob', [('funnel', 10, 128, 1), ('eight_schools_ncp', 10, 100, 3),
+                                              ('mixture', 5, 300, 2), ('isogauss', 1, 64, 1)])
+def test_predraw_equals_in_kernel_draws(objective, target, D, N, nprob, monkeypatch):
+    """Gaussian-family block-kernel runs whose Philox draws are pre-drawn by the
+    throughput kernel (VIABEL_AMD_PREDRAW=all; the t family always pre-draws,
+    DESIGN §4) give bit-identical trajectories, values and histories to the
+    in-kernel draws, across predraw chunk boundaries."""
+    import viabel_amd.vb as vbm
+    vb, targets, _, _ = _mods()
+    fam = _family(vb, 'gauss', None, D, 'philox')
+    tgt = _target(targets, target, D)
+    obj = {'klvi': lambda: vb.black_box_klvi(fam, tgt, N),
+           'chivi': lambda: vb.black_box_chivi(2.0, fam, tgt, N),
+           'klvi_pd': lambda: vb.black_box_klvi_pd(fam, tgt, N)}[objective]()
+    init = np.stack([_lam(D, 40 + q) for q in range(nprob)])
+    out = {}
+    for mode in ('0', 'all'):
+        monkeypatch.setenv('VIABEL_AMD_PREDRAW', mode)
+        run = vbm.DeviceRun(obj, 700, init, learning_rate=0.01)
+        run.advance_philox(3, 7, 5, 0)
+        run.advance_philox(697, 7, 5, 3)        # > one 512-step predraw chunk
+        out[mode] = run.result()
+    for a, b in zip(out['0'], out['all']):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize('objective', ['klvi', 'chivi'])
+def test_t_family_predraw_large_n_matches_oracle(objective):
+    """The t family's pre-drawn block-kernel path at N > 256 (rows looped per
+    thread, several problems, per-problem Philox streams) against the oracle loop
+    fed with the C-oracle draws (trajectory bar 1e-7)."""
+    vb, targets, vo, ro = _mods()
+    D, N, n_iters, R = 5, 300, 40, 2
+    fam = _family(vb, 't', 40.0, D, 'philox')
+    tgt = targets.mixture(D)
+    obj = (vb.black_box_klvi(fam, tgt, N) if objective == 'klvi'
+           else vb.black_box_chivi(2.0, fam, tgt, N))
+    inits = np.stack([_lam(D, 40 + q) for q in range(R)])
+    run = vb.DeviceRun(obj, n_iters, inits, learning_rate=0.01)
+    run.advance_philox(n_iters, seed=7, stream=5, step=0)
+    lam, hist, vals, smooth = run.result()
+    ofam = vo.Family('t', D, 40.0)
+    for r in range(R):
+        eps_fn = lambda i, r=r: ro.noise(7, 5 + r, i, N, D, 't', 40.0)
+        ores = _oracle_run(vo, ofam, objective, 'mixture', n_iters, inits[r], N,
+                           eps_fn=eps_fn, learning_rate=0.01)
+        np.testing.assert_allclose(vals[r], ores[2], rtol=1e-7, atol=1e-9)
+        np.testing.assert_allclose(lam[r], ores[1][-1], rtol=1e-7, atol=1e-9)

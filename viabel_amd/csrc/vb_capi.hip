@@ -8,7 +8,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -79,7 +81,7 @@ struct DevBuf {
   size_t cap = 0;
   int reserve(size_t bytes) {
     if (bytes <= cap) return VB_OK;
-    if (p) (void)hipFree(p);
+    if (p) (void)hipFree(p);  // synchronises the device first (HIP)
     p = nullptr;
     cap = 0;
     if (bytes == 0) return VB_OK;
@@ -178,6 +180,19 @@ using Out = OutT<double>;
 int sync(vb_ctx* c) {
   VB_HIP(hipStreamSynchronize(c->stream));
   return VB_OK;
+}
+
+// Block-kernel work with Philox draws of the mean-field t family always
+// pre-draws them (launch_block_predraw + the device-noise path: the t draws are a
+// step's critical path); the Gaussian family draws in kernel unless
+// VIABEL_AMD_PREDRAW=all (read per call: tests switch it).  Chunks hold at most
+// kPredrawBytes of draws and kPredrawMaxSteps steps.
+constexpr size_t kPredrawBytes = size_t(256) << 20;
+constexpr long long kPredrawMaxSteps = 512;
+bool predraw_enabled(int fam_kind) {
+  if (fam_kind == VB_FAMILY_MF_T) return true;
+  const char* e = std::getenv("VIABEL_AMD_PREDRAW");
+  return e && e[0] == 'a';
 }
 
 int check_ctx(vb_ctx* c) {
@@ -645,7 +660,19 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
     a.k1 = k1;
     a.stream = noise->stream;
     a.stream_stride = 1;
-    VB_HIP(vbk::launch_block(fi.kind, tgt->kind, host, a, 1, c->stream));
+    if (!host && predraw_enabled(fi.kind)) {
+      const bool need_lq = a.chivi || a.pd;
+      VB_TRY(c->slot[6].reserve(sizeof(double) * (size_t)N * D));
+      if (need_lq) VB_TRY(c->slot[7].reserve(sizeof(double) * (size_t)N));
+      VB_HIP(vbk::launch_block_predraw(fi.kind, D, N, 1, 1, k0, k1, a.stream, 1, a.rng_step0,
+                                       fi.t_scale, fi.shape, fi.df, fi.t_const, c->slot[6].d(),
+                                       need_lq ? c->slot[7].d() : nullptr, c->stream));
+      a.noise = c->slot[6].d();
+      a.noise_lq = need_lq ? c->slot[7].d() : nullptr;
+      VB_HIP(vbk::launch_block(fi.kind, tgt->kind, true, a, 1, c->stream));
+    } else {
+      VB_HIP(vbk::launch_block(fi.kind, tgt->kind, host, a, 1, c->stream));
+    }
   } else {
     // CHIVI or a non-separable target at D > kBlockDMax: materialised path
     vbk::FrWork* W;
@@ -676,6 +703,7 @@ struct vb_run {
   int n_waves = 0;
   int max_chunk = 256;
   DevBuf lam, ring, hist, values, vpart, noise, smooth;
+  DevBuf noise_lq;  // pre-drawn log q partials (block kernel, predraw)
   // full-rank family / wide mean-field: one value_grad + update per step
   bool fr = false, wide = false;
   vbk::FrSpec spec{};
@@ -970,11 +998,38 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
     a.values = r->values.d();
     a.grad = nullptr;
     a.noise = noise_base;
+    a.noise_lq = nullptr;
     a.k0 = k0;
     a.k1 = k1;
     a.stream = noise->stream;
     a.stream_stride = noise->stream_stride ? noise->stream_stride : 1;
-    VB_HIP(vbk::launch_block(r->fi.kind, r->tgt, host, a, (int)r->nprob, c->stream));
+    if (!host && predraw_enabled(r->fi.kind)) {
+      // Philox draws pre-drawn chunk by chunk by a throughput kernel over the
+      // whole chip, then consumed through the device-noise path: the same
+      // draws and log q partials, off the per-step critical path
+      const bool need_lq = a.chivi || a.pd;
+      const size_t per_step = (size_t)r->nprob * N * (D + (need_lq ? 1 : 0)) * sizeof(double);
+      const long long cap = std::max<long long>(1, (long long)(kPredrawBytes / per_step));
+      const int cmax = (int)std::min<long long>({n_steps, cap, (long long)kPredrawMaxSteps});
+      VB_TRY(r->noise.reserve((size_t)r->nprob * cmax * N * D * sizeof(double)));
+      if (need_lq) VB_TRY(r->noise_lq.reserve((size_t)r->nprob * cmax * N * sizeof(double)));
+      for (long long off = 0; off < n_steps; off += cmax) {
+        const int cs = (int)std::min<long long>(cmax, n_steps - off);
+        VB_HIP(vbk::launch_block_predraw(r->fi.kind, D, N, cs, (int)r->nprob, k0, k1, a.stream,
+                                         a.stream_stride, (long long)noise->step + off,
+                                         r->fi.t_scale, r->fi.shape, r->fi.df, r->fi.t_const,
+                                         r->noise.d(), need_lq ? r->noise_lq.d() : nullptr,
+                                         c->stream));
+        vbk::BlockArgs b = a;
+        b.n_steps = cs;
+        b.step0 = r->done + off;
+        b.noise = r->noise.d();
+        b.noise_lq = need_lq ? r->noise_lq.d() : nullptr;
+        VB_HIP(vbk::launch_block(r->fi.kind, r->tgt, true, b, (int)r->nprob, c->stream));
+      }
+    } else {
+      VB_HIP(vbk::launch_block(r->fi.kind, r->tgt, host, a, (int)r->nprob, c->stream));
+    }
   }
   if (call_ev) VB_HIP(hipEventRecord(call_ev->second, c->stream));
   r->done += n_steps;

@@ -790,6 +790,12 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm) {
   }
   // power steps: Sigma x and Z_prev u (the previous root's vectors as start)
   warm = warm && W->warm;
+  // a cold root starts a new problem: forget the iteration counts learnt on the
+  // previous one (fr_info learns them again from this run's warm steps)
+  if (!warm) {
+    W->ns_kmax = 12;
+    W->pcg_kmax = 14;
+  }
   const bool hz = warm && W->have_z && W->Zf;
   const int n_pow = warm ? 3 : 8;
   const unsigned nb = (unsigned)((D + 7) / 8);
@@ -898,7 +904,7 @@ int fr_pcg(FrWork* W, int D, hipStream_t st) {
   hipLaunchKernelGGL(pcg_p_kernel, tg, dim3(256), 0, st, D, -1, W->C2.d(), W->rz_part.d(),
                      4 * nblk, W->ee_part.d(), nblk, sc, W->P.d());
   // warm roots launch the learnt count (fr_info), others at least 16
-  const int kpcg = W->last_warm ? W->pcg_kmax : std::max(W->pcg_kmax, 16);
+  const int kpcg = W->last_warm ? std::max(W->pcg_kmax, 6) : std::max(W->pcg_kmax, 16);
   for (int it = 0; it < kpcg; ++it) {
     GemmOp g = mm(D, D, D, W->Yf, false, W->P.d(), false, W->C1.d());
     g.dot_with = W->P.d();

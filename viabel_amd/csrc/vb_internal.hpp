@@ -61,6 +61,9 @@ struct BlockArgs {
   double* values;       // [n_problems][n_iters] (indexed by global step)
   double* grad;         // [n_problems][P] (emit_grad)
   const double* noise;  // host noise [n_problems][n_steps][N][D] or null
+  // with noise: per-sample log q partials [n_problems][n_steps][N] (sum over the
+  // column pairs, without -sum log sigma) from launch_block_predraw, or null
+  const double* noise_lq;
   uint32_t k0, k1, stream, stream_stride;
 };
 
@@ -69,6 +72,14 @@ hipError_t launch_sep(int fam, int tgt, bool host_noise, const SepArgs& a, hipSt
 hipError_t launch_block(int fam, int tgt, bool host_noise, const BlockArgs& a, int n_problems,
                         hipStream_t s);
 bool target_separable(int tgt);
+// Pre-drawn block-kernel noise: the standardized draws of n_steps steps of
+// n_problems problems, [q][s][N][D], bit-identical to the block kernel's own
+// Philox draws (same counters: pair, sample, rng_step0 + s, stream + q * stride),
+// and, when lq is non-null, each sample's log q partial sum [q][s][N].
+hipError_t launch_block_predraw(int fam, int D, int N, int n_steps, int n_problems, uint32_t k0,
+                                uint32_t k1, uint32_t stream, uint32_t stride,
+                                long long rng_step0, double t_scale, double shape, double df,
+                                double t_const, double* noise, double* lq, hipStream_t s);
 
 // values[i] = -(c0 + sum_w vpart[s][w]) for i = step0 + s
 hipError_t launch_sep_values(const double* vpart, int n_steps, int n_waves, double c0,

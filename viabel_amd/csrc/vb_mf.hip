@@ -721,20 +721,27 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
     };
 
     if constexpr (HOST) {
+      const bool pre_lq = a.noise_lq != nullptr;
       for (int n = tid; n < N; n += RT) {
-        const double* row = a.noise + (((long long)prob * a.n_steps + s) * N + n) * D;
+        const long long rix = ((long long)prob * a.n_steps + s) * N + n;
+        const double* row = a.noise + rix * D;
         double e[DMAX];
         double lqs = 0.0;
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) {
-          e[d] = d < D ? row[d] : 0.0;
-          if (need_lq && d < D) {
+          // the index is clamped so that no load (the compiler may issue it
+          // unconditionally for the select) reads past the sample's D values,
+          // i.e. past the end of the noise array for the last sample
+          const double t = row[d < D ? d : D - 1];
+          e[d] = d < D ? t : 0.0;
+          if (need_lq && !pre_lq && d < D) {
             if constexpr (TFAM)
               lqs += a.t_const - log1p(e[d] * e[d] / a.df) * lq_half;
             else
               lqs += -0.5 * e[d] * e[d] - 0.5 * kLog2Pi;
           }
         }
+        if (need_lq && pre_lq) lqs = a.noise_lq[rix];
         row_of(e, lqs);
       }
     } else {
@@ -883,8 +890,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
     __syncthreads();
     VB_PH(6);
   };
-  // (the t family keeps one shared loop: its draw waves, the critical path there,
-  // measured slower in their own copy)
+  // (the t family runs only with pre-drawn noise: one loop of row waves)
   bool split = false;
   if constexpr (!HOST && !TFAM) split = L.pipe;
   if (split) {
@@ -911,6 +917,80 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
     for (int p = tid; p < P; p += NT) lam_g[p] = s_lam[p];
     for (int q = tid; q < W * P; q += NT) ring_g[q] = s_ring[q];
   }
+}
+
+// Pre-drawn noise for the block kernel's device-noise path (launch_block_predraw):
+// one thread per (problem, step, sample) walks the sample's column pairs with the
+// draw items' counters, transforms and log q partials (block_kernel's draw_item),
+// so the block kernel consuming it computes bit-identical results to drawing in
+// kernel -- while the draws, which never depend on lambda, run as a throughput
+// kernel over the whole chip instead of on the serial step chain of one
+// workgroup per problem.
+template <bool TFAM>
+__global__ __launch_bounds__(256) void block_predraw_kernel(int D, int N, int n_steps, long long total,
+                                                            uint32_t k0, uint32_t k1, uint32_t stream,
+                                                            uint32_t stride, long long rng_step0,
+                                                            double t_scale, double shape, double df,
+                                                            double t_const, double* noise,
+                                                            double* lq) {
+  __shared__ double2 s_sct[kSinCosN];
+  __shared__ double2 s_lt[kLogN + kLogU01N];
+  load_bm_tables(s_sct, s_lt);
+  __syncthreads();
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;  // (q * n_steps + s) * N + n
+  if (idx >= total) return;
+  const int n = (int)(idx % N);
+  const long long qs = idx / N;
+  const int s = (int)(qs % n_steps);
+  const uint32_t q = (uint32_t)(qs / n_steps);
+  const Rng rng{k0, k1, stream + q * stride};
+  const uint32_t ri = (uint32_t)(rng_step0 + s);
+  const int NP = (D + 1) / 2;
+  const double lq_half = 0.5 * (df + 1.0);
+  const double inv_df = 1.0 / df;
+  double* row = noise + idx * D;
+  double lqs = 0.0;
+  for (int j = 0; j < NP; ++j) {
+    double ea, eb;
+    normal_pair_tab(rng.draw((uint32_t)j, (uint32_t)n, ri, 0u), ea, eb, s_sct, s_lt);
+    if constexpr (TFAM) {
+      double ga, gb;
+      gamma_pair<true>(rng, (uint32_t)j, (uint32_t)n, ri, shape, ga, gb, s_sct, s_lt);
+      ea = t_scale * ea * rsqrt_pos(ga);
+      eb = t_scale * eb * rsqrt_pos(gb);
+    }
+    const bool hasb = 2 * j + 1 < D;
+    row[2 * j] = ea;
+    if (hasb) row[2 * j + 1] = eb;
+    if (lq) {
+      double lqp;
+      if constexpr (TFAM) {
+        lqp = t_const - log1p_pos_tab(ea * ea * inv_df, s_lt) * lq_half;
+        if (hasb) lqp += t_const - log1p_pos_tab(eb * eb * inv_df, s_lt) * lq_half;
+      } else {
+        lqp = -0.5 * ea * ea - 0.5 * kLog2Pi;
+        if (hasb) lqp += -0.5 * eb * eb - 0.5 * kLog2Pi;
+      }
+      lqs += lqp;
+    }
+  }
+  if (lq) lq[idx] = lqs;
+}
+
+hipError_t launch_block_predraw(int fam, int D, int N, int n_steps, int nprob, uint32_t k0,
+                                uint32_t k1, uint32_t stream, uint32_t stride, long long rng_step0,
+                                double t_scale, double shape, double df, double t_const,
+                                double* noise, double* lq, hipStream_t s) {
+  const long long total = (long long)nprob * n_steps * N;
+  if (total <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (fam == 1)
+    hipLaunchKernelGGL(block_predraw_kernel<true>, grid, dim3(256), 0, s, D, N, n_steps, total, k0,
+                       k1, stream, stride, rng_step0, t_scale, shape, df, t_const, noise, lq);
+  else
+    hipLaunchKernelGGL(block_predraw_kernel<false>, grid, dim3(256), 0, s, D, N, n_steps, total, k0,
+                       k1, stream, stride, rng_step0, t_scale, shape, df, t_const, noise, lq);
+  return hipGetLastError();
 }
 
 // -------------------------------------------------------------------------
@@ -1359,7 +1439,9 @@ static hipError_t block_dispatch_dm(int fam, bool host, const BlockArgs& a, int 
   } else if (host) {
     hipLaunchKernelGGL((block_kernel<TGT, false, true, DM>), grid, block, 0, s, a);
   } else if (fam == 1) {
-    hipLaunchKernelGGL((block_kernel<TGT, true, false, DM>), grid, block, 0, s, a);
+    // the t family's Philox draws are pre-drawn (launch_block_predraw) and
+    // consumed through the device-noise path; no in-kernel t sampler instance
+    return hipErrorInvalidValue;
   } else {
     hipLaunchKernelGGL((block_kernel<TGT, false, false, DM>), grid, block, 0, s, a);
   }
