@@ -32,6 +32,8 @@
  *   vb_ia_update           viabel/vb.py:436-453, 606-617 (one RMSProp-IA / Adam-IA step for a
  *                          foreign objective, or with avg_grad_norm)
  *   vb_log_weights         notebooks/experiments.py:60-63 (get_samples_and_log_weights)
+ *   vb_log_weights_rows    notebooks/experiments.py:60-63 for every restart of
+ *                          vb.py:417-421's restart loop in one launch
  *   vb_divergence_bound    viabel/bounds.py:142-192 (divergence_bound, mean_and_check_mc_error)
  *   vb_divergence_bound_rows viabel/bounds.py:142-192 (divergence_bound over many log-weight rows)
  *   vb_centered_moments    viabel/bounds.py:127-135 (wasserstein_bounds sample moments)
@@ -269,6 +271,14 @@ int vb_iterate_average(vb_ctx* ctx, const double* x, int64_t n, int64_t ld, int6
 int vb_log_weights(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,
                    const double* lam, int64_t m, const vb_noise* noise,
                    double* lw_out, double* samples_out /* nullable, [m, D] */);
+/* vb_log_weights for `rows` parameter vectors of a mean-field family at once
+ * (lam [rows][2D]; Philox noise only, row r drawing from stream
+ * noise->stream + r * noise->stream_stride), lw_out [rows][m], one launch.
+ * Targets / dimensions of the block kernel's range (D <= 16, or separable).
+ * rows <= 65535. */
+int vb_log_weights_rows(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,
+                        const double* lam, int64_t rows, int64_t m, const vb_noise* noise,
+                        double* lw_out);
 
 /* ---- bounds (bounds.py:142-192, 127-135) ------------------------------ */
 /* out[0] = d_alpha, out[1] = log_norm_bound (ELBO), out[2] = CUBO mean of

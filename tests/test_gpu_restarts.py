@@ -95,3 +95,27 @@ def test_numpy_rng_factory_is_rejected():
     with pytest.raises(ValueError, match='philox'):
         restarts.run_restarts(lambda: vb.mean_field_t_variational_family(D, 40, rng='numpy'),
                               targets.eight_schools_ncp(), 2, 5, n_bounds=100)
+
+
+@pytest.mark.parametrize('case', ['t_eight_schools', 'gauss_mixture', 'gauss_isogauss_wide'])
+def test_log_weights_rows_equal_per_row_calls(case):
+    """vb_log_weights_rows (one launch for every restart's bound draws) gives the
+    per-restart vb_log_weights results bit for bit (row r: stream base + r * stride)."""
+    from viabel_amd import vb, targets, experiments
+    if case == 't_eight_schools':
+        D, fam_fn, tgt = 10, lambda: vb.mean_field_t_variational_family(10, 40.0, rng='philox'), \
+            targets.eight_schools_ncp()
+    elif case == 'gauss_mixture':
+        D = 3
+        fam_fn, tgt = lambda: vb.mean_field_gaussian_variational_family(3, rng='philox'), targets.mixture(3)
+    else:
+        D = 40
+        fam_fn, tgt = lambda: vb.mean_field_gaussian_variational_family(40, rng='philox'), targets.isogauss(40)
+    R, m = 5, 20000
+    lams = np.random.RandomState(3).randn(R, 2 * D) * 0.3
+    rows = experiments.log_weights_rows(tgt, fam_fn(), lams, m, stream=100, stream_stride=3)
+    for r in range(R):
+        f = fam_fn()
+        f.stream = 100 + 3 * r
+        _, lw = experiments.log_weights(tgt, f, lams[r], m, return_samples=False)
+        np.testing.assert_array_equal(rows[r], lw)

@@ -99,6 +99,8 @@ _SIGNATURES = {
                       ctypes.c_double, c_double_p], ctypes.c_int),
     'vb_log_weights': ([ctypes.c_void_p, P(Family), P(Target), c_double_p, ctypes.c_int64,
                         P(Noise), c_double_p, c_double_p], ctypes.c_int),
+    'vb_log_weights_rows': ([ctypes.c_void_p, P(Family), P(Target), c_double_p, ctypes.c_int64,
+                             ctypes.c_int64, P(Noise), c_double_p], ctypes.c_int),
     'vb_divergence_bound': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_double,
                              ctypes.c_int32, ctypes.c_double, c_double_p], ctypes.c_int),
     'vb_divergence_bound_rows': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,

@@ -1168,6 +1168,35 @@ int vb_ia_update(vb_ctx* c, int32_t optimizer, int64_t P, double* lam, const dou
 }
 
 // ---------------------------------------------------------------------------
+int vb_log_weights_rows(vb_ctx* c, const vb_family* fam, const vb_target* tgt,
+                        const double* lam, int64_t rows, int64_t m, const vb_noise* noise,
+                        double* lw_out) {
+  VB_TRY(check_ctx(c));
+  FamInfo fi;
+  VB_TRY(check_family(fam, &fi));
+  VB_TRY(check_target(tgt, fi.D));
+  if (!lam || !noise || !lw_out || m < 0 || rows < 0) return fail(VB_EINVAL, "null argument");
+  if (rows > 65535) return fail(VB_EINVAL, "rows must be <= 65535");
+  if (fi.kind == VB_FAMILY_FR_T) return fail(VB_EUNSUPPORTED, "rows of log weights: mean-field families only");
+  if (noise->kind != VB_NOISE_PHILOX) return fail(VB_EINVAL, "rows of log weights need Philox noise");
+  if ((!vbk::target_separable(tgt->kind) && fi.D > vbk::kBlockDMax) || tgt->kind == VB_TARGET_CALLBACK)
+    return fail(VB_EUNSUPPORTED, "rows of log weights: D <= %d or a separable device target",
+                vbk::kBlockDMax);
+  if (m == 0 || rows == 0) return VB_OK;
+  In dl;
+  Out dlw;
+  VB_TRY(dl.stage(c, 0, lam, 2 * (size_t)fi.D * rows));
+  VB_TRY(dlw.stage(c, 2, lw_out, (size_t)m * rows));
+  uint32_t k0, k1;
+  key_of(noise->seed, &k0, &k1);
+  VB_HIP(vbk::launch_log_weights(fi.kind, tgt->kind, fi.D, m, dl.d, fi.t_scale, fi.shape, fi.df,
+                                 fi.t_const, nullptr, k0, k1, noise->stream,
+                                 (uint32_t)noise->step, dlw.d, nullptr, c->stream, (int)rows,
+                                 noise->stream_stride));
+  VB_TRY(dlw.finish(c));
+  return sync(c);
+}
+
 int vb_log_weights(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const double* lam,
                    int64_t m, const vb_noise* noise, double* lw_out, double* samples_out) {
   VB_TRY(check_ctx(c));

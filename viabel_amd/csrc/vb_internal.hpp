@@ -109,7 +109,8 @@ hipError_t launch_mfw_rows(int fam, int tgt, int D, long long n, const double* l
 hipError_t launch_log_weights(int fam, int tgt, int D, long long m, const double* lam,
                               double t_scale, double shape, double df, double t_const,
                               const double* noise, uint32_t k0, uint32_t k1, uint32_t stream,
-                              uint32_t step, double* lw, double* xs, hipStream_t s);
+                              uint32_t step, double* lw, double* xs, hipStream_t s, int rows = 1,
+                              uint32_t stride = 0);
 // scale (nullable): [min(step + 1, W)] window scales, oldest first
 hipError_t launch_adagrad_update(long long P, double* lam, const double* g, double* ring, int W,
                                  long long step, double lr, double eps, const double* scale,

@@ -1268,7 +1268,7 @@ template <class TGT, bool TFAM, bool HOST>
 __global__ __launch_bounds__(256) void logw_sep_kernel(int D, long long m, const double* lam,
                                                        double t_scale, double shape, double df,
                                                        double t_const, const double* noise,
-                                                       Rng rng, uint32_t step, double* lw,
+                                                       Rng rng, uint32_t step, uint32_t stride, double* lw,
                                                        double* xs) {
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
@@ -1276,6 +1276,14 @@ __global__ __launch_bounds__(256) void logw_sep_kernel(int D, long long m, const
     load_bm_tables(s_sct, s_lt);
     __syncthreads();
   }
+  // row q of a batched launch (vb_log_weights_rows): its own lambda, output
+  // row, noise rows and Philox stream (stream + q * stride)
+  const int q = blockIdx.y;
+  lam += (long long)q * 2 * D;
+  lw += (long long)q * m;
+  if (xs) xs += (long long)q * m * D;
+  if (noise) noise += (long long)q * m * D;
+  rng.stream += (uint32_t)q * stride;
   const long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= m) return;
   const int lane = threadIdx.x & 63, npairs = (D + 1) / 2;
@@ -1305,7 +1313,7 @@ template <class TGT, bool TFAM, bool HOST, int DMAX>
 __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const double* lam,
                                                        double t_scale, double shape, double df,
                                                        double t_const, const double* noise,
-                                                       Rng rng, uint32_t step, double* lw,
+                                                       Rng rng, uint32_t step, uint32_t stride, double* lw,
                                                        double* xs) {
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
@@ -1313,6 +1321,14 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
     load_bm_tables(s_sct, s_lt);
     __syncthreads();
   }
+  // row q of a batched launch (vb_log_weights_rows): its own lambda, output
+  // row, noise rows and Philox stream (stream + q * stride)
+  const int q = blockIdx.y;
+  lam += (long long)q * 2 * D;
+  lw += (long long)q * m;
+  if (xs) xs += (long long)q * m * D;
+  if (noise) noise += (long long)q * m * D;
+  rng.stream += (uint32_t)q * stride;
   const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
   if (r >= m) return;
   double x[DMAX], g[DMAX];
@@ -1758,47 +1774,49 @@ hipError_t launch_target_logdensity(int tgt, int D, long long n, const double* x
 template <class TGT, bool TFAM, bool HOST>
 static void logw_launch(int D, long long m, const double* lam, double t_scale, double shape,
                         double df, double t_const, const double* noise, Rng rng, uint32_t step,
-                        double* lw, double* xs, hipStream_t s) {
+                        int rows, uint32_t stride, double* lw, double* xs, hipStream_t s) {
   if constexpr (TGT::kSeparable) {
     if (D > kBlockDMax) {
-      hipLaunchKernelGGL((logw_sep_kernel<TGT, TFAM, HOST>), dim3((unsigned)((m + 3) / 4)),
-                         dim3(256), 0, s, D, m, lam, t_scale, shape, df, t_const, noise, rng,
-                         step, lw, xs);
+      hipLaunchKernelGGL((logw_sep_kernel<TGT, TFAM, HOST>),
+                         dim3((unsigned)((m + 3) / 4), (unsigned)rows), dim3(256), 0, s, D, m,
+                         lam, t_scale, shape, df, t_const, noise, rng, step, stride, lw, xs);
       return;
     }
   }
   {
     hipLaunchKernelGGL((logw_row_kernel<TGT, TFAM, HOST, kBlockDMax>),
-                       dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, D, m, lam, t_scale,
-                       shape, df, t_const, noise, rng, step, lw, xs);
+                       dim3((unsigned)((m + 255) / 256), (unsigned)rows), dim3(256), 0, s, D, m,
+                       lam, t_scale, shape, df, t_const, noise, rng, step, stride, lw, xs);
   }
 }
 
 template <class TGT>
 static void logw_fam(int fam, bool host, int D, long long m, const double* lam, double t_scale,
                      double shape, double df, double t_const, const double* noise, Rng rng,
-                     uint32_t step, double* lw, double* xs, hipStream_t s) {
+                     uint32_t step, int rows, uint32_t stride, double* lw, double* xs,
+                     hipStream_t s) {
   if (fam == 1) {
-    if (host) logw_launch<TGT, true, true>(D, m, lam, t_scale, shape, df, t_const, noise, rng, step, lw, xs, s);
-    else logw_launch<TGT, true, false>(D, m, lam, t_scale, shape, df, t_const, noise, rng, step, lw, xs, s);
+    if (host) logw_launch<TGT, true, true>(D, m, lam, t_scale, shape, df, t_const, noise, rng, step, rows, stride, lw, xs, s);
+    else logw_launch<TGT, true, false>(D, m, lam, t_scale, shape, df, t_const, noise, rng, step, rows, stride, lw, xs, s);
   } else {
-    if (host) logw_launch<TGT, false, true>(D, m, lam, t_scale, shape, df, t_const, noise, rng, step, lw, xs, s);
-    else logw_launch<TGT, false, false>(D, m, lam, t_scale, shape, df, t_const, noise, rng, step, lw, xs, s);
+    if (host) logw_launch<TGT, false, true>(D, m, lam, t_scale, shape, df, t_const, noise, rng, step, rows, stride, lw, xs, s);
+    else logw_launch<TGT, false, false>(D, m, lam, t_scale, shape, df, t_const, noise, rng, step, rows, stride, lw, xs, s);
   }
 }
 
 hipError_t launch_log_weights(int fam, int tgt, int D, long long m, const double* lam,
                               double t_scale, double shape, double df, double t_const,
                               const double* noise, uint32_t k0, uint32_t k1, uint32_t stream,
-                              uint32_t step, double* lw, double* xs, hipStream_t s) {
-  if (m == 0) return hipSuccess;
+                              uint32_t step, double* lw, double* xs, hipStream_t s, int rows,
+                              uint32_t stride) {
+  if (m == 0 || rows <= 0) return hipSuccess;
   const Rng rng{k0, k1, stream};
   const bool host = noise != nullptr;
   switch (tgt) {
-    case 0: logw_fam<IsoGauss>(fam, host, D, m, lam, t_scale, shape, df, t_const, noise, rng, step, lw, xs, s); break;
-    case 1: logw_fam<Mixture>(fam, host, D, m, lam, t_scale, shape, df, t_const, noise, rng, step, lw, xs, s); break;
-    case 2: logw_fam<Funnel>(fam, host, D, m, lam, t_scale, shape, df, t_const, noise, rng, step, lw, xs, s); break;
-    case 3: logw_fam<EightSchools>(fam, host, D, m, lam, t_scale, shape, df, t_const, noise, rng, step, lw, xs, s); break;
+    case 0: logw_fam<IsoGauss>(fam, host, D, m, lam, t_scale, shape, df, t_const, noise, rng, step, rows, stride, lw, xs, s); break;
+    case 1: logw_fam<Mixture>(fam, host, D, m, lam, t_scale, shape, df, t_const, noise, rng, step, rows, stride, lw, xs, s); break;
+    case 2: logw_fam<Funnel>(fam, host, D, m, lam, t_scale, shape, df, t_const, noise, rng, step, rows, stride, lw, xs, s); break;
+    case 3: logw_fam<EightSchools>(fam, host, D, m, lam, t_scale, shape, df, t_const, noise, rng, step, rows, stride, lw, xs, s); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -16,7 +16,7 @@ from . import _native as nat
 from .psis import psislw
 from .targets import Target
 
-__all__ = ['get_samples_and_log_weights', 'psis_correction', 'log_weights', 'check_accuracy',
+__all__ = ['get_samples_and_log_weights', 'psis_correction', 'log_weights', 'log_weights_rows', 'check_accuracy',
            'check_approx_accuracy', 'improve_with_psis', 'weighted_mean_and_cov']
 
 
@@ -46,6 +46,33 @@ def log_weights(logdensity, var_family, var_param, n_samples, return_samples=Tru
                                        logdensity._struct(), nat.dptr(lam), m, nz,
                                        nat.dptr(lw), nat.dptr(xs)))
     return xs, lw
+
+
+def log_weights_rows(logdensity, var_family, var_params, n_samples, stream, stream_stride=1,
+                     seed=None, lw_out=None):
+    """log_weights for many parameter vectors of one mean-field family at once
+    (the restart loop of vb.py:417-421 followed by experiments.py:60-63 per
+    restart): var_params [R, 2D]; row r draws n_samples Philox draws from stream
+    `stream + r * stream_stride` (key `seed`, default the family's), one device
+    launch.  Returns lw [R, n_samples] (lw_out: a float64 device tensor of that
+    shape to write into, kept in HBM for the bounds / PSIS calls)."""
+    if not isinstance(logdensity, Target):
+        raise TypeError('log weights on the device need a viabel_amd.targets target')
+    logdensity = logdensity.bind(var_family.dim)
+    lams = nat.as_f64(np.atleast_2d(var_params))
+    R, m = lams.shape[0], int(n_samples)
+    if lw_out is not None:
+        lw = nat.device_tensor(lw_out)
+        if lw is None or tuple(lw.shape) != (R, m) or not lw.is_contiguous():
+            raise ValueError('lw_out must be a contiguous float64 device tensor of shape (R, n_samples)')
+    else:
+        lw = np.empty((R, m))
+    key = var_family.seed if seed is None else int(seed) & 0xFFFFFFFFFFFFFFFF
+    nz = nat.Noise(nat.NOISE_PHILOX, int(stream) & 0xFFFFFF, key, 0, None, int(stream_stride))
+    nat.check(nat.lib().vb_log_weights_rows(nat.context().handle, var_family._struct(),
+                                            logdensity._struct(), nat.dptr(lams), R, m, nz,
+                                            nat.dptr(lw)))
+    return lw
 
 
 def get_samples_and_log_weights(logdensity, var_family, var_param, n_samples):

@@ -85,18 +85,23 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
     import torch
     lw = torch.empty((len(ids), int(n_bounds)), dtype=torch.float64,
                      device=torch.device('cuda', nat.context().device))
-    bfams = []
-    for j, r in enumerate(ids):
-        bfam = family_factory()
-        bfam.stream = (1 << 20) + r          # bound draws: a Philox stream of their own
-        experiments.log_weights(target, bfam, smooth[j], n_bounds, return_samples=False,
-                                lw_out=lw[j])
-        bfams.append(bfam)
+    # bound draws: restart r uses Philox stream 2^20 + r of its own; all of this
+    # rank's restarts (ids = r0, r0 + stride, ...) in one launch
+    bfam = family_factory()
+    if ids == list(range(ids[0], ids[0] + stride * len(ids), stride)):
+        experiments.log_weights_rows(target, bfam, smooth, n_bounds, (1 << 20) + ids[0],
+                                     stride, lw_out=lw)
+    else:
+        for j, r in enumerate(ids):
+            fj = family_factory()
+            fj.stream = (1 << 20) + r
+            experiments.log_weights(target, fj, smooth[j], n_bounds, return_samples=False,
+                                    lw_out=lw[j])
     # the divergence statistics of all restarts in one batched reduction chain
     div = bounds.divergence_rows(lw)
     recs = []
     for j, r in enumerate(ids):
-        opt, bfam = smooth[j], bfams[j]
+        opt = smooth[j]
         res = bounds.all_bounds_from_divergence(
             div[j], moment_bound_fn=lambda p, bfam=bfam, opt=opt: bfam.pth_moment(p, opt),
             q_var=bfam.mean_and_cov(opt)[1])
