@@ -421,8 +421,15 @@ def leg_cfg4(cpu, host, steps=30):
            'roofline': {'bound': 'mfma', 'achieved': ach, 'peak': FP64_PEAK_TFLOPS,
                         'unit': 'TFLOP/s', 'frac': ach / FP64_PEAK_TFLOPS,
                         'algorithmic_flops_per_step': flops,
+                        # GEMMs one step executes (rocprofv3 timeline of a config-4 step,
+                        # profiles/r02/cfg4/step_timeline.txt: Sigma, Newton-Schulz
+                        # iteration 0 + 4 x (T, Y|Z), x / grad / G_S, PCG 1 + 7 + 6,
+                        # G_L): 29.75 products of 2 D^3
+                        'executed_flops_per_step': 29.75 * 2 * Dm ** 3,
+                        'executed_tflops': 29.75 * 2 * Dm ** 3 / dt / 1e12,
                         'note': 'whole step (all launches) timed on the host clock; flops = '
-                                '8 N D^2 + 20 D^3 (SURVEY §8d)'}}
+                                '8 N D^2 + 20 D^3 (SURVEY §8d); executed = the GEMM flops the '
+                                'Newton-Schulz + PCG step runs (profiled count)'}}
     if cpu:
         from oracle import fullrank_oracle as fo
         ofam = fo.FullRankT(Dm, 100.0)
