@@ -890,11 +890,11 @@ int fr_pcg(FrWork* W, int D, hipStream_t st) {
     g.dot_with = W->R.d();
     g.dot_part = W->rz_part.d();
     g.skip_flag = &sc->pcg_done;
-    if (it >= 0) {   // converged when ||R||^2 <= 1e-22 ||E||^2 (relative residual 1e-11)
+    if (it >= 0) {   // converged when ||R||^2 <= 1e-18 ||E||^2 (relative residual 1e-9)
       g.conv_part = W->rr_part.d();
       g.conv_n = nblk;
       g.conv_ref_dev = &sc->ee;
-      g.conv_tol2 = 1e-22;
+      g.conv_tol2 = 1e-18;
       g.conv_iter_out = &sc->pcg_iter;
       g.conv_iter = it;
     }
