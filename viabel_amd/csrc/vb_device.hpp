@@ -445,10 +445,16 @@ struct Mixture {
   __device__ __forceinline__ static double lp1(double x, double& g) {
     const double a = -0.5 * (x + 2.0) * (x + 2.0) - 0.5 * kLog2Pi;
     const double b = -0.5 * (x - 2.0) * (x - 2.0) - 0.5 * kLog2Pi;
-    // posterior weight of the +2 component: 1 / (1 + exp(a - b)), a - b = -4x
-    const double wb = 1.0 / (1.0 + exp(a - b));
+    // one exp serves both terms: with t = a - b (= -4x) and e = exp(-|t|),
+    // logaddexp(a, b) = max(a, b) + log1p(e) (numpy's form; t = 0 gives
+    // log1p(1) = log 2) and the posterior weight of the +2 component
+    // 1 / (1 + exp(t)) = 1 / (1 + e) for t <= 0, e / (1 + e) for t > 0
+    const double t = a - b;
+    const double e = exp(-fabs(t));
+    const double r = 1.0 / (1.0 + e);
+    const double wb = t > 0.0 ? e * r : r;
     g = -(x + 2.0) + 4.0 * wb;
-    return logaddexp(a, b) - kLn2;
+    return (t > 0.0 ? a : b) + log1p(e) - kLn2;
   }
 };
 
