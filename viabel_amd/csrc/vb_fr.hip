@@ -540,6 +540,12 @@ __global__ __launch_bounds__(256) void pcg_init_kernel(int D, const double* G, c
   if (threadIdx.x == 0) ee_part[blockIdx.y * gridDim.x + blockIdx.x] = a;
 }
 
+// The update kernels below issue every global load of the block (their tile of
+// C^T for the LDS transpose, their own elements, the partials) before the first
+// barrier, so the load latencies overlap instead of adding up; the partials are
+// summed in the same per-thread order as sum_parts (bitwise-identical totals).
+constexpr int kPer = kTile * kTile / 256;   // elements per thread
+
 // X += alpha P, R -= alpha (C + C^T), rr partials;  alpha = rz / <P, L(P)>,
 // <P, L(P)> = 2 sum(pq_part)
 __global__ __launch_bounds__(256) void pcg_xr_kernel(int D, int it, const double* C,
@@ -549,18 +555,39 @@ __global__ __launch_bounds__(256) void pcg_xr_kernel(int D, int it, const double
   __shared__ double s[kTile][kTile + 1];
   __shared__ double red[16];
   if (sc->pcg_done) return;
-  const double alpha = sc->rz[it & 1] / (2.0 * sum_parts(pq_part, n_pq, red));
-  __syncthreads();
   const int bi = blockIdx.y, bj = blockIdx.x;
-  TileT::load_t(C, D, bi, bj, s);
+  double ct[kPer], cv[kPer], pv[kPer], xv[kPer], rv[kPer];
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int q = threadIdx.x + 256 * e, r = q / kTile, cc = q % kTile;
+    const int tr = bj * kTile + r, tc = bi * kTile + cc;     // transposed tile element
+    ct[e] = (tr < D && tc < D) ? C[(long long)tr * D + tc] : 0.0;
+    const int i = bi * kTile + r, j = bj * kTile + cc;
+    const bool ok = i < D && j < D;
+    const long long idx = (long long)i * D + j;
+    cv[e] = ok ? C[idx] : 0.0;
+    pv[e] = ok ? P[idx] : 0.0;
+    xv[e] = ok ? X[idx] : 0.0;
+    rv[e] = ok ? R[idx] : 0.0;
+  }
+  double pq = 0.0;
+  for (int k = threadIdx.x; k < n_pq; k += 256) pq += pq_part[k];
+  const double rz = sc->rz[it & 1];
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int q = threadIdx.x + 256 * e;
+    s[q / kTile][q % kTile] = ct[e];
+  }
+  const double alpha = rz / (2.0 * block_sum(pq, red));   // barriers: s is complete
   double a = 0.0;
-  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
-    const int r = e / kTile, cc = e % kTile;
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int q = threadIdx.x + 256 * e, r = q / kTile, cc = q % kTile;
     const int i = bi * kTile + r, j = bj * kTile + cc;
     if (i < D && j < D) {
       const long long idx = (long long)i * D + j;
-      X[idx] = fma(alpha, P[idx], X[idx]);
-      const double rn = R[idx] - alpha * (C[idx] + s[cc][r]);
+      X[idx] = fma(alpha, pv[e], xv[e]);
+      const double rn = rv[e] - alpha * (cv[e] + s[cc][r]);
       R[idx] = rn;
       a += rn * rn;
     }
@@ -579,22 +606,43 @@ __global__ __launch_bounds__(256) void pcg_p_kernel(int D, int it, const double*
   __shared__ double s[kTile][kTile + 1];
   __shared__ double red[16];
   if (sc->pcg_done) return;
-  const double rz = 0.5 * sum_parts(rz_part, n_rz, red);
-  const double beta = it < 0 ? 0.0 : rz / sc->rz[it & 1];
+  const int bi = blockIdx.y, bj = blockIdx.x;
+  double ct[kPer], cv[kPer], pv[kPer];
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int q = threadIdx.x + 256 * e, r = q / kTile, cc = q % kTile;
+    const int tr = bj * kTile + r, tc = bi * kTile + cc;
+    ct[e] = (tr < D && tc < D) ? C[(long long)tr * D + tc] : 0.0;
+    const int i = bi * kTile + r, j = bj * kTile + cc;
+    const bool ok = i < D && j < D;
+    const long long idx = (long long)i * D + j;
+    cv[e] = ok ? C[idx] : 0.0;
+    pv[e] = (ok && it >= 0) ? P[idx] : 0.0;
+  }
+  double rzp = 0.0, eep = 0.0;
+  for (int k = threadIdx.x; k < n_rz; k += 256) rzp += rz_part[k];
+  if (it < 0)
+    for (int k = threadIdx.x; k < n_ee; k += 256) eep += ee_part[k];
+  const double rz_prev = it < 0 ? 1.0 : sc->rz[it & 1];
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int q = threadIdx.x + 256 * e;
+    s[q / kTile][q % kTile] = ct[e];
+  }
+  const double rz = 0.5 * block_sum(rzp, red);   // barriers: s is complete
+  const double beta = it < 0 ? 0.0 : rz / rz_prev;
   double ee = 0.0;
   if (it < 0) {
     __syncthreads();
-    ee = sum_parts(ee_part, n_ee, red);
+    ee = block_sum(eep, red);
   }
-  const int bi = blockIdx.y, bj = blockIdx.x;
-  TileT::load_t(C, D, bi, bj, s);
-  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
-    const int r = e / kTile, cc = e % kTile;
+#pragma unroll
+  for (int e = 0; e < kPer; ++e) {
+    const int q = threadIdx.x + 256 * e, r = q / kTile, cc = q % kTile;
     const int i = bi * kTile + r, j = bj * kTile + cc;
     if (i < D && j < D) {
-      const long long idx = (long long)i * D + j;
-      const double z = 0.25 * (C[idx] + s[cc][r]);
-      P[idx] = it < 0 ? z : fma(beta, P[idx], z);
+      const double z = 0.25 * (cv[e] + s[cc][r]);
+      P[(long long)i * D + j] = it < 0 ? z : fma(beta, pv[e], z);
     }
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
