@@ -1452,7 +1452,7 @@ int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, 
 // Reads back (one synchronisation) the outcome of the device-side iterations
 // since the last call: dsyevd's info, and the sticky Newton-Schulz / PCG status;
 // adapts the iteration counts launched next (one spare Newton-Schulz
-// iteration, two PCG iterations over the largest count seen).
+// iteration; PCG: the largest converged count seen, see below).
 int fr_info(FrWork* W, hipStream_t st) {
   int info = 0;
   const bool eig = W->info.p && W->eig_pending, sq = W->sched.p && W->sqrt_pending;
@@ -1475,8 +1475,12 @@ int fr_info(FrWork* W, hipStream_t st) {
                             "iterations", W->pcg_kmax);
   if (W->last_warm && h.hint_ns > 0)
     W->ns_kmax = std::min(kFrNSMax, std::max(h.hint_ns, h.ns_iter));
+  // PCG: the learnt count is the index of the converged iteration, so + 1
+  // launches exactly the iterations the hardest warm step so far needed (a later
+  // step needing one more stops one iteration short: ~10x the 1e-9 target
+  // residual, far inside the 1e-7 status bar; the next advance learns it)
   if (W->last_warm && h.hint_pcg >= 0)
-    W->pcg_kmax = std::min(40, std::max(h.hint_pcg, h.pcg_iter) + 2);
+    W->pcg_kmax = std::min(40, std::max(h.hint_pcg, h.pcg_iter) + 1);
   return 0;
 }
 
