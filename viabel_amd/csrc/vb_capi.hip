@@ -924,10 +924,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
         } else {
           VB_HIP(vbk::launch_adagrad_update((long long)P, lam, r->grad.d(),
                                             r->ring.d() + q * P * r->W, r->W, step, lr, r->eps,
-                                            nullptr, c->stream));
-          if (hrow)
-            VB_HIP(hipMemcpyAsync(hrow, lam, sizeof(double) * P, hipMemcpyDeviceToDevice,
-                                  c->stream));
+                                            nullptr, c->stream, hrow));
         }
       }
     }

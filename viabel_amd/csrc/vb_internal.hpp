@@ -114,7 +114,8 @@ hipError_t launch_log_weights(int fam, int tgt, int D, long long m, const double
 // scale (nullable): [min(step + 1, W)] window scales, oldest first
 hipError_t launch_adagrad_update(long long P, double* lam, const double* g, double* ring, int W,
                                  long long step, double lr, double eps, const double* scale,
-                                 hipStream_t s);
+                                 hipStream_t s,
+                                 double* hrow = nullptr);
 // RMSProp-IA / Adam-IA step (opt 1 / 2) on device state [2][P], or (opt 3)
 // RMSProp-IA with avg_grad_norm: every coordinate divided by sqrt(eps + norm2);
 // old_out (nullable) receives the pre-update parameters.

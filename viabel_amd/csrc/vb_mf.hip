@@ -1189,10 +1189,13 @@ __global__ __launch_bounds__(256) void target_row_kernel(int D, long long n, con
 __global__ __launch_bounds__(256) void adagrad_update_kernel(long long P, double* lam,
                                                              const double* g, double* ring,
                                                              int W, long long step, double lr,
-                                                             double eps, const double* scale) {
+                                                             double eps, const double* scale,
+                                                             double* hrow) {
   const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
   if (p >= P) return;
-  lam[p] = adagrad_step(p, P, lam[p], g[p], ring, W, step, lr, eps, scale);
+  const double v = adagrad_step(p, P, lam[p], g[p], ring, W, step, lr, eps, scale);
+  lam[p] = v;
+  if (hrow) hrow[p] = v;   // history row (vb.py:375-376) without a separate copy
 }
 
 __global__ __launch_bounds__(256) void ia_update_kernel(int opt, long long P, double* lam,
@@ -1824,9 +1827,9 @@ hipError_t launch_log_weights(int fam, int tgt, int D, long long m, const double
 
 hipError_t launch_adagrad_update(long long P, double* lam, const double* g, double* ring, int W,
                                  long long step, double lr, double eps, const double* scale,
-                                 hipStream_t s) {
+                                 hipStream_t s, double* hrow) {
   hipLaunchKernelGGL(adagrad_update_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P,
-                     lam, g, ring, W, step, lr, eps, scale);
+                     lam, g, ring, W, step, lr, eps, scale, hrow);
   return hipGetLastError();
 }
 
