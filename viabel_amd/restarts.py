@@ -21,7 +21,8 @@ import numpy as np
 
 from . import _native as nat
 
-__all__ = ['shard', 'run_restarts', 'gather_records', 'bind_local_device', 'RECORD_HEAD']
+__all__ = ['shard', 'run_restarts', 'gather_records', 'bind_local_device', 'bounds_records',
+           'RECORD_HEAD']
 
 RECORD_HEAD = ['restart', 'elbo', 'd2', 'W1', 'W2', 'mean_error', 'std_error', 'cov_error',
                'khat', 'final_value']
@@ -97,17 +98,10 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
             fj.stream = (1 << 20) + r
             experiments.log_weights(target, fj, smooth[j], n_bounds, return_samples=False,
                                     lw_out=lw[j])
-    # the divergence statistics of all restarts in one batched reduction chain
+    # the divergence statistics of all restarts in one batched reduction chain,
+    # then the O(D) bound algebra for all restarts at once on the host
     div = bounds.divergence_rows(lw)
-    recs = []
-    for j, r in enumerate(ids):
-        opt = smooth[j]
-        res = bounds.all_bounds_from_divergence(
-            div[j], moment_bound_fn=lambda p, bfam=bfam, opt=opt: bfam.pth_moment(p, opt),
-            q_var=bfam.mean_and_cov(opt)[1])
-        elbo = float(res['log_norm_bound'])  # = mean log weight (bounds.py:170-172)
-        recs.append([r, elbo, res['d2'], res['W1'], res['W2'], res['mean_error'],
-                     res['std_error'], res['cov_error']])
+    recs = bounds_records(ids, div, smooth, bfam)
     khat = psis.psislw(lw.t())[1] if len(ids) > 1 else np.array([psis.psislw(lw[0])[1]])
     if timings is not None:
         _sync()
@@ -116,6 +110,43 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
         timings['bounds_psis_s'] = t2 - t1
     return np.array([np.concatenate([rec, [khat[j], vals[j, -1]], smooth[j]])
                      for j, rec in enumerate(recs)])
+
+
+def bounds_records(ids, div, lams, fam):
+    """Per-restart [id, elbo, d2, W1, W2, mean_error, std_error, cov_error]:
+    `all_bounds(lw, moment_bound_fn=fam.pth_moment, q_var=fam.mean_and_cov)`
+    (bounds.py:13-61) for every row of `divergence_rows` at once.  The family's
+    2nd / 4th moments (vb.py:72-82, 168-182) and the spectral norm of its
+    diagonal covariance (bounds.py:64-67) are evaluated for all rows as arrays
+    instead of 64 sets of per-restart calls; the Monte Carlo warnings
+    (bounds.py:187-191) are issued per row as all_bounds does."""
+    from . import bounds
+    div = np.asarray(div, dtype=float)
+    lams = np.atleast_2d(np.asarray(lams, dtype=float))
+    D = fam.dim
+    for row in div:
+        bounds._mc_warning(row[2], row[3], 'CUBO')
+        bounds._mc_warning(row[4], row[5], 'ELBO')
+    d2 = div[:, 0]
+    v = np.exp(2 * lams[:, D:])                       # variances (Gaussian) / squared scales (t)
+    if fam.kind == nat.FAMILY_MF_GAUSSIAN:
+        C2 = np.sum(v, axis=1)
+        C4 = 2 * np.sum(v ** 2, axis=1) + np.sum(v, axis=1) ** 2
+        qnorm = np.max(v, axis=1)
+    else:
+        df = fam.df
+        if df <= 4:
+            raise ValueError('df must be greater than p')
+        c = df / (df - 2)
+        s = np.exp(lams[:, D:])
+        C2 = c * np.sum(s ** 2, axis=1)
+        C4 = c ** 2 * (2 * (df - 1) / (df - 4) * np.sum(s ** 4, axis=1) + np.sum(s ** 2, axis=1) ** 2)
+        qnorm = np.max(np.abs(c * v), axis=1)
+    W1 = 2 * C2 ** .5 * np.expm1(d2) ** .5
+    W2 = 2 * C4 ** .25 * np.expm1(d2) ** .25
+    cov_error = 2 * (np.sqrt(qnorm) * W2 + W2 ** 2)
+    return [[r, float(div[j, 1]), d2[j], W1[j], W2[j], min(W1[j], W2[j]), W2[j], cov_error[j]]
+            for j, r in enumerate(ids)]
 
 
 def gather_records(local, n_restarts, width, group=None):
