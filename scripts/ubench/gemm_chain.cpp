@@ -56,7 +56,9 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
+  const int only = argc > 2 ? atoi(argv[2]) : -1;   // run one mode (0 single, 1 dual, 2 group2)
   for (int mode = 0; mode < 3; ++mode) {
+    if (only >= 0 && mode != only) continue;
     for (int r = 0; r < 50; ++r) {
       if (mode == 2) {
         vbk::GemmOp g2[2] = {op(r % NSET, false), op((r + 1) % NSET, false)};
