@@ -6,9 +6,9 @@
 //
 // Block tile 32 x 32 computed by 8 waves: 4 output quadrants of 16 x 16 x 2 halves
 // of every k tile (intra-block split-K, reduced through LDS at the end), each
-// wave running 4 independent MFMA accumulator chains.  K is staged 64 at a time
-// through double-buffered LDS with the next tile's global loads in flight while
-// the current one feeds the MFMAs (one barrier per tile).
+// wave running 4 independent MFMA accumulator chains.  K is staged KT (32) at a
+// time through double-buffered LDS with the next tile's global loads in flight
+// while the current one feeds the MFMAs (one barrier per tile).
 // LDS layout per operand follows its contiguous global dimension so both the
 // coalesced store and the fragment read are conflict-free at the 2-pass minimum:
 //   contiguous in k  -> [row][k]  (stride 36 doubles)
@@ -111,23 +111,53 @@ constexpr int PER = BT * KT / NTH;                             // elements per t
 
 // One operand tile (BT rows x KT k) of a row-major matrix X with leading
 // dimension ld; KCONTIG: X is [row][k] in memory (k contiguous), else [k][row].
+// Loads are branch-free: an element outside the matrix reads element 0 and
+// is zeroed (and k-scaled) only at store time, so no use of a loaded value and
+// no per-lane branch sits between a tile's loads and its store to LDS.  The
+// compiler then waits (s_waitcnt vmcnt) for exactly the tile being stored while
+// the next tile's loads stay in flight; guarded loads had made it wait for every
+// outstanding load (vmcnt(0)) on each k tile.
 template <bool KCONTIG, bool KS>
 struct Tile {
   double v[PER];
-  __device__ __forceinline__ void load(const double* X, long long ld, int r0, int k0, int R,
-                                       int K, const double* kscale, int t) {
+  double ks[KS ? PER : 1];
+  bool ok[PER];
+  // loop-invariant per-thread layout: element offsets from the tile base (a
+  // uniform pointer), row in range, k within the tile
+  unsigned off[PER], offr[PER];   // offr: 0 when the row is out of range
+  int kk[PER];
+  bool rok[PER];
+  __device__ __forceinline__ void init(long long ld, int r0, int R, int t) {
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
       const int idx = t + NTH * e;
       const int r = KCONTIG ? idx / KT : idx % BT;
       const int k = KCONTIG ? idx % KT : idx / BT;
-      const int gr = r0 + r, gk = k0 + k;
-      double x = 0.0;
-      if (gr < R && gk < K) {
-        x = KCONTIG ? X[(long long)gr * ld + gk] : X[(long long)gk * ld + gr];
-        if (KS) x *= kscale[gk];
+      off[e] = KCONTIG ? (unsigned)(r * ld + k) : (unsigned)(k * ld + r);
+      rok[e] = r0 + r < R;
+      offr[e] = rok[e] ? off[e] : 0u;
+      kk[e] = k;
+    }
+  }
+  __device__ __forceinline__ void load(const double* X, long long ld, int r0, int k0, int K,
+                                       const double* kscale) {
+    const double* base = X + (KCONTIG ? (long long)r0 * ld + k0 : (long long)k0 * ld + r0);
+    const int kl = K - k0;
+    if (kl >= KT) {   // whole k tile inside K (uniform): invariant offsets, no per-load math
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        v[e] = base[offr[e]];
+        if constexpr (KS) ks[e] = kscale[k0 + kk[e]];
+        ok[e] = rok[e];
       }
-      v[e] = x;
+    } else {
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        const bool in = rok[e] && kk[e] < kl;
+        v[e] = base[in ? off[e] : 0u];
+        if constexpr (KS) ks[e] = kscale[in ? k0 + kk[e] : 0];
+        ok[e] = in;
+      }
     }
   }
   __device__ __forceinline__ void store(double* s, int t) const {
@@ -136,7 +166,8 @@ struct Tile {
       const int idx = t + NTH * e;
       const int r = KCONTIG ? idx / KT : idx % BT;
       const int k = KCONTIG ? idx % KT : idx / BT;
-      s[KCONTIG ? r * SR + k : k * SK + r] = v[e];
+      const double x = KS ? v[e] * ks[KS ? e : 0] : v[e];
+      s[KCONTIG ? r * SR + k : k * SK + r] = ok[e] ? x : 0.0;
     }
   }
 };
@@ -218,16 +249,21 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
   auto src_a = [&](int it) { return (DUAL && it >= nt1) ? g.A2 : g.A; };
   auto src_b = [&](int it) { return (DUAL && it >= nt1) ? g.B2 : g.B; };
   auto koff = [&](int it) { return (DUAL && it >= nt1 ? it - nt1 : it) * KT; };
+  // prefetches past the last tile re-read the last one (unconditional loads keep
+  // the instruction stream straight for the waitcnt placement; the copy is unused)
+  auto cl = [&](int it) { return it < nt ? it : nt - 1; };
   // two register stages: tile it+2 is loaded while tile it feeds the MFMAs
   // and tile it+1 (loaded one iteration earlier) moves to LDS
   Tile<AK, KS> ta0, ta1;
   Tile<BK, false> tb0, tb1;
-  ta0.load(src_a(0), g.lda, i0, koff(0), g.M, g.K, g.kscale, t);
-  tb0.load(src_b(0), g.ldb, j0, koff(0), g.N, g.K, nullptr, t);
-  if (nt > 1) {
-    ta1.load(src_a(1), g.lda, i0, koff(1), g.M, g.K, g.kscale, t);
-    tb1.load(src_b(1), g.ldb, j0, koff(1), g.N, g.K, nullptr, t);
-  }
+  ta0.init(g.lda, i0, g.M, t);
+  ta1.init(g.lda, i0, g.M, t);
+  tb0.init(g.ldb, j0, g.N, t);
+  tb1.init(g.ldb, j0, g.N, t);
+  ta0.load(src_a(0), g.lda, i0, koff(0), g.K, g.kscale);
+  tb0.load(src_b(0), g.ldb, j0, koff(0), g.K, nullptr);
+  ta1.load(src_a(cl(1)), g.lda, i0, koff(cl(1)), g.K, g.kscale);
+  tb1.load(src_b(cl(1)), g.ldb, j0, koff(cl(1)), g.K, nullptr);
   ta0.store(sA[0], t);
   tb0.store(sB[0], t);
   __syncthreads();
@@ -260,10 +296,8 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
     }
   };
   for (int it = 0; it < nt; it += 2) {
-    if (it + 2 < nt) {
-      ta0.load(src_a(it + 2), g.lda, i0, koff(it + 2), g.M, g.K, g.kscale, t);
-      tb0.load(src_b(it + 2), g.ldb, j0, koff(it + 2), g.N, g.K, nullptr, t);
-    }
+    ta0.load(src_a(cl(it + 2)), g.lda, i0, koff(cl(it + 2)), g.K, g.kscale);
+    tb0.load(src_b(cl(it + 2)), g.ldb, j0, koff(cl(it + 2)), g.K, nullptr);
     mma(sA[0], sB[0], it);
     if (it + 1 < nt) {
       ta1.store(sA[1], t);
@@ -271,10 +305,8 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
     }
     __syncthreads();
     if (it + 1 >= nt) break;
-    if (it + 3 < nt) {
-      ta1.load(src_a(it + 3), g.lda, i0, koff(it + 3), g.M, g.K, g.kscale, t);
-      tb1.load(src_b(it + 3), g.ldb, j0, koff(it + 3), g.N, g.K, nullptr, t);
-    }
+    ta1.load(src_a(cl(it + 3)), g.lda, i0, koff(cl(it + 3)), g.K, g.kscale);
+    tb1.load(src_b(cl(it + 3)), g.ldb, j0, koff(cl(it + 3)), g.K, nullptr);
     mma(sA[1], sB[1], it + 1);
     if (it + 2 < nt) {
       ta0.store(sA[0], t);
