@@ -11,7 +11,7 @@
 // while the current one feeds the MFMAs (one barrier per tile).
 // LDS layout per operand follows its contiguous global dimension so both the
 // coalesced store and the fragment read are conflict-free at the 2-pass minimum:
-//   contiguous in k  -> [row][k]  (stride 36 doubles)
+//   contiguous in k  -> [row][k]  (stride 34 doubles)
 //   contiguous in row -> [k][row] (stride 48 doubles)
 // MFMA operand maps (cdna_hip_programming.md): A[l&15][k=l>>4], B[k=l>>4][l&15];
 // C row = (l>>4) + 4 r, col = l&15.
@@ -99,7 +99,8 @@ constexpr int BT = 32;   // block tile (rows and columns)
 #define VB_GEMM_KT 32
 #endif
 constexpr int KT = VB_GEMM_KT;  // k tile
-constexpr int SR = KT + 4;      // [row][k] stride
+constexpr int SR = KT + 2;      // [row][k] stride: 2 SR = 4 (mod 64 banks), so a 32-lane
+                                // pass of fragment reads (16 rows x 2 k) hits 64 distinct banks
 constexpr int SK = BT + 16;     // [k][row] stride
 constexpr int BUF = (BT * SR > KT * SK) ? BT * SR : KT * SK;  // doubles per operand buffer
 #ifndef VB_GEMM_KSPLIT
