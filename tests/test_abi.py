@@ -130,3 +130,33 @@ def test_host_side_closed_forms():
         np.testing.assert_array_equal(m, om)
         np.testing.assert_allclose(c, oc, rtol=1e-15)
         assert fam.var_param_dim == 6
+
+
+def test_viabel_namespace_is_the_device_implementation():
+    """`from viabel import ...` (reference tests/test_bounds.py:1-2,
+    viabel/__init__.py:1), `viabel.vb`, `viabel.bounds`, `viabel.functions` and
+    the notebooks' top-level `psis` / `experiments` resolve to viabel_amd."""
+    import importlib
+    import viabel
+    import viabel_amd
+    from viabel import all_bounds, error_bounds, wasserstein_bounds, divergence_bound
+    assert all_bounds is viabel_amd.bounds.all_bounds
+    assert divergence_bound is viabel_amd.divergence_bound
+    assert (error_bounds, wasserstein_bounds) == (viabel_amd.error_bounds,
+                                                  viabel_amd.wasserstein_bounds)
+    vbm = importlib.import_module('viabel.vb')
+    assert vbm is viabel_amd.vb is viabel.vb
+    assert importlib.import_module('viabel.bounds') is viabel_amd.bounds
+    assert importlib.import_module('viabel.functions') is viabel_amd.functions
+    from viabel.vb import (mean_field_gaussian_variational_family, black_box_klvi,  # noqa: F401
+                           black_box_chivi, adagrad_optimize, t_variational_family)
+    from viabel.bounds import mean_and_check_mc_error  # noqa: F401
+    psis = importlib.import_module('psis')
+    assert psis is viabel_amd.psis
+    from psis import psislw, gpdfitnew, gpinv, sumlogs  # noqa: F401
+    assert importlib.import_module('experiments') is viabel_amd.experiments
+    # the same errors as the reference, before any device work
+    with pytest.raises(ValueError, match='alpha must be greater than 1'):
+        divergence_bound(np.zeros(3), alpha=1.0)
+    with pytest.raises(ValueError, match='must provides samples'):
+        wasserstein_bounds(1.0)

@@ -119,3 +119,52 @@ def test_log_weights_rows_equal_per_row_calls(case):
         f.stream = 100 + 3 * r
         _, lw = experiments.log_weights(tgt, f, lams[r], m, return_samples=False)
         np.testing.assert_array_equal(rows[r], lw)
+
+
+def _per_restart_records(fac, tgt, R, n_iters, N, M):
+    """The fallback path spelled out with the single-call API: one DeviceRun
+    for all restarts (restart r: Philox stream 1 + r), then per restart
+    log_weights on stream 2^20 + r, all_bounds with the family's own moments
+    and covariance (bounds.py:13-61) and psislw."""
+    from viabel_amd import vb, experiments, bounds, psis, restarts
+    fam = fac()
+    P = fam.var_param_dim
+    inits = restarts.default_inits(R, P)
+    run = vb.DeviceRun(vb.black_box_klvi(fam, tgt, N), n_iters, inits, learning_rate=.01,
+                       learning_rate_end=.001)
+    run.advance_philox(n_iters, 0, 1, 0)
+    _, _, vals, smooth = run.result()
+    out = []
+    for r in range(R):
+        f = fac()
+        f.stream = (1 << 20) + r
+        _, lw = experiments.log_weights(tgt, f, smooth[r], M, return_samples=False)
+        res = bounds.all_bounds(lw, moment_bound_fn=lambda p, l=smooth[r]: fam.pth_moment(p, l),
+                                q_var=fam.mean_and_cov(smooth[r])[1])
+        k = psis.psislw(lw)[1]
+        out.append(np.concatenate([[r, np.mean(lw), res['d2'], res['W1'], res['W2'],
+                                    res['mean_error'], res['std_error'], res['cov_error'], k,
+                                    vals[r, -1]], smooth[r]]))
+    return np.array(out)
+
+
+@pytest.mark.parametrize('case', ['full_rank_t', 'callback_target'])
+def test_run_restarts_fallback_families_and_targets(case):
+    """Families / targets the batched bound kernel does not cover (full-rank q,
+    host-callback targets) take the per-restart log-weight path and the
+    family's own moments (no VB_EUNSUPPORTED after the fit, no mean-field
+    moment formulas applied to a full-rank q)."""
+    from viabel_amd import vb, targets, restarts
+    R, n_iters, N, M = 3, 25, 16, 3000
+    if case == 'full_rank_t':
+        fac = lambda: vb.t_variational_family(3, 10.0, rng='philox')
+        tgt = targets.isogauss(3)
+    else:
+        fac = lambda: vb.mean_field_t_variational_family(3, 10.0, rng='philox')
+        tgt = targets.callback(lambda x: (-0.5 * np.sum(x ** 2, axis=1), -x), 3)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        table = restarts.run_restarts(fac, tgt, R, n_iters, n_samples=N, n_bounds=M)
+        expect = _per_restart_records(fac, tgt, R, n_iters, N, M)
+    assert table.shape == expect.shape
+    np.testing.assert_allclose(table, expect, rtol=1e-12, atol=1e-14)

@@ -374,6 +374,16 @@ def test_adagrad_chunked_progress_and_interrupt(monkeypatch):
     run2.advance_philox(1000, seed2, stream2, step2)
     np.testing.assert_array_equal(part[2], run2.values()[:1000])
     assert part[1].shape == (0, 2 * D) and np.all(np.isnan(part[0]))
+    # an interrupt landing after an advance returned (before the caller counted
+    # it): the result covers every step the device ran
+    def late(self, *a, **k):
+        orig(self, *a, **k)
+        raise KeyboardInterrupt
+    monkeypatch.setattr(vb.DeviceRun, 'advance_philox', late)
+    fam3 = vb.mean_field_gaussian_variational_family(D, rng='philox')
+    obj3 = vb.black_box_klvi(fam3, targets.funnel(D), N)
+    part3 = vb.adagrad_optimize(n_iters, obj3, init, learning_rate=0.02, learning_rate_end=0.005)
+    assert part3[2].shape == (1000,)
 
 
 # ---------------------------------------------------------------------------

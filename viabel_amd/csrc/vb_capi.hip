@@ -897,7 +897,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
                                     noise->stream + (uint32_t)q * stride,
                                     (uint32_t)(noise->step + off),
                                     r->values.d() + q * r->n_iters + step, r->grad.d(), c->stream,
-                                    r->nprob == 1 && step > 0));
+                                    r->nprob == 1 && step > 0, r));
         double* hrow = step >= r->hist_start
                            ? r->hist.d() + (q * r->n_hist + (step - r->hist_start)) * P
                            : nullptr;

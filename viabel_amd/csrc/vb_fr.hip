@@ -687,6 +687,7 @@ struct FrWork {
   bool warm = false;              // pv hold the previous root's vectors
   bool zv_init = false;           // pv[2..3] hold a Z power vector
   bool last_warm = false;         // the last root was a warm one (iteration hints apply)
+  const void* owner = nullptr;    // the run whose root the warm state above holds
   int ns_kmax = 12, pcg_kmax = 14;  // iterations launched (device skips past convergence)
   int last_kmax = 12;             // Newton-Schulz iterations the last root launched
   bool eig_pending = false;       // a dsyevd ran since the last fr_info
@@ -825,7 +826,7 @@ int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st) {
 // run), so 3 warm-started power steps suffice and l_0 comes from the previous
 // root; otherwise 8 power steps from ones and l_0 = 0.05.
 // Also: L, Sigma = L L^T, scal[0] = 0.5 log det Sigma = sum log L_ii.
-int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm) {
+int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, const void* owner) {
   if (int rc = reserve_d(W, D, st)) return rc;
   const long long dd = (long long)D * D;
   const int nblk = ((D + 31) / 32) * ((D + 31) / 32);
@@ -836,8 +837,12 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm) {
     g.sq_part = W->fro_part.d();
     FR_HIP(gemm(g, st));
   }
-  // power steps: Sigma x and Z_prev u (the previous root's vectors as start)
-  warm = warm && W->warm;
+  // power steps: Sigma x and Z_prev u (the previous root's vectors as start).
+  // Warm state (previous root, power vectors, learnt iteration counts) belongs
+  // to the run that made it: any other caller's root (another run, a cold
+  // log-weight or single-call root) invalidates it
+  warm = warm && W->warm && owner != nullptr && W->owner == owner;
+  W->owner = owner;
   // a cold root starts a new problem: forget the iteration counts learnt on the
   // previous one (fr_info learns them again from this run's warm steps)
   if (!warm) {
@@ -883,6 +888,7 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm) {
     t.sq_part = tp;
     t.sq_shift_dev = &sc->shift[k];
     t.skip_flag = &sc->ns_conv;
+    t.skip_tag = 2 * k + 1;
     t.skip_flag2 = &sc->ns_fin;
     FR_HIP(gemm(t, st));
     GemmOp yz[2] = {mm(D, D, D, Yk, false, W->T.d(), false, W->Yb[(k + 1) & 1].d()),
@@ -891,6 +897,7 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm) {
       GemmOp& g = yz[o];
       g.alpha_dev = &sc->halpha[k];
       g.skip_flag = &sc->ns_conv;
+      g.skip_tag = 2 * k + 2;
       // the root ends in buffer (kmax + 1) & 1: the first skipped launch copies
       // it there when it sits in the other one
       g.copy_src = ((k & 1) != ((kmax + 1) & 1)) ? (o == 0 ? Yk : Zk) : nullptr;
@@ -945,6 +952,7 @@ int fr_pcg(FrWork* W, int D, hipStream_t st) {
       g.conv_tol2 = 1e-18;
       g.conv_iter_out = &sc->pcg_iter;
       g.conv_iter = it;
+      g.skip_tag = it + 1;
     }
     return g;
   };
@@ -1023,9 +1031,9 @@ int fr_target(FrWork* W, int tgt, int D, long long n, const double* tparams, dou
 // and the value into *value (device pointers).
 int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* host_eps,
                   uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
-                  double* grad, hipStream_t st, bool warm) {
+                  double* grad, hipStream_t st, bool warm, const void* owner) {
   const int D = f.D, N = f.N;
-  if (int rc = fr_sqrt(W, D, lam, st, warm)) return rc;
+  if (int rc = fr_sqrt(W, D, lam, st, warm, owner)) return rc;
   if (int rc = reserve_n(W, D, N)) return rc;
   const double *s, *z;
   if (int rc = fr_draw(W, D, N, f.df, host_eps, k0, k1, stream, step, &s, &z, st)) return rc;

@@ -46,12 +46,18 @@ struct GemmOp {
   // ---- device-resident scalars and control (the sync-free full-rank step) ----
   const double* alpha_dev;     // alpha (and alpha2) *= *alpha_dev
   const double* sq_shift_dev;  // overrides sq_shift
-  // skip: when *skip_flag != 0 the block copies copy_src into C (if given) or
-  // returns.  Convergence test run first by every block, in the same fixed
-  // order: s = conv_scale * sum(conv_part[0, conv_n)); if s <= conv_tol2 *
-  // (*conv_ref or 1) the block sets *skip_flag = 1 and writes conv_iter to
-  // *conv_iter_out (when the flag was clear on entry), then skips.
+  // skip: when *skip_flag was set by an EARLIER launch the block copies copy_src
+  // into C (if given) or returns.  Convergence test run first by every block, in
+  // the same fixed order: s = conv_scale * sum(conv_part[0, conv_n)); if s <=
+  // conv_tol2 * (*conv_ref or 1) the block sets *skip_flag = skip_tag and writes
+  // conv_iter to *conv_iter_out, then skips.  A launch that writes the flag
+  // carries a tag (> 0) distinct from every other launch that writes the same
+  // flag in one step: a block that finds its OWN launch's tag (a peer block got
+  // there first) ignores it and runs the test itself -- every block sums the same
+  // partials in the same order, so all decide alike, and no block depends on the
+  // order in which peers' stores to the flag and to conv_iter_out become visible.
   int* skip_flag;
+  int skip_tag;
   const double* copy_src;
   const double* conv_part;
   int conv_n;
@@ -73,8 +79,10 @@ struct GemmOp {
   int* fin_flag;
   double conv_fin_tol2;
   const int* skip_flag2;
-  // copy_src applies only when *conv_iter_out == copy_if_iter (-1: always), i.e.
-  // only in the first skipped launch after convergence
+  // copy_src applies only in the first skipped launch after convergence
+  // (copy_if_iter = that launch's iteration; -1: always): the launch whose own
+  // test converged (conv_iter == copy_if_iter), or a launch skipped by an earlier
+  // one with *conv_iter_out == copy_if_iter
   int copy_if_iter;
   // optional: per-wave partial sums of dot_with_ij * C_ij (before beta), 4 per block
   const double* dot_with;
@@ -178,10 +186,12 @@ __device__ __forceinline__ double frag(const double* s, int r, int k) {
   return KCONTIG ? s[r * SR + k] : s[k * SK + r];
 }
 
-// Block-uniform skip decision (see GemmOp::skip_flag).  Every block sums the
-// partials in the same order, so all blocks decide alike.
-__device__ __forceinline__ bool gemm_skip(const GemmOp& g, double* red) {
-  if (!g.skip_flag) return false;
+// Block-uniform skip decision (see GemmOp::skip_flag): 0 = compute the tile;
+// 1 = skipped (converged in an earlier launch); 2 = skipped (this launch's own
+// convergence test).  Every block sums the partials in the same order, so all
+// blocks decide alike.
+__device__ __forceinline__ int gemm_skip(const GemmOp& g, double* red) {
+  if (!g.skip_flag) return 0;
   __shared__ int s_skip;
   const int t = threadIdx.x;
   if (g.conv_part) {
@@ -202,10 +212,13 @@ __device__ __forceinline__ bool gemm_skip(const GemmOp& g, double* red) {
   }
   __syncthreads();
   if (t == 0) {
-    int sk = *g.skip_flag != 0;
+    const int tag = g.skip_tag > 0 ? g.skip_tag : 1;
+    const int f = __hip_atomic_load(g.skip_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a flag holding this launch's own tag was set by a peer block: ignore it
+    int sk = (f != 0 && !(g.skip_tag > 0 && f == g.skip_tag)) ? 1 : 0;
     if (!sk && g.skip_flag2 && *g.skip_flag2 != 0) {
       sk = 1;
-      *g.skip_flag = 1;
+      __hip_atomic_store(g.skip_flag, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!sk && g.conv_part) {
       double a = 0.0, b = 0.0;
@@ -218,9 +231,9 @@ __device__ __forceinline__ bool gemm_skip(const GemmOp& g, double* red) {
       const double ref = g.conv_ref_dev ? *g.conv_ref_dev : 1.0;
       const bool stall = g.conv_prev_part && a <= g.conv_stall_tol2 * ref && a * 16.0 >= b;
       if (a <= g.conv_tol2 * ref || stall) {
-        sk = 1;
-        *g.skip_flag = 1;
+        sk = 2;
         if (g.conv_iter_out) *g.conv_iter_out = g.conv_iter;
+        __hip_atomic_store(g.skip_flag, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else if (g.fin_flag && a <= g.conv_fin_tol2 * ref) {
         *g.fin_flag = 1;
         if (g.conv_iter_out) *g.conv_iter_out = g.conv_iter + 1;
@@ -229,7 +242,7 @@ __device__ __forceinline__ bool gemm_skip(const GemmOp& g, double* red) {
     s_skip = sk;
   }
   __syncthreads();
-  return s_skip != 0;
+  return s_skip;
 }
 
 // One BT x BT output tile (bx, by) of g (the whole block, NTH threads).  ntx =
@@ -380,8 +393,12 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   const GemmOp& g = gg.op[blockIdx.z];
   __shared__ double sA[2][BUF];
   __shared__ double sB[2][BUF];
-  if (gemm_skip(g, sB[1])) {
-    if (g.copy_src && (g.copy_if_iter < 0 || *g.conv_iter_out == g.copy_if_iter)) {
+  if (const int sk = gemm_skip(g, sB[1])) {
+    // the copy decision uses this block's own test (sk == 2) or state written
+    // by earlier launches (sk == 1), never a peer block's stores in this launch
+    const bool first = g.copy_if_iter < 0 ||
+                       (sk == 2 ? g.conv_iter == g.copy_if_iter : *g.conv_iter_out == g.copy_if_iter);
+    if (g.copy_src && first) {
       for (int e = threadIdx.x; e < BT * BT; e += NTH) {
         const int row = blockIdx.y * BT + e / BT, col = blockIdx.x * BT + e % BT;
         if (row < g.M && col < g.N)

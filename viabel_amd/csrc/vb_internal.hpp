@@ -204,7 +204,8 @@ struct FrSpec {
 // All return 0 or a VB_E* code (message via vb_set_error).
 int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st);  // eigh of Sigma
 // Newton-Schulz sqrtm; warm: Sigma is close to the previous call's (optimisation run)
-int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm = false);
+int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm = false,
+            const void* owner = nullptr);
 constexpr int kFrNSMax = 40;  // Newton-Schulz iterations launched at most per root
 int fr_draw(FrWork* W, int D, long long n, double df, const double* host_eps, uint32_t k0,
             uint32_t k1, uint32_t stream, uint32_t step, const double** s_out,
@@ -215,7 +216,8 @@ int fr_target(FrWork* W, int tgt, int D, long long n, const double* tparams, dou
               const double* x, double* logp, double* G, hipStream_t st);
 int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* host_eps,
                   uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
-                  double* grad, hipStream_t st, bool warm = false);
+                  double* grad, hipStream_t st, bool warm = false,
+                  const void* owner = nullptr);
 int fr_logdensity(FrWork* W, int D, double df, double t_const, const double* lam, const double* x,
                   long long n, double* out, hipStream_t st);
 int fr_log_weights(FrWork* W, const FrSpec& f, const double* lam, long long m,

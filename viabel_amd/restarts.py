@@ -59,6 +59,23 @@ def _sync():
     nat.context().synchronize()
 
 
+# the batched bound-draw kernel (vb_log_weights_rows) covers the block kernel's
+# target dimensions (vb_internal.hpp kBlockDMax) or separable targets at any D
+_ROWS_DMAX = 16
+
+
+def _rows_supported(fam, target):
+    """Whether vb_log_weights_rows accepts this family and target
+    (vb_capi.hip vb_log_weights_rows: mean-field family, device target,
+    separable or D <= 16)."""
+    from .targets import Target
+    if fam.kind == nat.FAMILY_FR_T or not isinstance(target, Target):
+        return False
+    if target.kind == nat.TARGET_CALLBACK:
+        return False
+    return target.separable or fam.dim <= _ROWS_DMAX
+
+
 def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bounds,
                     learning_rate, learning_rate_end, window, seed, stream_base, stride,
                     timings=None):
@@ -87,9 +104,13 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
     lw = torch.empty((len(ids), int(n_bounds)), dtype=torch.float64,
                      device=torch.device('cuda', nat.context().device))
     # bound draws: restart r uses Philox stream 2^20 + r of its own; all of this
-    # rank's restarts (ids = r0, r0 + stride, ...) in one launch
+    # rank's restarts (ids = r0, r0 + stride, ...) in one launch where the
+    # batched kernel covers the family and target (mean-field family, a device
+    # target that is separable or has D <= 16), else one launch per restart
     bfam = family_factory()
-    if ids == list(range(ids[0], ids[0] + stride * len(ids), stride)):
+    batched = (_rows_supported(bfam, target)
+               and ids == list(range(ids[0], ids[0] + stride * len(ids), stride)))
+    if batched:
         experiments.log_weights_rows(target, bfam, smooth, n_bounds, (1 << 20) + ids[0],
                                      stride, lw_out=lw)
     else:
@@ -101,7 +122,18 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
     # the divergence statistics of all restarts in one batched reduction chain,
     # then the O(D) bound algebra for all restarts at once on the host
     div = bounds.divergence_rows(lw)
-    recs = bounds_records(ids, div, smooth, bfam)
+    if bfam.kind == nat.FAMILY_FR_T:
+        # full-rank q: the family's own moments and covariance (eigenvalues of
+        # Sigma on the device), restart by restart, as all_bounds does
+        recs = []
+        for j, r in enumerate(ids):
+            res = bounds.all_bounds_from_divergence(
+                div[j], lambda p, lam=smooth[j]: bfam.pth_moment(p, lam),
+                q_var=bfam.mean_and_cov(smooth[j])[1])
+            recs.append([r, float(div[j, 1]), res['d2'], res['W1'], res['W2'],
+                         res['mean_error'], res['std_error'], res['cov_error']])
+    else:
+        recs = bounds_records(ids, div, smooth, bfam)
     khat = psis.psislw(lw.t())[1] if len(ids) > 1 else np.array([psis.psislw(lw[0])[1]])
     if timings is not None:
         _sync()
@@ -121,6 +153,9 @@ def bounds_records(ids, div, lams, fam):
     instead of 64 sets of per-restart calls; the Monte Carlo warnings
     (bounds.py:187-191) are issued per row as all_bounds does."""
     from . import bounds
+    if fam.kind not in (nat.FAMILY_MF_GAUSSIAN, nat.FAMILY_MF_T):
+        raise ValueError('bounds_records: mean-field families only (a full-rank q needs its '
+                         'own moments: all_bounds_from_divergence per restart)')
     div = np.asarray(div, dtype=float)
     lams = np.atleast_2d(np.asarray(lams, dtype=float))
     D = fam.dim

@@ -452,6 +452,14 @@ class DeviceRun:
         nat.check(nat.lib().vb_run_result(self.handle, None, None, nat.dptr(vals), None))
         return vals[0]
 
+    def steps_done(self):
+        """Steps the library has run (vb_run_steps_done): the truth after an
+        interrupt, whatever the caller's own counter says."""
+        import ctypes
+        n = ctypes.c_int64()
+        nat.check(nat.lib().vb_run_steps_done(self.handle, ctypes.byref(n)))
+        return int(n.value)
+
     def synchronize(self):
         nat.context().synchronize()
 
@@ -509,6 +517,9 @@ def _native_adagrad(n_iters, obj, init_param, window, learning_rate, epsilon,
     finally:
         if bar is not None:
             bar.close()
+    # a ctypes call cannot be interrupted, but the interrupt may land between an
+    # advance returning and `done` being updated: the run's own count is the truth
+    done = run.steps_done()
     _, hist, vals, smooth = run.result()
     if done == n_iters:
         return smooth[0], hist[0], vals[0], np.zeros(n_iters)
