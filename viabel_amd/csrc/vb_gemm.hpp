@@ -396,9 +396,14 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   if (const int sk = gemm_skip(g, sB[1])) {
     // the copy decision uses this block's own test (sk == 2) or state written
     // by earlier launches (sk == 1), never a peer block's stores in this launch
-    const bool first = g.copy_if_iter < 0 ||
-                       (sk == 2 ? g.conv_iter == g.copy_if_iter : *g.conv_iter_out == g.copy_if_iter);
-    if (g.copy_src && first) {
+    // (launches without copy_src or conv_iter_out never look at the counter)
+    bool first = false;
+    if (g.copy_src) {
+      if (g.copy_if_iter < 0) first = true;
+      else if (sk == 2) first = g.conv_iter == g.copy_if_iter;
+      else if (g.conv_iter_out) first = *g.conv_iter_out == g.copy_if_iter;
+    }
+    if (first) {
       for (int e = threadIdx.x; e < BT * BT; e += NTH) {
         const int row = blockIdx.y * BT + e / BT, col = blockIdx.x * BT + e % BT;
         if (row < g.M && col < g.N)
