@@ -91,6 +91,9 @@ struct GemmOp {
   // ns0_z = ns0[2] (3 I - ns0[3] Sigma), written for the same tile
   const double* ns0;
   double* ns0_z;
+  // set by gemm_group: M, N, K multiples of 32, 16-byte aligned operand rows, no
+  // kscale / dual product -> the LDS-DMA main loop
+  int glds;
 };
 
 // Up to two independent GEMMs of equal shape / transposes in one launch
@@ -245,18 +248,157 @@ __device__ __forceinline__ int gemm_skip(const GemmOp& g, double* red) {
   return s_skip;
 }
 
+// ---- LDS-DMA main loop (M, N, K multiples of 32; no kscale / dual product) ----
+// Operand tiles go global -> LDS directly (global_load_lds_dwordx4: no VGPR
+// staging, so no register of an in-flight load is ever reused and the loop
+// keeps GS - 1 tiles in flight across its barriers).  A tile is 32 "rows" of 32
+// doubles, a row = the operand's contiguous global dimension: one wave
+// instruction moves 1 KB = 4 rows, each lane 16 B (a pair of doubles).  The LDS
+// destination of a lane is fixed (wave base + 16 lane), so the bank swizzle is
+// applied to the GLOBAL address: LDS slot s of row r holds element s ^ sw(r)
+// (pairs stay pairs: sw even).
+//   rows = m / n, k contiguous (A, or B^T):  sw(r) = 2 (r & 15)  -- a fragment
+//     read (16 rows x 2 k per 32 lanes) then covers 64 distinct banks;
+//   rows = k, m / n contiguous (A^T, or B): sw(r) = 16 (r & 1)   -- rows k, k+1
+//     land in opposite bank halves.
+#ifndef VB_GEMM_GS
+#define VB_GEMM_GS 4
+#endif
+constexpr int GS = VB_GEMM_GS; // LDS stages (tiles it+1 .. it+GS-1 in flight)
+constexpr int TD = BT * KT;    // doubles per operand tile
+constexpr int SMEM = (4 * BUF > 2 * GS * TD) ? 4 * BUF : 2 * GS * TD;  // doubles of LDS per block
+template <bool KROWS>
+__device__ __forceinline__ int swz(int r) { return KROWS ? 2 * (r & 15) : 16 * (r & 1); }
+
+// Global element offset (from the tile origin) that lane `lane` of wave `w`
+// loads for its 16-byte LDS slot; ld = leading dimension.
+template <bool KROWS>
+__device__ __forceinline__ long long glds_src(int w, int lane, long long ld) {
+  const int r = 4 * w + (lane >> 4);          // tile row
+  const int s = 2 * (lane & 15);              // LDS slot (doubles) within the row
+  return (long long)r * ld + (s ^ swz<KROWS>(r));
+}
+
+// LDS offset (doubles) of fragment element (row r, column c) of a tile laid
+// out with `rows` = r.
+template <bool KROWS>
+__device__ __forceinline__ int glds_at(int r, int c) { return r * 32 + (c ^ swz<KROWS>(r)); }
+
+template <int STG>
+__device__ __forceinline__ void vm_wait_tiles(int pending) {
+  // each wave has 2 LDS-DMA instructions per tile (A, B) in flight
+  if (pending >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (pending == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (pending == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool TA, bool TB>
+__device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, double* lds,
+                                              d4 (&acc)[4]) {
+  // A rows: m when not transposed (k contiguous), k when transposed.
+  // B rows: n when transposed (k contiguous), k otherwise.
+  constexpr bool AK = !TA, BK = TB;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int q = w & 3, h = w >> 2;
+  const int wm = q >> 1, wn = q & 1;
+  double* sA = lds;                 // [GS][TD]
+  double* sB = lds + GS * TD;       // [GS][TD]
+  const int nt = g.K / KT;
+  // per-lane global sources: tile origin + fixed offset; the origin moves by KT
+  // along k each tile (k is the row index of the "rows = k" layouts)
+  const double* a0 = g.A + (AK ? (long long)i0 * g.lda : (long long)i0);
+  const double* b0 = g.B + (BK ? (long long)j0 * g.ldb : (long long)j0);
+  const long long aoff = glds_src<AK>(w, lane, g.lda), boff = glds_src<BK>(w, lane, g.ldb);
+  const long long astep = AK ? KT : (long long)KT * g.lda;
+  const long long bstep = BK ? KT : (long long)KT * g.ldb;
+  auto issue = [&](int it) {
+    const int st = it % GS;
+    __builtin_amdgcn_global_load_lds((const void*)(a0 + it * astep + aoff),
+                                     (void*)(sA + st * TD + 128 * w), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(b0 + it * bstep + boff),
+                                     (void*)(sB + st * TD + 128 * w), 16, 0, 0);
+  };
+#pragma unroll
+  for (int s = 0; s < GS - 1; ++s)
+    if (s < nt) issue(s);
+  // fragment offsets within a stage for the 4 k4-steps of this wave's k part
+  const int ra = wm * 16 + (lane & 15), cb = wn * 16 + (lane & 15), kq = lane >> 4;
+  static_assert(KT / (4 * KS_) == 4, "the fragment-read schedule below assumes 4 k4-steps");
+  int fa[4], fb[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int kk = h * (KT / KS_) + 4 * s + kq;
+    fa[s] = AK ? glds_at<true>(ra, kk) : glds_at<false>(kk, ra);
+    fb[s] = BK ? glds_at<true>(cb, kk) : glds_at<false>(kk, cb);
+  }
+  // LDS byte addresses of this lane's fragments in stage 0 (stage st: + st * 8 TD)
+  typedef __attribute__((address_space(3))) double lds_f64;
+  const unsigned la = (unsigned)(uintptr_t)((lds_f64*)sA), lb = (unsigned)(uintptr_t)((lds_f64*)sB);
+  unsigned xa[4], xb[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    xa[s] = la + 8u * (unsigned)fa[s];
+    xb[s] = lb + 8u * (unsigned)fb[s];
+  }
+  for (int it = 0; it < nt; ++it) {
+    const int last_issued = it + GS - 2 < nt - 1 ? it + GS - 2 : nt - 1;
+    vm_wait_tiles<GS>(last_issued - it);
+    __builtin_amdgcn_s_barrier();            // tile it is in LDS; stage (it - 1) % GS is free
+    if (it + GS - 1 < nt) issue(it + GS - 1);
+    // fragment reads as inline asm: the compiler would otherwise guard every
+    // ds_read behind vmcnt(0) (it cannot tell which LDS-DMA tile a read
+    // aliases), draining the tiles in flight; the waits below are explicit
+    const unsigned so = (unsigned)((it % GS) * TD * 8);
+    double a0, b0, a1, b1, a2, b2, a3, b3;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(a0) : "v"(xa[0] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(b0) : "v"(xb[0] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(a1) : "v"(xa[1] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(b1) : "v"(xb[1] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(a2) : "v"(xa[2] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(b2) : "v"(xb[2] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(a3) : "v"(xa[3] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(b3) : "v"(xb[3] + so));
+    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a0), "+v"(b0));
+    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a1), "+v"(b1));
+    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a2), "+v"(b2));
+    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc[2], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a3), "+v"(b3));
+    acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a3, b3, acc[3], 0, 0, 0);
+  }
+  __syncthreads();
+}
+
 // One BT x BT output tile (bx, by) of g (the whole block, NTH threads).  ntx =
 // tiles per row (partial-sum index).  sA / sB: the block's LDS operand buffers.
 // Ends with a barrier, so a caller may run further tiles on the same buffers.
 template <bool TA, bool TB, bool KS, bool DUAL>
 __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int ntx,
-                                          double (*sA)[BUF], double (*sB)[BUF]) {
+                                          double (*sA)[BUF], double (*sB)[BUF], double* lds) {
   // A is k-contiguous when not transposed; B is k-contiguous when transposed.
   constexpr bool AK = !TA, BK = TB;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int q = w & 3, h = w >> 2;           // output quadrant, k part of each tile
   const int wm = q >> 1, wn = q & 1;
   const int i0 = by * BT, j0 = bx * BT;
+  const int kq = lane >> 4;
+  // four independent accumulator chains (interleaved k4 steps): one dependent
+  // f64 MFMA chain per wave is latency-bound on gfx950
+  d4 acc[4], acc2[DUAL ? 4 : 1];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < (DUAL ? 4 : 1); ++c) acc2[c] = d4{0.0, 0.0, 0.0, 0.0};
+  bool done = false;
+  if constexpr (!KS && !DUAL) {
+    if (g.glds) {   // aligned shapes: LDS-DMA main loop (same k order, same bits)
+      mainloop_glds<TA, TB>(g, i0, j0, lds, acc);
+      done = true;
+    }
+  }
+  if (!done) {
   const int nt1 = (g.K + KT - 1) / KT;
   const int nt = DUAL ? 2 * nt1 : nt1;   // the second product's tiles follow the first's
   // tile `it` of the virtual k range: operands and k offset
@@ -281,14 +423,7 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
   ta0.store(sA[0], t);
   tb0.store(sB[0], t);
   __syncthreads();
-  // four independent accumulator chains (interleaved k4 steps): one dependent
-  // f64 MFMA chain per wave is latency-bound on gfx950
-  d4 acc[4], acc2[DUAL ? 4 : 1];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int c = 0; c < (DUAL ? 4 : 1); ++c) acc2[c] = d4{0.0, 0.0, 0.0, 0.0};
-  const int ra = wm * 16 + (lane & 15), cb = wn * 16 + (lane & 15), kq = lane >> 4;
+  const int ra = wm * 16 + (lane & 15), cb = wn * 16 + (lane & 15);
   const int kb = h * (KT / KS_);
   auto mma = [&](const double* a_s, const double* b_s, int it) {
     if (DUAL && it >= nt1) {
@@ -327,6 +462,7 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
       tb0.store(sB[0], t);
     }
     __syncthreads();
+  }
   }
   d4 r4 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   if constexpr (DUAL) {
@@ -391,8 +527,9 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
 template <bool TA, bool TB, bool KS, bool DUAL>
 __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   const GemmOp& g = gg.op[blockIdx.z];
-  __shared__ double sA[2][BUF];
-  __shared__ double sB[2][BUF];
+  __shared__ __attribute__((aligned(16))) double smem[SMEM];
+  double(*sA)[BUF] = reinterpret_cast<double(*)[BUF]>(smem);
+  double(*sB)[BUF] = reinterpret_cast<double(*)[BUF]>(smem + 2 * BUF);
   if (const int sk = gemm_skip(g, sB[1])) {
     // the copy decision uses this block's own test (sk == 2) or state written
     // by earlier launches (sk == 1), never a peer block's stores in this launch
@@ -412,10 +549,25 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
     }
     return;
   }
-  gemm_tile<TA, TB, KS, DUAL>(g, blockIdx.x, blockIdx.y, gridDim.x, sA, sB);
+  gemm_tile<TA, TB, KS, DUAL>(g, blockIdx.x, blockIdx.y, gridDim.x, sA, sB, smem);
 }
 
 }  // namespace gemm_detail
+
+// The LDS-DMA main loop needs whole 32 x 32 x 32 tiles and 16-byte aligned pairs.
+// (gemm_glds_enable: A/B switch for micro-benchmarks; both loops give the same bits)
+inline bool gemm_glds_enable = true;
+inline bool glds_ok(const GemmOp& o) {
+#ifdef VB_GEMM_NO_GLDS
+  (void)o;
+  return false;
+#else
+  if (!gemm_glds_enable) return false;
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return o.M % 32 == 0 && o.N % 32 == 0 && o.K % 32 == 0 && !o.kscale && !o.A2 &&
+         o.lda % 2 == 0 && o.ldb % 2 == 0 && al(o.A) && al(o.B);
+#endif
+}
 
 // Launch n (1 or 2) GEMMs of equal shape and transposes; dual products (A2/B2)
 // must not use kscale.
@@ -424,7 +576,11 @@ inline hipError_t gemm_group(const GemmOp* ops, int n, hipStream_t s) {
   const GemmOp& g = ops[0];
   if (g.M <= 0 || g.N <= 0 || n < 1 || n > 2) return n < 1 ? hipSuccess : hipErrorInvalidValue;
   GemmGroup gg{};
-  for (int i = 0; i < n; ++i) gg.op[i] = ops[i];
+  for (int i = 0; i < n; ++i) {
+    gg.op[i] = ops[i];
+    const GemmOp& o = ops[i];
+    gg.op[i].glds = glds_ok(o) ? 1 : 0;
+  }
   const dim3 grid((unsigned)((g.N + BT - 1) / BT), (unsigned)((g.M + BT - 1) / BT), (unsigned)n);
   const bool ks = g.kscale != nullptr, dual = g.A2 != nullptr;
   if (ks && dual) return hipErrorInvalidValue;
