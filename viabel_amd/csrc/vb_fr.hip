@@ -27,16 +27,13 @@
 // mean_and_cov / pth_moment, off the optimisation loop.
 #include "vb_device.hpp"
 #include "vb_internal.hpp"
-#include "vb_gemm_comb.hpp"
 
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
 #include <cmath>
-#include <cstdlib>
 #include <new>
-#include <string>
 
 namespace vbk {
 using namespace vbd;
@@ -678,10 +675,10 @@ struct FrWork {
   rocblas_handle blas = nullptr;
   int D = 0;
   // D x D
-  Buf L, E, T, GS, H, Sig, Yb[2], Zb[2], Eh, Xs, R, P, C1, C2, R2, P2;
+  Buf L, E, T, GS, H, Sig, Yb[2], Zb[2], Eh, Xs, R, P, C1, C2;
   // D
   Buf w, offd, scal, pv[4];
-  Buf info, sched, fro_part, tpart[2], pq_part, rz_part, rz_part2, rr_part, ee_part;
+  Buf info, sched, fro_part, tpart[2], pq_part, rz_part, rr_part, ee_part;
   FrSched* host_sched = nullptr;  // pinned copy of the schedule / status block
   const double* Yf = nullptr;     // final Newton-Schulz iterates (A^(1/2), A^(-1/2))
   const double* Zf = nullptr;
@@ -691,7 +688,6 @@ struct FrWork {
   bool zv_init = false;           // pv[2..3] hold a Z power vector
   bool last_warm = false;         // the last root was a warm one (iteration hints apply)
   const void* owner = nullptr;    // the run whose root the warm state above holds
-  bool pcg_classic = false;       // VIABEL_AMD_PCG=classic: the four-launch CG iteration
   int ns_kmax = 12, pcg_kmax = 14;  // iterations launched (device skips past convergence)
   int last_kmax = 12;             // Newton-Schulz iterations the last root launched
   bool eig_pending = false;       // a dsyevd ran since the last fr_info
@@ -709,14 +705,7 @@ struct FrWork {
   }
 };
 
-FrWork* fr_work_create() {
-  FrWork* w = new (std::nothrow) FrWork();
-  if (w) {
-    const char* e = std::getenv("VIABEL_AMD_PCG");
-    w->pcg_classic = e && std::string(e) == "classic";
-  }
-  return w;
-}
+FrWork* fr_work_create() { return new (std::nothrow) FrWork(); }
 void fr_work_destroy(FrWork* w) { delete w; }
 
 namespace {
@@ -739,16 +728,14 @@ int reserve_d(FrWork* W, int D, hipStream_t st) {
   if (W->D >= D) return 0;
   const size_t dd = sizeof(double) * (size_t)D * D;
   for (FrWork::Buf* b : {&W->L, &W->E, &W->T, &W->GS, &W->H, &W->Sig, &W->Yb[0], &W->Yb[1],
-                         &W->Zb[0], &W->Zb[1], &W->Eh, &W->Xs, &W->R, &W->P, &W->C1, &W->C2,
-                         &W->R2, &W->P2})
+                         &W->Zb[0], &W->Zb[1], &W->Eh, &W->Xs, &W->R, &W->P, &W->C1, &W->C2})
     FR_HIP(b->reserve(dd));
   for (FrWork::Buf* b : {&W->w, &W->offd, &W->pv[0], &W->pv[1], &W->pv[2], &W->pv[3]})
     FR_HIP(b->reserve(sizeof(double) * D));
   FR_HIP(W->scal.reserve(sizeof(double) * 8));
   FR_HIP(W->info.reserve(sizeof(int) * 4));
   const size_t nblk = (size_t)((D + 31) / 32) * ((D + 31) / 32);
-  for (FrWork::Buf* b : {&W->fro_part, &W->tpart[0], &W->tpart[1], &W->pq_part, &W->rz_part,
-                         &W->rz_part2})
+  for (FrWork::Buf* b : {&W->fro_part, &W->tpart[0], &W->tpart[1], &W->pq_part, &W->rz_part})
     FR_HIP(b->reserve(sizeof(double) * 4 * nblk));
   for (FrWork::Buf* b : {&W->rr_part, &W->ee_part}) FR_HIP(b->reserve(sizeof(double) * nblk));
   if (!W->sched.p) {
@@ -946,76 +933,12 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
 
 // Preconditioned conjugate gradients for autograd's sqrtm VJP (see pcg_* above):
 // X = the symmetric solution of S X + X S = G_S + G_S^T, into W->Xs.
-// D a multiple of 32: two launches per iteration, the vector updates folded into
-// the next GEMM's operand loads (vb_gemm_comb.hpp); otherwise four launches.
 int fr_pcg(FrWork* W, int D, hipStream_t st) {
   FrSched* sc = static_cast<FrSched*>(W->sched.p);
   const int nt = (D + kTile - 1) / kTile, nblk = nt * nt;
   const dim3 tg(nt, nt);
   hipLaunchKernelGGL(pcg_init_kernel, tg, dim3(256), 0, st, D, W->GS.d(), sc, W->Eh.d(),
                      W->R.d(), W->Xs.d(), W->ee_part.d());
-  // warm roots launch the learnt count (fr_info), others at least 16
-  const int kpcg = W->last_warm ? std::max(W->pcg_kmax, 6) : std::max(W->pcg_kmax, 16);
-  if (D % 32 == 0 && !W->pcg_classic) {
-    double* Rb[2] = {W->R.d(), W->R2.d()};
-    double* Pb[2] = {W->P.d(), W->P2.d()};
-    double* rzp[2] = {W->rz_part.d(), W->rz_part2.d()};
-    CombOp z{};
-    z.D = D;
-    z.mode = 0;
-    z.A = W->Zf;
-    z.B0 = Rb[0];
-    z.B1 = Rb[0];
-    z.C = W->C2.d();
-    z.dot_out = rzp[0];
-    z.done = &sc->pcg_done;
-    FR_HIP(gemm_comb(z, st));
-    for (int it = 0; it < kpcg; ++it) {
-      CombOp y{};
-      y.D = D;
-      y.mode = 2;
-      y.it = it;
-      y.A = W->Yf;
-      y.B0 = Pb[(it + 1) & 1];
-      y.B1 = W->C2.d();
-      y.Bout = Pb[it & 1];
-      y.C = W->C1.d();
-      y.rz_new = rzp[it & 1];
-      y.rz_old = rzp[(it + 1) & 1];
-      y.n_rz = 4 * nblk;
-      y.dot_out = W->pq_part.d();
-      y.done = &sc->pcg_done;
-      y.rr_in = W->rr_part.d();
-      y.n_rr = nblk;
-      y.ee_part = W->ee_part.d();
-      y.n_ee = nblk;
-      y.ee_out = &sc->ee;
-      y.tol2 = 1e-18;   // relative residual 1e-9 (as the four-launch iteration)
-      y.conv_iter_out = &sc->pcg_iter;
-      FR_HIP(gemm_comb(y, st));
-      CombOp r{};
-      r.D = D;
-      r.mode = 1;
-      r.it = it;
-      r.A = W->Zf;
-      r.B0 = Rb[it & 1];
-      r.B1 = W->C1.d();
-      r.Bout = Rb[(it + 1) & 1];
-      r.C = W->C2.d();
-      r.rz_new = rzp[it & 1];
-      r.n_rz = 4 * nblk;
-      r.pq = W->pq_part.d();
-      r.n_pq = 4 * nblk;
-      r.dot_out = rzp[(it + 1) & 1];
-      r.rr_out = W->rr_part.d();
-      r.X = W->Xs.d();
-      r.P = Pb[it & 1];
-      r.done = &sc->pcg_done;
-      FR_HIP(gemm_comb(r, st));
-    }
-    FR_HIP(hipGetLastError());
-    return 0;
-  }
   // P_0 = M^-1(R_0) from C2 = Z R_0, <R_0, Z R_0> in the epilogue
   auto zr = [&](int it) {
     GemmOp g = mm(D, D, D, W->Zf, false, W->R.d(), false, W->C2.d());
@@ -1036,6 +959,8 @@ int fr_pcg(FrWork* W, int D, hipStream_t st) {
   FR_HIP(gemm(zr(-1), st));
   hipLaunchKernelGGL(pcg_p_kernel, tg, dim3(256), 0, st, D, -1, W->C2.d(), W->rz_part.d(),
                      4 * nblk, W->ee_part.d(), nblk, sc, W->P.d());
+  // warm roots launch the learnt count (fr_info), others at least 16
+  const int kpcg = W->last_warm ? std::max(W->pcg_kmax, 6) : std::max(W->pcg_kmax, 16);
   for (int it = 0; it < kpcg; ++it) {
     GemmOp g = mm(D, D, D, W->Yf, false, W->P.d(), false, W->C1.d());
     g.dot_with = W->P.d();

@@ -264,45 +264,32 @@ __device__ __forceinline__ int gemm_skip(const GemmOp& g, double* red) {
 #ifndef VB_GEMM_GS
 #define VB_GEMM_GS 4
 #endif
-#ifndef VB_GEMM_GKT
-#define VB_GEMM_GKT 32
-#endif
-constexpr int GS = VB_GEMM_GS;   // LDS stages (tiles it+1 .. it+GS-1 in flight)
-constexpr int GKT = VB_GEMM_GKT; // k tile of the LDS-DMA loop
-constexpr int TD = BT * GKT;     // doubles per operand tile
-constexpr int GNI = TD / 128;    // 1-KB LDS-DMA instructions per operand tile
-static_assert(GNI % (NTH / 64) == 0, "LDS-DMA instructions must divide over the waves");
-constexpr int GPW = GNI / (NTH / 64);   // per wave per operand tile
-constexpr int GSTEPS = GKT / (4 * KS_); // k4-steps per wave per tile
-static_assert(GSTEPS % 4 == 0 && KS_ == 2 && KT == 32, "fragment schedule: groups of four k4-steps");
+constexpr int GS = VB_GEMM_GS; // LDS stages (tiles it+1 .. it+GS-1 in flight)
+constexpr int TD = BT * KT;    // doubles per operand tile
 constexpr int SMEM = (4 * BUF > 2 * GS * TD) ? 4 * BUF : 2 * GS * TD;  // doubles of LDS per block
 template <bool KROWS>
 __device__ __forceinline__ int swz(int r) { return KROWS ? 2 * (r & 15) : 16 * (r & 1); }
-template <bool KROWS>
-constexpr int row_len() { return KROWS ? GKT : BT; }
 
-// Global element offset (from the tile origin) that lane `lane` loads for its
-// 16-byte slot of LDS-DMA instruction u (LDS doubles [128 u, 128 u + 128)).
+// Global element offset (from the tile origin) that lane `lane` of wave `w`
+// loads for its 16-byte LDS slot; ld = leading dimension.
 template <bool KROWS>
-__device__ __forceinline__ long long glds_src(int u, int lane, long long ld) {
-  constexpr int RL = row_len<KROWS>();
-  const int e = 128 * u + 2 * lane;
-  const int r = e / RL, sl = e % RL;
-  return (long long)r * ld + (sl ^ swz<KROWS>(r));
+__device__ __forceinline__ long long glds_src(int w, int lane, long long ld) {
+  const int r = 4 * w + (lane >> 4);          // tile row
+  const int s = 2 * (lane & 15);              // LDS slot (doubles) within the row
+  return (long long)r * ld + (s ^ swz<KROWS>(r));
 }
 
-// LDS offset (doubles) of element (row r, column c) of a tile laid out with rows = r.
+// LDS offset (doubles) of fragment element (row r, column c) of a tile laid
+// out with `rows` = r.
 template <bool KROWS>
-__device__ __forceinline__ int glds_at(int r, int c) {
-  return r * row_len<KROWS>() + (c ^ swz<KROWS>(r));
-}
+__device__ __forceinline__ int glds_at(int r, int c) { return r * 32 + (c ^ swz<KROWS>(r)); }
 
-// each wave has 2 GPW LDS-DMA instructions per tile (A, B) in flight
+template <int STG>
 __device__ __forceinline__ void vm_wait_tiles(int pending) {
-  constexpr int P = 2 * GPW;
-  if (pending >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * P) : "memory");
-  else if (pending == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * P) : "memory");
-  else if (pending == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(P) : "memory");
+  // each wave has 2 LDS-DMA instructions per tile (A, B) in flight
+  if (pending >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (pending == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (pending == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -317,76 +304,69 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
   const int wm = q >> 1, wn = q & 1;
   double* sA = lds;                 // [GS][TD]
   double* sB = lds + GS * TD;       // [GS][TD]
-  const int nt = g.K / GKT;
-  // per-lane global sources: tile origin + fixed offset; the origin moves by GKT
+  const int nt = g.K / KT;
+  // per-lane global sources: tile origin + fixed offset; the origin moves by KT
   // along k each tile (k is the row index of the "rows = k" layouts)
   const double* a0 = g.A + (AK ? (long long)i0 * g.lda : (long long)i0);
   const double* b0 = g.B + (BK ? (long long)j0 * g.ldb : (long long)j0);
-  long long aoff[GPW], boff[GPW];
-#pragma unroll
-  for (int j = 0; j < GPW; ++j) {
-    aoff[j] = glds_src<AK>(w + (NTH / 64) * j, lane, g.lda);
-    boff[j] = glds_src<BK>(w + (NTH / 64) * j, lane, g.ldb);
-  }
-  const long long astep = AK ? GKT : (long long)GKT * g.lda;
-  const long long bstep = BK ? GKT : (long long)GKT * g.ldb;
+  const long long aoff = glds_src<AK>(w, lane, g.lda), boff = glds_src<BK>(w, lane, g.ldb);
+  const long long astep = AK ? KT : (long long)KT * g.lda;
+  const long long bstep = BK ? KT : (long long)KT * g.ldb;
   auto issue = [&](int it) {
     const int st = it % GS;
-#pragma unroll
-    for (int j = 0; j < GPW; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(a0 + it * astep + aoff[j]),
-                                       (void*)(sA + st * TD + 128 * (w + (NTH / 64) * j)), 16, 0, 0);
-#pragma unroll
-    for (int j = 0; j < GPW; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(b0 + it * bstep + boff[j]),
-                                       (void*)(sB + st * TD + 128 * (w + (NTH / 64) * j)), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(a0 + it * astep + aoff),
+                                     (void*)(sA + st * TD + 128 * w), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(b0 + it * bstep + boff),
+                                     (void*)(sB + st * TD + 128 * w), 16, 0, 0);
   };
 #pragma unroll
   for (int s = 0; s < GS - 1; ++s)
     if (s < nt) issue(s);
-  // LDS byte addresses of this lane's fragments in stage 0 (stage st: + 8 st TD)
+  // fragment offsets within a stage for the 4 k4-steps of this wave's k part
   const int ra = wm * 16 + (lane & 15), cb = wn * 16 + (lane & 15), kq = lane >> 4;
+  static_assert(KT / (4 * KS_) == 4, "the fragment-read schedule below assumes 4 k4-steps");
+  int fa[4], fb[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int kk = h * (KT / KS_) + 4 * s + kq;
+    fa[s] = AK ? glds_at<true>(ra, kk) : glds_at<false>(kk, ra);
+    fb[s] = BK ? glds_at<true>(cb, kk) : glds_at<false>(kk, cb);
+  }
+  // LDS byte addresses of this lane's fragments in stage 0 (stage st: + st * 8 TD)
   typedef __attribute__((address_space(3))) double lds_f64;
   const unsigned la = (unsigned)(uintptr_t)((lds_f64*)sA), lb = (unsigned)(uintptr_t)((lds_f64*)sB);
-  unsigned xa[GSTEPS], xb[GSTEPS];
+  unsigned xa[4], xb[4];
 #pragma unroll
-  for (int s = 0; s < GSTEPS; ++s) {
-    // each 32-deep half of a 64-deep tile is split over the k parts exactly as
-    // a 32-deep tile: the same k order (and bits) as the register-staged loop
-    const int kk = (s >> 2) * KT + h * (KT / KS_) + 4 * (s & 3) + kq;
-    xa[s] = la + 8u * (unsigned)(AK ? glds_at<true>(ra, kk) : glds_at<false>(kk, ra));
-    xb[s] = lb + 8u * (unsigned)(BK ? glds_at<true>(cb, kk) : glds_at<false>(kk, cb));
+  for (int s = 0; s < 4; ++s) {
+    xa[s] = la + 8u * (unsigned)fa[s];
+    xb[s] = lb + 8u * (unsigned)fb[s];
   }
   for (int it = 0; it < nt; ++it) {
     const int last_issued = it + GS - 2 < nt - 1 ? it + GS - 2 : nt - 1;
-    vm_wait_tiles(last_issued - it);
+    vm_wait_tiles<GS>(last_issued - it);
     __builtin_amdgcn_s_barrier();            // tile it is in LDS; stage (it - 1) % GS is free
     if (it + GS - 1 < nt) issue(it + GS - 1);
     // fragment reads as inline asm: the compiler would otherwise guard every
     // ds_read behind vmcnt(0) (it cannot tell which LDS-DMA tile a read
-    // aliases), draining the tiles in flight; the waits below are explicit and
-    // tie the values they release (same k order as the register-staged loop)
+    // aliases), draining the tiles in flight; the waits below are explicit
     const unsigned so = (unsigned)((it % GS) * TD * 8);
-#pragma unroll
-    for (int g4 = 0; g4 < GSTEPS; g4 += 4) {
-      double a0_, b0_, a1_, b1_, a2_, b2_, a3_, b3_;
-      asm volatile("ds_read_b64 %0, %1" : "=v"(a0_) : "v"(xa[g4] + so));
-      asm volatile("ds_read_b64 %0, %1" : "=v"(b0_) : "v"(xb[g4] + so));
-      asm volatile("ds_read_b64 %0, %1" : "=v"(a1_) : "v"(xa[g4 + 1] + so));
-      asm volatile("ds_read_b64 %0, %1" : "=v"(b1_) : "v"(xb[g4 + 1] + so));
-      asm volatile("ds_read_b64 %0, %1" : "=v"(a2_) : "v"(xa[g4 + 2] + so));
-      asm volatile("ds_read_b64 %0, %1" : "=v"(b2_) : "v"(xb[g4 + 2] + so));
-      asm volatile("ds_read_b64 %0, %1" : "=v"(a3_) : "v"(xa[g4 + 3] + so));
-      asm volatile("ds_read_b64 %0, %1" : "=v"(b3_) : "v"(xb[g4 + 3] + so));
-      asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a0_), "+v"(b0_));
-      acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0_, b0_, acc[0], 0, 0, 0);
-      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a1_), "+v"(b1_));
-      acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1_, b1_, acc[1], 0, 0, 0);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a2_), "+v"(b2_));
-      acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2_, b2_, acc[2], 0, 0, 0);
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a3_), "+v"(b3_));
-      acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a3_, b3_, acc[3], 0, 0, 0);
-    }
+    double a0, b0, a1, b1, a2, b2, a3, b3;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(a0) : "v"(xa[0] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(b0) : "v"(xb[0] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(a1) : "v"(xa[1] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(b1) : "v"(xb[1] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(a2) : "v"(xa[2] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(b2) : "v"(xb[2] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(a3) : "v"(xa[3] + so));
+    asm volatile("ds_read_b64 %0, %1" : "=v"(b3) : "v"(xb[3] + so));
+    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a0), "+v"(b0));
+    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a1), "+v"(b1));
+    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a2), "+v"(b2));
+    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc[2], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a3), "+v"(b3));
+    acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a3, b3, acc[3], 0, 0, 0);
   }
   __syncthreads();
 }
@@ -584,7 +564,7 @@ inline bool glds_ok(const GemmOp& o) {
 #else
   if (!gemm_glds_enable) return false;
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  return o.M % 32 == 0 && o.N % 32 == 0 && o.K % gemm_detail::GKT == 0 && !o.kscale && !o.A2 &&
+  return o.M % 32 == 0 && o.N % 32 == 0 && o.K % 32 == 0 && !o.kscale && !o.A2 &&
          o.lda % 2 == 0 && o.ldb % 2 == 0 && al(o.A) && al(o.B);
 #endif
 }
