@@ -906,12 +906,14 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
       g.conv_n = 4 * nblk;
       g.conv_scale_dev = &sc->inv_a4[k];
       g.conv_tol2 = 1e-20 * D;
-      // ||I - Z_k Y_k||_F <= 1e-5: the residual after this update is at most
-      // 0.75 ||E||_F ||E||_2 <= 7.5e-11 (e' = (3 e^2 + e^3) / 4 per eigenvalue),
-      // below the 1e-10 sqrt(D) bar, so this update is the last one (saves the
-      // detection-only T_{k+1} product; the root is the same iterate)
+      // ||I - Z_k Y_k||_F <= tau: the residual after this update is at most
+      // 0.75 ||E||_F ||E||_2 <= 0.75 tau^2 (e' = (3 e^2 + e^3) / 4 per
+      // eigenvalue), so with tau^2 = 0.67e-10 sqrt(D) (half the largest tau that
+      // keeps 0.75 tau^2 below the 1e-10 sqrt(D) bar) this update is the last
+      // one: the detection-only T_{k+1} product and the Y|Z launch after it are
+      // saved, and the root is the same iterate
       g.fin_flag = &sc->ns_fin;
-      g.conv_fin_tol2 = 1e-10;
+      g.conv_fin_tol2 = 0.67e-10 * std::sqrt((double)D);
       if (k >= 2) {
         g.conv_prev_part = W->tpart[(k - 1) & 1].d();
         g.conv_prev_scale_dev = &sc->inv_a4[k - 1];
