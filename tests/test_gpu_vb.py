@@ -436,3 +436,42 @@ def test_t_family_predraw_large_n_matches_oracle(objective):
                            eps_fn=eps_fn, learning_rate=0.01)
         np.testing.assert_allclose(vals[r], ores[2], rtol=1e-7, atol=1e-9)
         np.testing.assert_allclose(lam[r], ores[1][-1], rtol=1e-7, atol=1e-9)
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize('kind,df', [('gauss', None), ('t', 40.0)])
+@pytest.mark.parametrize('objective', ['klvi', 'chivi'])
+@pytest.mark.parametrize('D', [1, 2, 10, 16])
+def test_in_kernel_draws_at_layout_boundaries(kind, df, objective, D, monkeypatch):
+    """In-kernel Philox draws of the block kernel (VIABEL_AMD_PREDRAW=0, the t
+    family included: its instance faulted at N > 256 when its draw routine was
+    compiled out of line) across the draw-buffer layouts: N from the
+    overlapped draw/row layout through the chunked layout and several chunks,
+    for every DMAX instance; each N equals the pre-drawn path bit for bit and the
+    oracle fed with the C-oracle draws (1e-9)."""
+    import viabel_amd.vb as vbm
+    vb, targets, vo, ro = _mods()
+    tgt = targets.funnel(D) if D >= 2 else targets.isogauss(D)
+    tname = 'funnel' if D >= 2 else 'isogauss'
+    ofam = vo.Family(kind, D, df)
+    for N in (255, 256, 257, 300, 600):
+        fam = _family(vb, kind, df, D, 'philox')
+        obj = (vb.black_box_klvi(fam, tgt, N) if objective == 'klvi'
+               else vb.black_box_chivi(2.0, fam, tgt, N))
+        init = np.stack([_lam(D, 60 + q) for q in range(2)])
+        out = {}
+        for mode in ('0', 'all'):
+            monkeypatch.setenv('VIABEL_AMD_PREDRAW', mode)
+            run = vbm.DeviceRun(obj, 4, init, learning_rate=0.02)
+            run.advance_philox(4, 11, 9, 0)
+            out[mode] = run.result()
+        for a, b in zip(out['0'], out['all']):
+            np.testing.assert_array_equal(a, b, err_msg='N=%d' % N)
+        lam, _, vals, _ = out['0']
+        for r in range(2):
+            eps_fn = lambda i, r=r: ro.noise(11, 9 + r, i, N, D, kind, df or 0.0)
+            ores = _oracle_run(vo, ofam, objective, tname, 4, init[r], N, eps_fn=eps_fn,
+                               learning_rate=0.02)
+            np.testing.assert_allclose(vals[r], ores[2], rtol=1e-9, atol=1e-9, err_msg='N=%d' % N)
+            np.testing.assert_allclose(lam[r], ores[1][-1], rtol=1e-9, atol=1e-11,
+                                       err_msg='N=%d' % N)

@@ -189,9 +189,12 @@ int sync(vb_ctx* c) {
 // kPredrawBytes of draws and kPredrawMaxSteps steps.
 constexpr size_t kPredrawBytes = size_t(256) << 20;
 constexpr long long kPredrawMaxSteps = 512;
+// VIABEL_AMD_PREDRAW: unset / "t" -> the t family pre-draws (default), "all" ->
+// every family, "0" -> in-kernel draws for every family (same bits either way)
 bool predraw_enabled(int fam_kind) {
-  if (fam_kind == VB_FAMILY_MF_T) return true;
   const char* e = std::getenv("VIABEL_AMD_PREDRAW");
+  if (e && e[0] == '0') return false;
+  if (fam_kind == VB_FAMILY_MF_T) return true;
   return e && e[0] == 'a';
 }
 

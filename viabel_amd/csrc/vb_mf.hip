@@ -598,8 +598,15 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   const double lq_half = 0.5 * (a.df + 1.0);
   const double inv_df = 1.0 / a.df;
 
-  // one (sample, pair) draw item: e pair [+ log q partial of the pair, sans -log sigma]
-  auto draw_item = [&](int it0, int it_step, int n_items, int nbase, long long ri, double* buf) {
+  // one (sample, pair) draw item: e pair [+ log q partial of the pair, sans -log sigma].
+  // Always inlined: the t instances once kept it out of line, where `buf` (an LDS
+  // array) became a generic pointer and its two-double record stores were merged
+  // into flat 16-byte stores at 8-byte-aligned LDS addresses (odd record lengths:
+  // CHIVI's 3 NP, and the s_e base itself is only 8-byte aligned) -- the memory
+  // aperture violation of the in-kernel t sampler.  Inlined, the
+  // stores are ds_write_b64 / ds_write2_b64 on the LDS array.
+  auto draw_item = [&](int it0, int it_step, int n_items, int nbase, long long ri,
+                       double* buf) __attribute__((always_inline)) {
     for (int it = it0; it < n_items; it += it_step) {
       const int nl = it / NP, j = it - nl * NP;
       const uint32_t n = (uint32_t)(nbase + nl);
@@ -1458,9 +1465,8 @@ static hipError_t block_dispatch_dm(int fam, bool host, const BlockArgs& a, int 
   } else if (host) {
     hipLaunchKernelGGL((block_kernel<TGT, false, true, DM>), grid, block, 0, s, a);
   } else if (fam == 1) {
-    // the t family's Philox draws are pre-drawn (launch_block_predraw) and
-    // consumed through the device-noise path; no in-kernel t sampler instance
-    return hipErrorInvalidValue;
+    // (runs pre-draw the t family's Philox noise by default: launch_block_predraw)
+    hipLaunchKernelGGL((block_kernel<TGT, true, false, DM>), grid, block, 0, s, a);
   } else {
     hipLaunchKernelGGL((block_kernel<TGT, false, false, DM>), grid, block, 0, s, a);
   }
