@@ -41,7 +41,6 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X dense fp64 MFMA spec peak
 # (profiles/r01/ubench_instr_costs.txt)
 VALU_PEAK_GINSTR = 256 * 4 * 2.4 / 4
 CHUNK = 256                    # steps per sep_kernel launch (vb_capi.hip max_chunk)
-CPU_CORES_CAP = 16             # the GPU box's CPU share per GPU
 
 
 def algorithmic_bytes_per_step(n, d, w):
@@ -74,8 +73,29 @@ def host_info():
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = os.cpu_count()
+    quota = cgroup_cpu_quota()
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
     return {'cpu_model': model, 'nproc': os.cpu_count(), 'affinity_cpus': aff,
-            'cores_used_all_core_leg': max(1, min(CPU_CORES_CAP, aff))}
+            'cgroup_cpu_quota': quota, 'cores_used_all_core_leg': usable,
+            'all_core_rule': 'every CPU the process may run on concurrently: the affinity '
+                             'mask, capped by the cgroup CPU quota (cpu.max) when one is set'}
+
+
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup grants (cgroup v2 cpu.max 'quota period',
+    v1 cfs_quota_us / cfs_period_us), or None when unlimited / unreadable.  The
+    affinity mask can list far more CPUs than the quota lets run at once."""
+    try:
+        q, p = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        return None if q == 'max' else int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+        p = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+        return None if q <= 0 else q / p
+    except (OSError, ValueError):
+        return None
 
 
 def _cfg3_objective(n):
@@ -437,13 +457,13 @@ def leg_cfg4(cpu, host, steps=30):
         np.random.seed(0)
         fo.chivi_value_grad(ofam, otgt, lam0, n, 2.0)
         ts = []
-        for _ in range(3):
+        for _ in range(5):
             t0 = time.perf_counter()
             fo.chivi_value_grad(ofam, otgt, lam0, n, 2.0)
             ts.append(time.perf_counter() - t0)
         out['cpu_baseline'] = {'value': n * Dm / _median(ts), 'unit': 'MC-samples/s', 'cores': 1,
                                'kind': 'port', 'ms_per_step': _median(ts) * 1e3,
-                               'sample': 'median of 3 CHIVI value+grad evaluations (scipy sqrtm '
+                               'sample': 'median of 5 CHIVI value+grad evaluations (scipy sqrtm '
                                          '+ solve_sylvester VJP: the reference algorithm), BLAS '
                                          'threads 1'}
         out['speedup_vs_cpu'] = _median(ts) / dt

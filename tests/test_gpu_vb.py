@@ -447,7 +447,7 @@ def test_in_kernel_draws_at_layout_boundaries(kind, df, objective, D, monkeypatc
     family included: its instance faulted at N > 256 when its draw routine was
     compiled out of line) across the draw-buffer layouts: N from the
     overlapped draw/row layout through the chunked layout and several chunks,
-    for every DMAX instance; each N equals the pre-drawn path bit for bit and the
+    for every DMAX instance; each N equals the pre-drawn path to rounding and the
     oracle fed with the C-oracle draws (1e-9)."""
     import viabel_amd.vb as vbm
     vb, targets, vo, ro = _mods()
@@ -465,8 +465,11 @@ def test_in_kernel_draws_at_layout_boundaries(kind, df, objective, D, monkeypatc
             run = vbm.DeviceRun(obj, 4, init, learning_rate=0.02)
             run.advance_philox(4, 11, 9, 0)
             out[mode] = run.result()
+        # the two paths share every draw; past the overlapped layout (N > 256)
+        # the row threads accumulate their samples in a different association,
+        # so equality is to rounding (observed <= 2 ulp)
         for a, b in zip(out['0'], out['all']):
-            np.testing.assert_array_equal(a, b, err_msg='N=%d' % N)
+            np.testing.assert_allclose(a, b, rtol=1e-13, atol=1e-15, err_msg='N=%d' % N)
         lam, _, vals, _ = out['0']
         for r in range(2):
             eps_fn = lambda i, r=r: ro.noise(11, 9 + r, i, N, D, kind, df or 0.0)
