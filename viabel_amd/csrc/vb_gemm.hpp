@@ -91,7 +91,7 @@ struct GemmOp {
   // ns0_z = ns0[2] (3 I - ns0[3] Sigma), written for the same tile
   const double* ns0;
   double* ns0_z;
-  // set by gemm_group: M, N, K multiples of 32, 16-byte aligned operand rows, no
+  // set by gemm_group: M, N multiples of 32, K of KTG, 16-byte aligned operand rows, no
   // kscale / dual product -> the LDS-DMA main loop
   int glds;
 };
@@ -248,48 +248,68 @@ __device__ __forceinline__ int gemm_skip(const GemmOp& g, double* red) {
   return s_skip;
 }
 
-// ---- LDS-DMA main loop (M, N, K multiples of 32; no kscale / dual product) ----
+// ---- LDS-DMA main loop (M, N, K multiples of KTG; no kscale / dual product) ----
 // Operand tiles go global -> LDS directly (global_load_lds_dwordx4: no VGPR
 // staging, so no register of an in-flight load is ever reused and the loop
-// keeps GS - 1 tiles in flight across its barriers).  A tile is 32 "rows" of 32
-// doubles, a row = the operand's contiguous global dimension: one wave
-// instruction moves 1 KB = 4 rows, each lane 16 B (a pair of doubles).  The LDS
-// destination of a lane is fixed (wave base + 16 lane), so the bank swizzle is
-// applied to the GLOBAL address: LDS slot s of row r holds element s ^ sw(r)
-// (pairs stay pairs: sw even).
+// keeps GS - 1 tiles in flight across its barriers).  A stage holds KTG (64) k
+// of both operands: a tile is "rows" of the operand's contiguous global
+// dimension (RL doubles each: KTG for k-contiguous operands, BT for
+// row-contiguous ones); one wave instruction moves 1 KB, each lane 16 B (a pair
+// of doubles), and each wave issues KTG / 32 instructions per operand and
+// stage.  The LDS destination of a lane is fixed (instruction base + 16 lane),
+// so the bank swizzle is applied to the GLOBAL address: LDS slot s of row r
+// holds element s ^ sw(r) (pairs stay pairs: sw even).
 //   rows = m / n, k contiguous (A, or B^T):  sw(r) = 2 (r & 15)  -- a fragment
-//     read (16 rows x 2 k per 32 lanes) then covers 64 distinct banks;
+//     read (16 rows x 2 k per 32 lanes) then covers 64 distinct banks (row
+//     stride KTG doubles = 0 mod 64 banks);
 //   rows = k, m / n contiguous (A^T, or B): sw(r) = 16 (r & 1)   -- rows k, k+1
 //     land in opposite bank halves.
+// Within a stage, wave (quadrant q, k part h) consumes k = 32 u + 16 h + 4 s + kq
+// (sub-tile u, step s) into accumulator chain s: the k order of every chain is
+// that of the register-staged loop (KT = 32), so both loops give the same bits.
+// (Sweep over k depth x stages, profiles/r03/gemm_glds_sweep.log: 64 x 2 is the
+// fastest, 10.5 us per cold 512^3 product against 11.2 for 32 x 4.)
 #ifndef VB_GEMM_GS
-#define VB_GEMM_GS 4
+#define VB_GEMM_GS 2
 #endif
-constexpr int GS = VB_GEMM_GS; // LDS stages (tiles it+1 .. it+GS-1 in flight)
-constexpr int TD = BT * KT;    // doubles per operand tile
+#ifndef VB_GEMM_KTG
+#define VB_GEMM_KTG 64
+#endif
+constexpr int GS = VB_GEMM_GS;   // LDS stages (tiles it+1 .. it+GS-1 in flight)
+constexpr int KTG = VB_GEMM_KTG; // k per stage
+static_assert(KTG % 32 == 0 && KT == 32 && KS_ == 2, "LDS-DMA loop: 32-deep sub-tiles, 2 k parts");
+constexpr int NSUB = KTG / 32;   // 32-deep sub-tiles per stage
+constexpr int TD = BT * KTG;     // doubles per operand tile
 constexpr int SMEM = (4 * BUF > 2 * GS * TD) ? 4 * BUF : 2 * GS * TD;  // doubles of LDS per block
+static_assert(SMEM * 8 <= 65536, "static LDS of one block");
 template <bool KROWS>
 __device__ __forceinline__ int swz(int r) { return KROWS ? 2 * (r & 15) : 16 * (r & 1); }
+template <bool KROWS>
+constexpr int row_len() { return KROWS ? KTG : BT; }
 
 // Global element offset (from the tile origin) that lane `lane` of wave `w`
-// loads for its 16-byte LDS slot; ld = leading dimension.
+// loads for its 16-byte LDS slot in instruction j; ld = leading dimension.
 template <bool KROWS>
-__device__ __forceinline__ long long glds_src(int w, int lane, long long ld) {
-  const int r = 4 * w + (lane >> 4);          // tile row
-  const int s = 2 * (lane & 15);              // LDS slot (doubles) within the row
+__device__ __forceinline__ long long glds_src(int j, int w, int lane, long long ld) {
+  constexpr int RL = row_len<KROWS>();
+  const int o = (j * 8 + w) * 128 + 2 * lane;   // LDS double offset within the tile
+  const int r = o / RL, s = o % RL;
   return (long long)r * ld + (s ^ swz<KROWS>(r));
 }
 
 // LDS offset (doubles) of fragment element (row r, column c) of a tile laid
 // out with `rows` = r.
 template <bool KROWS>
-__device__ __forceinline__ int glds_at(int r, int c) { return r * 32 + (c ^ swz<KROWS>(r)); }
+__device__ __forceinline__ int glds_at(int r, int c) {
+  return r * row_len<KROWS>() + (c ^ swz<KROWS>(r));
+}
 
-template <int STG>
+// each wave has 2 NSUB LDS-DMA instructions per tile (A, B) in flight
 __device__ __forceinline__ void vm_wait_tiles(int pending) {
-  // each wave has 2 LDS-DMA instructions per tile (A, B) in flight
-  if (pending >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (pending == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (pending == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  static_assert(GS <= 4 && 2 * NSUB * 3 <= 63, "vmcnt range");
+  if (pending >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * NSUB) : "memory");
+  else if (pending == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NSUB) : "memory");
+  else if (pending == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NSUB) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -304,69 +324,75 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
   const int wm = q >> 1, wn = q & 1;
   double* sA = lds;                 // [GS][TD]
   double* sB = lds + GS * TD;       // [GS][TD]
-  const int nt = g.K / KT;
-  // per-lane global sources: tile origin + fixed offset; the origin moves by KT
+  const int nt = g.K / KTG;
+  // per-lane global sources: tile origin + fixed offsets; the origin moves by KTG
   // along k each tile (k is the row index of the "rows = k" layouts)
   const double* a0 = g.A + (AK ? (long long)i0 * g.lda : (long long)i0);
   const double* b0 = g.B + (BK ? (long long)j0 * g.ldb : (long long)j0);
-  const long long aoff = glds_src<AK>(w, lane, g.lda), boff = glds_src<BK>(w, lane, g.ldb);
-  const long long astep = AK ? KT : (long long)KT * g.lda;
-  const long long bstep = BK ? KT : (long long)KT * g.ldb;
+  long long aoff[NSUB], boff[NSUB];
+#pragma unroll
+  for (int j = 0; j < NSUB; ++j) {
+    aoff[j] = glds_src<AK>(j, w, lane, g.lda);
+    boff[j] = glds_src<BK>(j, w, lane, g.ldb);
+  }
+  const long long astep = AK ? KTG : (long long)KTG * g.lda;
+  const long long bstep = BK ? KTG : (long long)KTG * g.ldb;
   auto issue = [&](int it) {
     const int st = it % GS;
-    __builtin_amdgcn_global_load_lds((const void*)(a0 + it * astep + aoff),
-                                     (void*)(sA + st * TD + 128 * w), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(b0 + it * bstep + boff),
-                                     (void*)(sB + st * TD + 128 * w), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) {
+      __builtin_amdgcn_global_load_lds((const void*)(a0 + it * astep + aoff[j]),
+                                       (void*)(sA + st * TD + 128 * (j * 8 + w)), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(b0 + it * bstep + boff[j]),
+                                       (void*)(sB + st * TD + 128 * (j * 8 + w)), 16, 0, 0);
+    }
   };
 #pragma unroll
   for (int s = 0; s < GS - 1; ++s)
     if (s < nt) issue(s);
-  // fragment offsets within a stage for the 4 k4-steps of this wave's k part
+  // fragment offsets within a stage for this wave's 4 NSUB k4-steps (sub-tile u,
+  // step s: k = 32 u + 16 h + 4 s + kq)
   const int ra = wm * 16 + (lane & 15), cb = wn * 16 + (lane & 15), kq = lane >> 4;
-  static_assert(KT / (4 * KS_) == 4, "the fragment-read schedule below assumes 4 k4-steps");
-  int fa[4], fb[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int kk = h * (KT / KS_) + 4 * s + kq;
-    fa[s] = AK ? glds_at<true>(ra, kk) : glds_at<false>(kk, ra);
-    fb[s] = BK ? glds_at<true>(cb, kk) : glds_at<false>(kk, cb);
-  }
-  // LDS byte addresses of this lane's fragments in stage 0 (stage st: + st * 8 TD)
+  constexpr int NST = 4 * NSUB;
   typedef __attribute__((address_space(3))) double lds_f64;
   const unsigned la = (unsigned)(uintptr_t)((lds_f64*)sA), lb = (unsigned)(uintptr_t)((lds_f64*)sB);
-  unsigned xa[4], xb[4];
+  unsigned xa[NST], xb[NST];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    xa[s] = la + 8u * (unsigned)fa[s];
-    xb[s] = lb + 8u * (unsigned)fb[s];
+  for (int f = 0; f < NST; ++f) {
+    const int kk = 32 * (f >> 2) + 16 * h + 4 * (f & 3) + kq;
+    xa[f] = la + 8u * (unsigned)(AK ? glds_at<true>(ra, kk) : glds_at<false>(kk, ra));
+    xb[f] = lb + 8u * (unsigned)(BK ? glds_at<true>(cb, kk) : glds_at<false>(kk, cb));
   }
   for (int it = 0; it < nt; ++it) {
     const int last_issued = it + GS - 2 < nt - 1 ? it + GS - 2 : nt - 1;
-    vm_wait_tiles<GS>(last_issued - it);
+    vm_wait_tiles(last_issued - it);
     __builtin_amdgcn_s_barrier();            // tile it is in LDS; stage (it - 1) % GS is free
     if (it + GS - 1 < nt) issue(it + GS - 1);
     // fragment reads as inline asm: the compiler would otherwise guard every
     // ds_read behind vmcnt(0) (it cannot tell which LDS-DMA tile a read
-    // aliases), draining the tiles in flight; the waits below are explicit
+    // aliases), draining the tiles in flight; the waits below are explicit.
+    // Four steps' reads (8) stay in flight: step f + 4 is issued after step f's
+    // MFMA, into its own registers (lgkmcnt counts LDS reads in order)
     const unsigned so = (unsigned)((it % GS) * TD * 8);
-    double a0, b0, a1, b1, a2, b2, a3, b3;
-    asm volatile("ds_read_b64 %0, %1" : "=v"(a0) : "v"(xa[0] + so));
-    asm volatile("ds_read_b64 %0, %1" : "=v"(b0) : "v"(xb[0] + so));
-    asm volatile("ds_read_b64 %0, %1" : "=v"(a1) : "v"(xa[1] + so));
-    asm volatile("ds_read_b64 %0, %1" : "=v"(b1) : "v"(xb[1] + so));
-    asm volatile("ds_read_b64 %0, %1" : "=v"(a2) : "v"(xa[2] + so));
-    asm volatile("ds_read_b64 %0, %1" : "=v"(b2) : "v"(xb[2] + so));
-    asm volatile("ds_read_b64 %0, %1" : "=v"(a3) : "v"(xa[3] + so));
-    asm volatile("ds_read_b64 %0, %1" : "=v"(b3) : "v"(xb[3] + so));
-    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a0), "+v"(b0));
-    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0], 0, 0, 0);
-    asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a1), "+v"(b1));
-    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1], 0, 0, 0);
-    asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a2), "+v"(b2));
-    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc[2], 0, 0, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a3), "+v"(b3));
-    acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(a3, b3, acc[3], 0, 0, 0);
+    double fa[NST], fb[NST];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      asm volatile("ds_read_b64 %0, %1" : "=v"(fa[f]) : "v"(xa[f] + so));
+      asm volatile("ds_read_b64 %0, %1" : "=v"(fb[f]) : "v"(xb[f] + so));
+    }
+#pragma unroll
+    for (int f = 0; f < NST; ++f) {
+      const int ahead = (NST - 1 - f) < 3 ? (NST - 1 - f) : 3;   // steps issued after f
+      if (ahead == 3) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(fa[f]), "+v"(fb[f]));
+      else if (ahead == 2) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(fa[f]), "+v"(fb[f]));
+      else if (ahead == 1) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(fa[f]), "+v"(fb[f]));
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[f]), "+v"(fb[f]));
+      acc[f & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[f], fb[f], acc[f & 3], 0, 0, 0);
+      if (f + 4 < NST) {
+        asm volatile("ds_read_b64 %0, %1" : "=v"(fa[f + 4]) : "v"(xa[f + 4] + so));
+        asm volatile("ds_read_b64 %0, %1" : "=v"(fb[f + 4]) : "v"(xb[f + 4] + so));
+      }
+    }
   }
   __syncthreads();
 }
@@ -554,7 +580,7 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
 
 }  // namespace gemm_detail
 
-// The LDS-DMA main loop needs whole 32 x 32 x 32 tiles and 16-byte aligned pairs.
+// The LDS-DMA main loop needs whole 32 x 32 x KTG tiles and 16-byte aligned pairs.
 // (gemm_glds_enable: A/B switch for micro-benchmarks; both loops give the same bits)
 inline bool gemm_glds_enable = true;
 inline bool glds_ok(const GemmOp& o) {
@@ -564,7 +590,7 @@ inline bool glds_ok(const GemmOp& o) {
 #else
   if (!gemm_glds_enable) return false;
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  return o.M % 32 == 0 && o.N % 32 == 0 && o.K % 32 == 0 && !o.kscale && !o.A2 &&
+  return o.M % 32 == 0 && o.N % 32 == 0 && o.K % gemm_detail::KTG == 0 && !o.kscale && !o.A2 &&
          o.lda % 2 == 0 && o.ldb % 2 == 0 && al(o.A) && al(o.B);
 #endif
 }
