@@ -217,3 +217,50 @@ def test_errors():
     ft = vb.t_variational_family(4, 3.5)
     with pytest.raises(ValueError, match='df must be greater than p'):
         ft.pth_moment(4, np.zeros(ft.var_param_dim))
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize('objective', ['klvi', 'chivi', 'klvi_pd'])
+@pytest.mark.parametrize('target,D', [('corr_gauss', 40), ('corr_gauss', 64), ('funnel', 33)])
+def test_fused_philox_steps_across_advances(objective, target, D):
+    """The fused full-rank step (Philox draws, adagrad in the last kernel, which
+    prepares the next step's L, draws and Z power step; vb_fr.hip fr_value_grad):
+    advances of 7, 1 and 5 steps -- ready steps, the first (unprepared) step of
+    each advance, a one-step advance, a foreign root in between (log weights at
+    another lambda clears the prepared state) -- against the oracle's adagrad on
+    the C oracle's draws, step by step."""
+    vb, targets, fo, ro, vo = _mods()
+    N, n_iters = 24, 13
+    lam0 = _lam(D, 7)
+    fam = vb.t_variational_family(D, 30.0, rng='philox')
+    tgt = _target(targets, target, D)
+    if objective == 'klvi':
+        obj = vb.black_box_klvi(fam, tgt, N)
+    elif objective == 'chivi':
+        obj = vb.black_box_chivi(2.0, fam, tgt, N)
+    else:
+        obj = vb.black_box_klvi_pd(fam, tgt, N)
+    run = vb.DeviceRun(obj, n_iters, lam0, learning_rate=0.02)
+    run.advance_philox(7, 3, 5, 0)
+    run.advance_philox(1, 3, 5, 7)
+    from viabel_amd import experiments
+    experiments.log_weights(tgt, fam, _lam(D, 8), 64)          # another root on the workspace
+    run.advance_philox(5, 3, 5, 8)
+    lam, hist, vals, _ = run.result()
+
+    ofam = fo.FullRankT(D, 30.0)
+    otgt = fo.target_fn(target, D)
+    step = [0]
+
+    def f(l):
+        draws = ro.fr_noise(3, 5, step[0], N, D, 30.0)
+        step[0] += 1
+        if objective == 'klvi':
+            return fo.klvi_value_grad(ofam, otgt, l, N, draws=draws)
+        if objective == 'chivi':
+            return fo.chivi_value_grad(ofam, otgt, l, N, 2.0, draws=draws)
+        return fo.klvi_pd_value_grad(ofam, otgt, l, N, draws=draws)
+    osm, ohist, ovals, _ = vo.adagrad_optimize(n_iters, f, lam0, learning_rate=0.02)
+    _close(vals[0], ovals, 1e-7)
+    _close(hist[0], ohist, 1e-7)
+    _close(lam[0], ohist[-1], 1e-7)

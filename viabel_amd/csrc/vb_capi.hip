@@ -198,6 +198,14 @@ bool predraw_enabled(int fam_kind) {
   return e && e[0] == 'a';
 }
 
+// VIABEL_AMD_FR_FUSE=0: the full-rank step keeps its separate unpack / power /
+// draw / rows / colsum / pack / adagrad launches (A/B switch; same results to
+// rounding)
+bool fr_fuse_enabled() {
+  const char* e = std::getenv("VIABEL_AMD_FR_FUSE");
+  return !(e && e[0] == '0');
+}
+
 int check_ctx(vb_ctx* c) {
   if (!c) return fail(VB_EINVAL, "null vb_ctx");
   VB_HIP(hipSetDevice(c->device));
@@ -895,15 +903,23 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
         double* lam = r->lam.d() + q * P;
         const double* eps =
             host ? noise_base + ((size_t)q * n_steps + off) * per_step : nullptr;
-        if (r->fr)
+        double* hrow = step >= r->hist_start
+                           ? r->hist.d() + (q * r->n_hist + (step - r->hist_start)) * P
+                           : nullptr;
+        if (r->fr) {
+          // one problem with Philox draws: the adagrad step rides in the step's last
+          // kernel, which also prepares the next step of this advance (vb_fr.hip)
+          const bool fuse = r->nprob == 1 && !host && r->opt == VB_OPT_ADAGRAD && fr_fuse_enabled();
+          const vbk::MfUpdate up{r->ring.d() + q * P * r->W, r->W, step, lr, r->eps, hrow};
+          const vbk::FrNext nx{off + 1 < n_steps, (uint32_t)(noise->step + off + 1)};
           VB_TRY(vbk::fr_value_grad(W, r->spec, lam, eps, k0, k1,
                                     noise->stream + (uint32_t)q * stride,
                                     (uint32_t)(noise->step + off),
                                     r->values.d() + q * r->n_iters + step, r->grad.d(), c->stream,
-                                    r->nprob == 1 && step > 0, r));
-        double* hrow = step >= r->hist_start
-                           ? r->hist.d() + (q * r->n_hist + (step - r->hist_start)) * P
-                           : nullptr;
+                                    r->nprob == 1 && step > 0, r, fuse ? &up : nullptr,
+                                    fuse ? &nx : nullptr));
+          if (fuse) continue;
+        }
         if (!r->fr && r->opt == VB_OPT_ADAGRAD) {
           // gradient pass applies the adagrad step and writes the history row
           const vbk::MfUpdate up{r->ring.d() + q * P * r->W, r->W, step, lr, r->eps, hrow};

@@ -129,6 +129,39 @@ __global__ __launch_bounds__(256) void fr_noise_kernel(int D, long long n, Rng r
   if (2 * j + 1 < D) z[r * D + 2 * j + 1] = z1;
 }
 
+// The same draws as fr_noise_kernel, one 256-thread block per row n, which also
+// reduces zz[n] = sum_d z_nd^2 (the Mahalanobis invariant of log q): the fused
+// step needs no separate row pass over z.
+__device__ void fr_noise_row(int D, long long r, const Rng& rng, uint32_t step, double df, double* z,
+                             double* s, double* zz, double* red) {
+  const int np = (D + 1) / 2;
+  double a = 0.0;
+  for (int j = threadIdx.x; j <= np; j += blockDim.x) {
+    if (j == np) {
+      double ga, gb;
+      gamma_pair(rng, 0xFFFFFFFFu, (uint32_t)r, step, 0.5 * df, ga, gb);
+      s[r] = sqrt(2.0 * ga / df);
+      continue;
+    }
+    double z0, z1;
+    normal_pair(rng.draw((uint32_t)j, (uint32_t)r, step, 0u), z0, z1);
+    z[r * D + 2 * j] = z0;
+    a = fma(z0, z0, a);
+    if (2 * j + 1 < D) {
+      z[r * D + 2 * j + 1] = z1;
+      a = fma(z1, z1, a);
+    }
+  }
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) zz[r] = a;
+}
+
+__global__ __launch_bounds__(256) void fr_noise_rows_kernel(int D, Rng rng, uint32_t step, double df,
+                                                            double* z, double* s, double* zz) {
+  __shared__ double red[16];
+  fr_noise_row(D, blockIdx.x, rng, step, df, z, s, zz, red);
+}
+
 // One wave per row: zz[n] = sum_d z^2 (maha = zz / s^2), and for corr_gauss
 // logp[n] = 0.5 sum_d x G + const (G = -P x).
 __global__ __launch_bounds__(256) void fr_rows_kernel(int D, long long n, const double* z,
@@ -158,13 +191,24 @@ __global__ __launch_bounds__(256) void fr_rows_kernel(int D, long long n, const 
 // KLVI (vb.py:236-245):  value = -(entropy + mean logp), r_n = -1/N.
 // CHIVI (vb.py:248-266): lw = logp - logq, w = exp(lw - max)^alpha,
 //   value = log(mean w)/alpha + max, r_n = alpha w_n / N.
+// lp_part (fused step, corr_gauss): logp[n] = 0.5 sum_t lp_part[t][n] + lp_const
+// from the target GEMM's per-row partials of x . G (n_lp parts), written here.
 __global__ __launch_bounds__(1024) void fr_weights_kernel(int N, int D, int chivi, int pd,
                                                           double alpha,
                                                           double df, double t_const,
-                                                          const double* logp, const double* zz,
+                                                          double* logp, const double* zz,
                                                           const double* s, double* scal,
-                                                          double* r, double* rk, double* value) {
+                                                          double* r, double* rk, double* value,
+                                                          const double* lp_part = nullptr,
+                                                          int n_lp = 0, double lp_const = 0.0) {
   __shared__ double red[16];
+  if (lp_part) {
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+      double a = 0.0;
+      for (int t = 0; t < n_lp; ++t) a += lp_part[(long long)t * N + k];
+      logp[k] = 0.5 * a + lp_const;
+    }
+  }
   const double hld = scal[0];
   const double e = 0.5 * (df + D);
   if (!chivi) {
@@ -420,17 +464,34 @@ __device__ double ns_alpha(double l) { return sqrt(3.0 / (1.0 + l + l * l)); }
 
 // One block: c, l_0 and the whole schedule; resets the per-step flags.
 // Also scal[0] = 0.5 log det Sigma = sum_i log L_ii, the free log-diagonal of lam.
+// Power vectors: y = Sigma x (x the previous unit vector; in a fused step the
+// Sigma GEMM's per-row partials ypart [nyp][D], summed here and saved to ysave),
+// v = Z_prev u.  Every sched also stores the unit vectors uS = y / ||y||,
+// uZ = v / ||v|| that the next fused step multiplies by.
 __global__ __launch_bounds__(256) void fr_sched_kernel(int D, int kmax, const double* fro_part,
                                                        int n_part, const double* y,
                                                        const double* v, int has_z,
                                                        double l_default, FrSched* sc,
-                                                       const double* lam, double* scal) {
+                                                       const double* lam, double* scal,
+                                                       const double* ypart, int nyp, double* ysave,
+                                                       double* vsave, double* uS, double* uZ) {
   __shared__ double red[16];
   double f = 0.0, ly = 0.0, lv = 0.0, ld = 0.0;
   for (int i = threadIdx.x; i < n_part; i += 256) f += fro_part[i];
   for (int i = threadIdx.x; i < D; i += 256) {
-    ly += y[i] * y[i];
-    if (has_z) lv += v[i] * v[i];
+    double yi;
+    if (ypart) {
+      yi = 0.0;
+      for (int t = 0; t < nyp; ++t) yi += ypart[(long long)t * D + i];
+      ysave[i] = yi;
+    } else {
+      yi = y[i];
+    }
+    ly += yi * yi;
+    if (has_z) {
+      lv += v[i] * v[i];
+      if (vsave) vsave[i] = v[i];
+    }
     ld += lam[D + (long long)i * (i + 1) / 2 + i];
   }
   f = block_sum(f, red);
@@ -440,6 +501,13 @@ __global__ __launch_bounds__(256) void fr_sched_kernel(int D, int kmax, const do
   lv = block_sum(lv, red);
   __syncthreads();
   ld = block_sum(ld, red);
+  {
+    const double iy = ly > 0.0 ? 1.0 / sqrt(ly) : 0.0, iv = lv > 0.0 ? 1.0 / sqrt(lv) : 0.0;
+    for (int i = threadIdx.x; i < D; i += 256) {
+      uS[i] = (ypart ? ysave[i] : y[i]) * iy;
+      if (has_z && lv > 0.0) uZ[i] = v[i] * iv;
+    }
+  }
   if (threadIdx.x != 0) return;
   scal[0] = ld;
   const double lmax = sqrt(ly);                  // ||Sigma x|| for unit x <= lambda_max
@@ -479,6 +547,98 @@ __global__ __launch_bounds__(256) void fr_sched_kernel(int D, int kmax, const do
   sc->pcg_iter = -1;
 }
 
+// The fused step's last kernel (adagrad runs, Philox draws): the packed gradient
+// of fr_pack_kernel goes straight into the windowed adagrad step (adagrad_step,
+// as adagrad_update_kernel) and L of the new parameters is written for the next
+// step's Sigma GEMM (no unpack); extra blocks prepare the next step: its draws
+// (fr_noise_row, with zz) and one power step v = Z u on this step's root.
+// Blocks [0, npb): parameters (mu first, then the packed lower triangle),
+// [npb, npb + nrows): draw rows, then Z rows (8 per block).
+struct FrPackArgs {
+  int D, npb, nrows, nzb;
+  const double* GL;
+  double* L;
+  const double* scal;
+  FrSched* sc;
+  const double* rr_part;
+  int n_rr;
+  const double* gmu;   // mean gradient (pcg_init's colsum blocks)
+  double* lam;
+  double* ring;
+  int W;
+  long long step;
+  double lr, eps;
+  double* hrow;
+  // next step
+  Rng rng;
+  uint32_t next_step;
+  double df;
+  double *z, *s, *zz;
+  const double* Zf;
+  const double* uZ;
+  double* pz;
+};
+
+__global__ __launch_bounds__(256) void fr_pack_update_kernel(FrPackArgs a) {
+  __shared__ double red[16];
+  const int D = a.D;
+  const int b = blockIdx.x;
+  if (b >= a.npb) {
+    const int k = b - a.npb;
+    if (k < a.nrows) {
+      fr_noise_row(D, k, a.rng, a.next_step, a.df, a.z, a.s, a.zz, red);
+      return;
+    }
+    // v = Z u: two rows per wave
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int rr = 0; rr < 2; ++rr) {
+      const int row = (k - a.nrows) * 8 + wv * 2 + rr;
+      if (row >= D) break;
+      double t = 0.0;
+      for (int j = lane; j < D; j += 64) t = fma(a.Zf[(long long)row * D + j], a.uZ[j], t);
+      t = wave_sum(t);
+      if (lane == 0) a.pz[row] = t;
+    }
+    return;
+  }
+  const long long p = (long long)b * 256 + threadIdx.x;
+  if (p == 0) {
+    FrSched* sc = a.sc;
+    if (!sc->ns_conv && !sc->ns_fin) sc->status |= 1;
+    if (!sc->pcg_done) {
+      double rr = 0.0;
+      for (int k = 0; k < a.n_rr; ++k) rr += a.rr_part[k];
+      if (!(rr <= 1e-14 * sc->ee)) sc->status |= 2;  // relative residual above 1e-7
+    }
+    if (sc->warm_step) {
+      sc->hint_ns = max(sc->hint_ns, sc->ns_iter);
+      sc->hint_pcg = max(sc->hint_pcg, sc->pcg_iter);
+    }
+  }
+  const long long P = D + (long long)D * (D + 1) / 2;
+  if (p >= P) return;
+  double g;
+  long long li = -1;
+  bool diag = false;
+  if (p < D) {
+    g = a.gmu[p];
+  } else {
+    const long long k = p - D;
+    long long i = (long long)((sqrt(8.0 * (double)k + 1.0) - 1.0) * 0.5);
+    while ((i + 1) * (i + 2) / 2 <= k) ++i;
+    while (i * (i + 1) / 2 > k) --i;
+    const long long j = k - i * (i + 1) / 2;
+    li = i * D + j;
+    diag = i == j;
+    g = a.GL[li];
+    if (diag) g = fma(g, a.L[li], 2.0 * a.scal[1]);
+  }
+  const double v = adagrad_step(p, P, a.lam[p], g, a.ring, a.W, a.step, a.lr, a.eps, nullptr);
+  a.lam[p] = v;
+  if (a.hrow) a.hrow[p] = v;
+  if (li >= 0) a.L[li] = diag ? exp(v) : v;
+}
+
 // ---- PCG for the sqrtm VJP ----------------------------------------------------
 // autograd's sqrtm VJP solves S X + X S = G_S (solve_sylvester); Sigma = L L^T
 // needs only the symmetric part: S X + X S = E, E = G_S + G_S^T.  In the scaled
@@ -514,12 +674,37 @@ __device__ double sum_parts(const double* p, int n, double* red) {
   return block_sum(a, red);
 }
 
-// Eh = (G + G^T) / sqrt(c), R = Eh, X = 0, ee partials
+// gmu[j] = sum_n r_n Gm[n][j] by one 256-thread block per 64 columns (the
+// fused step's mean gradient, run as extra blocks of pcg_init_kernel): 4 waves
+// take every 4th row, combined in a fixed order
+__device__ void colsum_block(int N, int D, int cb, const double* r, const double* Gm, double* gmu) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int j = cb * 64 + lane;
+  double a = 0.0;
+  if (j < D) {
+#pragma unroll 8
+    for (int n = wv; n < N; n += 4) a = fma(r[n], Gm[(long long)n * D + j], a);
+  }
+  part[wv][lane] = a;
+  __syncthreads();
+  if (wv == 0 && j < D) gmu[j] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+}
+
+// Eh = (G + G^T) / sqrt(c), R = Eh, X = 0, ee partials.  Blocks of the extra grid
+// row blockIdx.y == gridDim.x (when n_cs > 0) compute the mean gradient instead.
 __global__ __launch_bounds__(256) void pcg_init_kernel(int D, const double* G, const FrSched* sc,
                                                        double* Eh, double* R, double* X,
-                                                       double* ee_part) {
+                                                       double* ee_part, int n_cs = 0, int N = 0,
+                                                       const double* rw = nullptr,
+                                                       const double* Gm = nullptr,
+                                                       double* gmu = nullptr) {
   __shared__ double s[kTile][kTile + 1];
   __shared__ double red[16];
+  if ((int)blockIdx.y == (int)gridDim.x) {
+    if ((int)blockIdx.x < n_cs) colsum_block(N, D, blockIdx.x, rw, Gm, gmu);
+    return;
+  }
   const int bi = blockIdx.y, bj = blockIdx.x;
   TileT::load_t(G, D, bi, bj, s);
   const double isc = sc->inv_sqrt_c;
@@ -692,6 +877,16 @@ struct FrWork {
   int last_kmax = 12;             // Newton-Schulz iterations the last root launched
   bool eig_pending = false;       // a dsyevd ran since the last fr_info
   bool sqrt_pending = false;      // a Newton-Schulz / PCG status to read at fr_info
+  bool last_hz = false;           // the last root's schedule had a Z power vector (uZ valid)
+  // fused steps (fr_value_grad with an adagrad update and Philox draws): the last
+  // step's final kernel prepared the next one -- L of the updated parameters, the
+  // draws (Z, s, zz) of rng step prep_step on (prep_k0, prep_k1, prep_stream) and
+  // the power step pz = Z u -- for prep_owner; any other use of the workspace
+  // clears prep_owner
+  const void* prep_owner = nullptr;
+  long long prep_step = -1;
+  uint32_t prep_k0 = 0, prep_k1 = 0, prep_stream = 0;
+  Buf uS, uZ, pz, ypart, lp_part;
   // N x D / N
   Buf Z, X, G, s, logp, zz, r, rk;
   // pinned host staging for host-callback targets
@@ -730,8 +925,10 @@ int reserve_d(FrWork* W, int D, hipStream_t st) {
   for (FrWork::Buf* b : {&W->L, &W->E, &W->T, &W->GS, &W->H, &W->Sig, &W->Yb[0], &W->Yb[1],
                          &W->Zb[0], &W->Zb[1], &W->Eh, &W->Xs, &W->R, &W->P, &W->C1, &W->C2})
     FR_HIP(b->reserve(dd));
-  for (FrWork::Buf* b : {&W->w, &W->offd, &W->pv[0], &W->pv[1], &W->pv[2], &W->pv[3]})
+  for (FrWork::Buf* b : {&W->w, &W->offd, &W->pv[0], &W->pv[1], &W->pv[2], &W->pv[3], &W->uS,
+                         &W->uZ, &W->pz})
     FR_HIP(b->reserve(sizeof(double) * D));
+  FR_HIP(W->ypart.reserve(sizeof(double) * 2 * ((D + 31) / 32) * (size_t)D));
   FR_HIP(W->scal.reserve(sizeof(double) * 8));
   FR_HIP(W->info.reserve(sizeof(int) * 4));
   const size_t nblk = (size_t)((D + 31) / 32) * ((D + 31) / 32);
@@ -756,6 +953,7 @@ int reserve_n(FrWork* W, int D, long long n) {
   FR_HIP(W->X.reserve(nd));
   FR_HIP(W->G.reserve(nd));
   for (FrWork::Buf* b : {&W->s, &W->logp, &W->zz, &W->r, &W->rk}) FR_HIP(b->reserve(n1));
+  FR_HIP(W->lp_part.reserve(n1 * 2 * ((D + 31) / 32)));
   return 0;
 }
 
@@ -797,6 +995,7 @@ int eval_target(FrWork* W, int tgt, const HostTarget& host, int D, long long n, 
 // L, eigh(L L^T) -> (w ascending, Vt rows = eigenvectors), half log det from the
 // eigenvalues (multivariate_t_logpdf's log_pdet, _distributions.py:27-32)
 int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st) {
+  W->prep_owner = nullptr;
   if (int rc = reserve_d(W, D, st)) return rc;
   hipLaunchKernelGGL(fr_unpack_kernel, dim3(blocks((long long)D * D)), dim3(256), 0, st, D, lam,
                      W->L.d());
@@ -826,15 +1025,27 @@ int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st) {
 // run), so 3 warm-started power steps suffice and l_0 comes from the previous
 // root; otherwise 8 power steps from ones and l_0 = 0.05.
 // Also: L, Sigma = L L^T, scal[0] = 0.5 log det Sigma = sum log L_ii.
-int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, const void* owner) {
+// `ready` (a fused step prepared by the previous one, see FrWork::prep_owner): L
+// is current, the power step on Sigma rides in the Sigma GEMM's epilogue (per-row
+// partials of Sigma uS) and the one on Z came from the previous step's last
+// kernel, so no unpack and no power launches.
+int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, const void* owner,
+            bool ready) {
+  if (!ready) W->prep_owner = nullptr;   // L, Sigma, the root and uS change below
   if (int rc = reserve_d(W, D, st)) return rc;
   const long long dd = (long long)D * D;
   const int nblk = ((D + 31) / 32) * ((D + 31) / 32);
+  const int nyp = 2 * ((D + 31) / 32);
   FrSched* sc = static_cast<FrSched*>(W->sched.p);
-  hipLaunchKernelGGL(fr_unpack_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, lam, W->L.d());
+  if (!ready)
+    hipLaunchKernelGGL(fr_unpack_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, lam, W->L.d());
   {
     GemmOp g = mm(D, D, D, W->L.d(), false, W->L.d(), true, W->Sig.d());
     g.sq_part = W->fro_part.d();
+    if (ready) {
+      g.rp_x = W->uS.d();
+      g.rp_part = W->ypart.d();
+    }
     FR_HIP(gemm(g, st));
   }
   // power steps: Sigma x and Z_prev u (the previous root's vectors as start).
@@ -850,7 +1061,7 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
     W->pcg_kmax = 14;
   }
   const bool hz = warm && W->have_z && W->Zf;
-  const int n_pow = warm ? 3 : 8;
+  const int n_pow = ready ? 0 : warm ? 3 : 8;
   const unsigned nb = (unsigned)((D + 7) / 8);
   for (int p = 0; p < n_pow; ++p) {
     const int a = W->pv_cur, b = 1 - a;
@@ -869,9 +1080,15 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
       std::min(warm ? std::max(W->ns_kmax + 2, 6) : std::max(W->ns_kmax + 1, 12), kFrNSMax);
   W->last_warm = warm;
   W->last_kmax = kmax;
-  hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(256), 0, st, D, kmax, W->fro_part.d(),
-                     4 * nblk, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), hz ? 1 : 0, 0.05,
-                     sc, lam, W->scal.d());
+  if (ready)
+    hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(256), 0, st, D, kmax, W->fro_part.d(),
+                       4 * nblk, nullptr, W->pz.d(), 1, 0.05, sc, lam, W->scal.d(), W->ypart.d(),
+                       nyp, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), W->uS.d(), W->uZ.d());
+  else
+    hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(256), 0, st, D, kmax, W->fro_part.d(),
+                       4 * nblk, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), hz ? 1 : 0, 0.05,
+                       sc, lam, W->scal.d(), nullptr, 0, nullptr, nullptr, W->uS.d(), W->uZ.d());
+  W->last_hz = ready || hz;
   // iteration 0: Y_1 -> Yb[1], Z_1 -> Zb[1]
   {
     GemmOp g = mm(D, D, D, W->Sig.d(), false, W->Sig.d(), false, W->Yb[1].d());
@@ -935,12 +1152,17 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
 
 // Preconditioned conjugate gradients for autograd's sqrtm VJP (see pcg_* above):
 // X = the symmetric solution of S X + X S = G_S + G_S^T, into W->Xs.
-int fr_pcg(FrWork* W, int D, hipStream_t st) {
+// (gmu non-null: the init launch also reduces the mean gradient gmu = r^T Gm,
+// N x D, in an extra row of blocks.)
+int fr_pcg(FrWork* W, int D, hipStream_t st, int N = 0, const double* rw = nullptr,
+           const double* Gm = nullptr, double* gmu = nullptr) {
   FrSched* sc = static_cast<FrSched*>(W->sched.p);
   const int nt = (D + kTile - 1) / kTile, nblk = nt * nt;
   const dim3 tg(nt, nt);
-  hipLaunchKernelGGL(pcg_init_kernel, tg, dim3(256), 0, st, D, W->GS.d(), sc, W->Eh.d(),
-                     W->R.d(), W->Xs.d(), W->ee_part.d());
+  const int n_cs = gmu ? (D + 63) / 64 : 0;
+  hipLaunchKernelGGL(pcg_init_kernel, dim3(nt, nt + (n_cs ? 1 : 0)), dim3(256), 0, st, D,
+                     W->GS.d(), sc, W->Eh.d(), W->R.d(), W->Xs.d(), W->ee_part.d(), n_cs, N, rw,
+                     Gm, gmu);
   // P_0 = M^-1(R_0) from C2 = Z R_0, <R_0, Z R_0> in the epilogue
   auto zr = [&](int it) {
     GemmOp g = mm(D, D, D, W->Zf, false, W->R.d(), false, W->C2.d());
@@ -983,6 +1205,7 @@ int fr_pcg(FrWork* W, int D, hipStream_t st) {
 int fr_draw(FrWork* W, int D, long long n, double df, const double* host_eps, uint32_t k0,
             uint32_t k1, uint32_t stream, uint32_t step, const double** s_out,
             const double** z_out, hipStream_t st) {
+  W->prep_owner = nullptr;
   if (host_eps) {
     *s_out = host_eps;
     *z_out = host_eps + n;
@@ -1033,45 +1256,118 @@ int fr_target(FrWork* W, int tgt, int D, long long n, const double* tparams, dou
 // and the value into *value (device pointers).
 int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* host_eps,
                   uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
-                  double* grad, hipStream_t st, bool warm, const void* owner) {
+                  double* grad, hipStream_t st, bool warm, const void* owner,
+                  const MfUpdate* up, const FrNext* next) {
   const int D = f.D, N = f.N;
-  if (int rc = fr_sqrt(W, D, lam, st, warm, owner)) return rc;
+  // fused step: adagrad in the last kernel, Philox draws reduced with zz by their
+  // own kernel, logp (corr_gauss) from the target GEMM's row partials, the mean
+  // gradient in pcg_init's extra blocks; `ready`: the previous fused step of this
+  // run already prepared L, the draws and the Z power step (FrWork::prep_owner)
+  const bool fused = up != nullptr && host_eps == nullptr;
+  const bool ready = fused && warm && owner != nullptr && W->prep_owner == owner &&
+                     W->prep_step == (long long)step && W->prep_k0 == k0 && W->prep_k1 == k1 &&
+                     W->prep_stream == stream;
+  W->prep_owner = nullptr;
+  if (int rc = fr_sqrt(W, D, lam, st, warm, owner, ready)) return rc;
   if (int rc = reserve_n(W, D, N)) return rc;
   const double *s, *z;
-  if (int rc = fr_draw(W, D, N, f.df, host_eps, k0, k1, stream, step, &s, &z, st)) return rc;
+  if (ready) {
+    s = W->s.d();
+    z = W->Z.d();
+  } else if (fused) {
+    hipLaunchKernelGGL(fr_noise_rows_kernel, dim3(N), dim3(256), 0, st, D, Rng{k0, k1, stream},
+                       step, f.df, W->Z.d(), W->s.d(), W->zz.d());
+    s = W->s.d();
+    z = W->Z.d();
+  } else if (int rc = fr_draw(W, D, N, f.df, host_eps, k0, k1, stream, step, &s, &z, st)) {
+    return rc;
+  }
   if (int rc = fr_transform(W, D, N, lam, s, z, W->X.d(), st)) return rc;
+  const int nlp = 2 * ((D + 31) / 32);
+  bool lp_parts = false;
   // target
   if (f.tgt == kTargetCorrGauss) {
-    FR_HIP(gemm(mm(N, D, D, W->X.d(), false, f.tparams, false, W->G.d(), -1.0), st));
-    hipLaunchKernelGGL(fr_rows_kernel, dim3(blocks(N, 4)), dim3(256), 0, st, D, (long long)N,
-                       (f.chivi || f.pd) ? z : nullptr, W->X.d(), W->G.d(), f.tconst, 1, W->zz.d(),
-                       W->logp.d());
+    GemmOp tg = mm(N, D, D, W->X.d(), false, f.tparams, false, W->G.d(), -1.0);
+    if (fused) {   // logp = 0.5 x . G + const from per-row partials
+      tg.rp_w = W->X.d();
+      tg.rp_part = W->lp_part.d();
+      lp_parts = true;
+    }
+    FR_HIP(gemm(tg, st));
+    if (!fused)
+      hipLaunchKernelGGL(fr_rows_kernel, dim3(blocks(N, 4)), dim3(256), 0, st, D, (long long)N,
+                         (f.chivi || f.pd) ? z : nullptr, W->X.d(), W->G.d(), f.tconst, 1,
+                         W->zz.d(), W->logp.d());
   } else {
     if (int rc = eval_target(W, f.tgt, f.host, D, N, W->X.d(), W->logp.d(), W->G.d(), st)) return rc;
-    if (f.chivi || f.pd)
+    if (!fused && (f.chivi || f.pd))
       hipLaunchKernelGGL(fr_rows_kernel, dim3(blocks(N, 4)), dim3(256), 0, st, D, (long long)N,
                          z, nullptr, nullptr, 0.0, 0, W->zz.d(), nullptr);
   }
   hipLaunchKernelGGL(fr_weights_kernel, dim3(1), dim3(1024), 0, st, N, D, f.chivi, f.pd, f.alpha, f.df,
                      f.t_const, W->logp.d(), W->zz.d(), s, W->scal.d(), W->r.d(), W->rk.d(),
-                     value);
+                     value, lp_parts ? W->lp_part.d() : nullptr, lp_parts ? nlp : 0, f.tconst);
   // cotangent of S: G_S = Z^T diag(r / s) G
   GemmOp g = mm(D, D, N, z, true, W->G.d(), false, W->GS.d());
   g.kscale = W->rk.d();
   FR_HIP(gemm(g, st));
-  hipLaunchKernelGGL(fr_colsum_kernel, dim3(blocks(D, 64)), dim3(1024), 0, st, N, D, W->r.d(),
-                     W->G.d(), grad);
+  if (!fused)
+    hipLaunchKernelGGL(fr_colsum_kernel, dim3(blocks(D, 64)), dim3(1024), 0, st, N, D, W->r.d(),
+                       W->G.d(), grad);
   // Sylvester solve (sqrtm VJP): X, symmetric Sigma cotangent of the sample term
-  if (int rc = fr_pcg(W, D, st)) return rc;
+  if (int rc = fused ? fr_pcg(W, D, st, N, W->r.d(), W->G.d(), grad) : fr_pcg(W, D, st)) return rc;
   // G_L = X L, packed with the exp-diagonal chain rule; the entropy / log q term
   // 2 c Sigma^-1 contributes 2 c Sigma^-1 L = 2 c L^-T, whose lower triangle is
   // diag(2 c / L_ii): 2 c on each packed (log) diagonal entry
   FR_HIP(gemm(mm(D, D, D, W->Xs.d(), false, W->L.d(), false, W->H.d()), st));
   const int nt = (D + kTile - 1) / kTile;
-  hipLaunchKernelGGL(fr_pack_kernel, dim3(blocks((long long)D * D)), dim3(256), 0, st, D, W->H.d(),
-                     W->L.d(), W->scal.d(), static_cast<FrSched*>(W->sched.p), W->rr_part.d(),
-                     nt * nt, grad);
+  FrSched* sc = static_cast<FrSched*>(W->sched.p);
+  if (!fused) {
+    hipLaunchKernelGGL(fr_pack_kernel, dim3(blocks((long long)D * D)), dim3(256), 0, st, D, W->H.d(),
+                       W->L.d(), W->scal.d(), sc, W->rr_part.d(), nt * nt, grad);
+    FR_HIP(hipGetLastError());
+    return 0;
+  }
+  // the next step can be prepared when this root ran a Z power step (uZ valid)
+  const bool prep = next && next->prep && W->last_warm && W->last_hz;
+  FrPackArgs a{};
+  a.D = D;
+  const long long P = D + (long long)D * (D + 1) / 2;
+  a.npb = (int)blocks(P);
+  a.nrows = prep ? N : 0;
+  a.nzb = prep ? (D + 7) / 8 : 0;
+  a.GL = W->H.d();
+  a.L = W->L.d();
+  a.scal = W->scal.d();
+  a.sc = sc;
+  a.rr_part = W->rr_part.d();
+  a.n_rr = nt * nt;
+  a.gmu = grad;
+  a.lam = const_cast<double*>(lam);
+  a.ring = up->ring;
+  a.W = up->W;
+  a.step = up->step;
+  a.lr = up->lr;
+  a.eps = up->eps;
+  a.hrow = up->hrow;
+  a.rng = Rng{k0, k1, stream};
+  a.next_step = prep ? next->step : 0;
+  a.df = f.df;
+  a.z = W->Z.d();
+  a.s = W->s.d();
+  a.zz = W->zz.d();
+  a.Zf = W->Zf;
+  a.uZ = W->uZ.d();
+  a.pz = W->pz.d();
+  hipLaunchKernelGGL(fr_pack_update_kernel, dim3(a.npb + a.nrows + a.nzb), dim3(256), 0, st, a);
   FR_HIP(hipGetLastError());
+  if (prep) {
+    W->prep_owner = owner;
+    W->prep_step = next->step;
+    W->prep_k0 = k0;
+    W->prep_k1 = k1;
+    W->prep_stream = stream;
+  }
   return 0;
 }
 
@@ -1094,6 +1390,7 @@ int fr_logdensity(FrWork* W, int D, double df, double t_const, const double* lam
 int fr_log_weights(FrWork* W, const FrSpec& f, const double* lam, long long m,
                    const double* host_eps, uint32_t k0, uint32_t k1, uint32_t stream,
                    uint32_t step, double* lw, double* xs, hipStream_t st) {
+  W->prep_owner = nullptr;
   const int D = f.D;
   if (int rc = fr_sqrt(W, D, lam, st, false)) return rc;
   if (int rc = reserve_n(W, D, m)) return rc;
@@ -1358,6 +1655,7 @@ __global__ __launch_bounds__(64 * kGradWaves) void mfw_grad_kernel(MfwGradArgs A
 int mf_wide_value_grad(FrWork* W, const MfSpec& f, const double* lam, const double* host_eps,
                        uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
                        double* grad, hipStream_t st, const MfUpdate* up) {
+  W->prep_owner = nullptr;
   const int D = f.D, N = f.N;
   if (int rc = reserve_d(W, 1, st)) return rc;
   if (int rc = reserve_n(W, D, N)) return rc;
@@ -1434,6 +1732,7 @@ __global__ __launch_bounds__(256) void sub_kernel(long long n, const double* a, 
 int mf_wide_log_weights(FrWork* W, const MfSpec& f, const double* lam, long long m,
                         const double* host_eps, uint32_t k0, uint32_t k1, uint32_t stream,
                         uint32_t step, double* lw, double* xs, hipStream_t st) {
+  W->prep_owner = nullptr;
   const int D = f.D;
   if (int rc = reserve_d(W, 1, st)) return rc;
   if (int rc = reserve_n(W, D, m)) return rc;
@@ -1448,6 +1747,7 @@ int mf_wide_log_weights(FrWork* W, const MfSpec& f, const double* lam, long long
 
 // Sigma [D][D] (nullable) and ascending eigenvalues [D] (nullable) of Sigma = L L^T
 int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, hipStream_t st) {
+  W->prep_owner = nullptr;
   if (int rc = reserve_d(W, D, st)) return rc;
   hipLaunchKernelGGL(fr_unpack_kernel, dim3(blocks((long long)D * D)), dim3(256), 0, st, D, lam,
                      W->L.d());

@@ -91,6 +91,13 @@ struct GemmOp {
   // ns0_z = ns0[2] (3 I - ns0[3] Sigma), written for the same tile
   const double* ns0;
   double* ns0_z;
+  // optional per-row partials of the written tile, 2 per 32-column tile (one per
+  // 16-column quadrant) at rp_part[(2 bx + quadrant column) M + row]:
+  //   rp_x: sum_j C_ij rp_x[j]  (a matrix-vector product: a power step on C)
+  //   rp_w: sum_j C_ij rp_w[i][j] (leading dimension ldc; a row-wise dot product)
+  const double* rp_x;
+  const double* rp_w;
+  double* rp_part;
   // set by gemm_group: M, N multiples of 32, K of KTG, 16-byte aligned operand rows, no
   // kscale / dual product -> the LDS-DMA main loop
   int glds;
@@ -512,7 +519,8 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
       r4[r] += p;
     }
     const int col = j0 + wn * 16 + (lane & 15);
-    double sq = 0.0, dt = 0.0;
+    double sq = 0.0, dt = 0.0, rp[4] = {0.0, 0.0, 0.0, 0.0};
+    const double rpx = (g.rp_x && col < g.N) ? g.rp_x[col] : 0.0;
     const double alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
     const double shift = g.sq_shift_dev ? *g.sq_shift_dev : g.sq_shift;
 #pragma unroll
@@ -530,6 +538,8 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
         }
         double* c = g.C + (long long)row * g.ldc + col;
         if (g.dot_with) dt = fma(g.dot_with[(long long)row * g.ldc + col], v, dt);
+        if (g.rp_x) rp[r] = v * rpx;
+        if (g.rp_w) rp[r] = v * g.rp_w[(long long)row * g.ldc + col];
         if (g.beta != 0.0) v += g.beta * *c;
         *c = v;
         const double e = row == col ? v - shift : v;
@@ -545,6 +555,16 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) dt += __shfl_xor(dt, off, 64);
       if (lane == 0) g.dot_part[4 * (by * ntx + bx) + q] = dt;
+    }
+    if (g.rp_part) {
+      // sum over the 16 lanes of a row (lanes 16 kq .. 16 kq + 15 hold row kq + 4 r)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) rp[r] += __shfl_xor(rp[r], off, 64);
+        const int row = i0 + wm * 16 + kq + 4 * r;
+        if ((lane & 15) == 0 && row < g.M) g.rp_part[(long long)(2 * bx + wn) * g.M + row] = rp[r];
+      }
     }
   }
   __syncthreads();

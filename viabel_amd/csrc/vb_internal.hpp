@@ -205,7 +205,7 @@ struct FrSpec {
 int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st);  // eigh of Sigma
 // Newton-Schulz sqrtm; warm: Sigma is close to the previous call's (optimisation run)
 int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm = false,
-            const void* owner = nullptr);
+            const void* owner = nullptr, bool ready = false);
 constexpr int kFrNSMax = 40;  // Newton-Schulz iterations launched at most per root
 int fr_draw(FrWork* W, int D, long long n, double df, const double* host_eps, uint32_t k0,
             uint32_t k1, uint32_t stream, uint32_t step, const double** s_out,
@@ -214,10 +214,21 @@ int fr_transform(FrWork* W, int D, long long n, const double* mu, const double* 
                  const double* z, double* x, hipStream_t st);
 int fr_target(FrWork* W, int tgt, int D, long long n, const double* tparams, double tconst,
               const double* x, double* logp, double* G, hipStream_t st);
+struct MfUpdate;
+// The next step of a fused run: its draws (rng step `step`) and L are prepared by
+// this step's last kernel when `prep`.
+struct FrNext {
+  bool prep;
+  uint32_t step;
+};
+// up (non-null, Philox draws): the windowed adagrad step is fused into the last
+// kernel (lam updated in place, ring / history row written; grad keeps only the
+// mean part), and with next->prep the step after it is prepared (FrWork).
 int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* host_eps,
                   uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* value,
                   double* grad, hipStream_t st, bool warm = false,
-                  const void* owner = nullptr);
+                  const void* owner = nullptr, const MfUpdate* up = nullptr,
+                  const FrNext* next = nullptr);
 int fr_logdensity(FrWork* W, int D, double df, double t_const, const double* lam, const double* x,
                   long long n, double* out, hipStream_t st);
 int fr_log_weights(FrWork* W, const FrSpec& f, const double* lam, long long m,
