@@ -6,7 +6,9 @@ import sys
 path = sys.argv[1] if len(sys.argv) > 1 else 'gpurun_out/prof_fr/fr_kernel_trace.csv'
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r['Start_Timestamp']))
-starts = [i for i, r in enumerate(rows) if 'fr_unpack_kernel' in r['Kernel_Name']]
+# a step starts with Sigma = L L^T, the step's only NT GEMM (fused steps have
+# no unpack launch)
+starts = [i for i, r in enumerate(rows) if 'gemm_f64_kernel<false, true' in r['Kernel_Name']]
 i0, i1 = starts[k], starts[k + 1]
 t0 = int(rows[i0]['Start_Timestamp'])
 prev = t0

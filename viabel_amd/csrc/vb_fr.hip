@@ -203,11 +203,21 @@ __global__ __launch_bounds__(1024) void fr_weights_kernel(int N, int D, int chiv
                                                           int n_lp = 0, double lp_const = 0.0) {
   __shared__ double red[16];
   if (lp_part) {
-    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+    // 8 threads per row (independent loads of every 8th partial), fixed xor tree
+    const int T = blockDim.x;
+    for (int base = 0; base < N; base += T / 8) {
+      const int k = base + (int)threadIdx.x / 8, sub = threadIdx.x & 7;
       double a = 0.0;
-      for (int t = 0; t < n_lp; ++t) a += lp_part[(long long)t * N + k];
-      logp[k] = 0.5 * a + lp_const;
+      if (k < N) {
+#pragma unroll 4
+        for (int t = sub; t < n_lp; t += 8) a += lp_part[(long long)t * N + k];
+      }
+      a += __shfl_xor(a, 1, 64);
+      a += __shfl_xor(a, 2, 64);
+      a += __shfl_xor(a, 4, 64);
+      if (sub == 0 && k < N) logp[k] = 0.5 * a + lp_const;
     }
+    __syncthreads();   // logp rows are re-read below by other threads
   }
   const double hld = scal[0];
   const double e = 0.5 * (df + D);
@@ -468,7 +478,7 @@ __device__ double ns_alpha(double l) { return sqrt(3.0 / (1.0 + l + l * l)); }
 // Sigma GEMM's per-row partials ypart [nyp][D], summed here and saved to ysave),
 // v = Z_prev u.  Every sched also stores the unit vectors uS = y / ||y||,
 // uZ = v / ||v|| that the next fused step multiplies by.
-__global__ __launch_bounds__(256) void fr_sched_kernel(int D, int kmax, const double* fro_part,
+__global__ __launch_bounds__(1024) void fr_sched_kernel(int D, int kmax, const double* fro_part,
                                                        int n_part, const double* y,
                                                        const double* v, int has_z,
                                                        double l_default, FrSched* sc,
@@ -476,18 +486,35 @@ __global__ __launch_bounds__(256) void fr_sched_kernel(int D, int kmax, const do
                                                        const double* ypart, int nyp, double* ysave,
                                                        double* vsave, double* uS, double* uZ) {
   __shared__ double red[16];
+  const int T = blockDim.x;
   double f = 0.0, ly = 0.0, lv = 0.0, ld = 0.0;
-  for (int i = threadIdx.x; i < n_part; i += 256) f += fro_part[i];
-  for (int i = threadIdx.x; i < D; i += 256) {
-    double yi;
-    if (ypart) {
-      yi = 0.0;
-      for (int t = 0; t < nyp; ++t) yi += ypart[(long long)t * D + i];
-      ysave[i] = yi;
-    } else {
-      yi = y[i];
+  for (int i = threadIdx.x; i < n_part; i += T) f += fro_part[i];
+  if (ypart) {
+    // TPR threads per row (all rows in one round when D <= T / 2), each summing
+    // every TPR-th partial with independent loads, then a fixed xor-shuffle tree:
+    // the same total in every run
+    const int TPR = D >= T / 2 ? 2 : (D >= T / 4 ? 4 : 8);
+    for (int base = 0; base < D; base += T / TPR) {
+      const int i = base + (int)threadIdx.x / TPR, sub = threadIdx.x & (TPR - 1);
+      double yp[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int t = sub + u * TPR;
+        yp[u] = (i < D && t < nyp) ? ypart[(long long)t * D + i] : 0.0;
+      }
+      double yi = 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) yi += yp[u];
+      for (int t = sub + 16 * TPR; t < nyp; t += TPR) yi += (i < D) ? ypart[(long long)t * D + i] : 0.0;
+      for (int o = 1; o < TPR; o <<= 1) yi += __shfl_xor(yi, o, 64);
+      if (sub == 0 && i < D) {
+        ysave[i] = yi;
+        ly += yi * yi;
+      }
     }
-    ly += yi * yi;
+  }
+  for (int i = threadIdx.x; i < D; i += T) {
+    if (!ypart) ly += y[i] * y[i];
     if (has_z) {
       lv += v[i] * v[i];
       if (vsave) vsave[i] = v[i];
@@ -503,7 +530,7 @@ __global__ __launch_bounds__(256) void fr_sched_kernel(int D, int kmax, const do
   ld = block_sum(ld, red);
   {
     const double iy = ly > 0.0 ? 1.0 / sqrt(ly) : 0.0, iv = lv > 0.0 ? 1.0 / sqrt(lv) : 0.0;
-    for (int i = threadIdx.x; i < D; i += 256) {
+    for (int i = threadIdx.x; i < D; i += T) {
       uS[i] = (ypart ? ysave[i] : y[i]) * iy;
       if (has_z && lv > 0.0) uZ[i] = v[i] * iv;
     }
@@ -1081,11 +1108,11 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
   W->last_warm = warm;
   W->last_kmax = kmax;
   if (ready)
-    hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(256), 0, st, D, kmax, W->fro_part.d(),
+    hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(1024), 0, st, D, kmax, W->fro_part.d(),
                        4 * nblk, nullptr, W->pz.d(), 1, 0.05, sc, lam, W->scal.d(), W->ypart.d(),
                        nyp, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), W->uS.d(), W->uZ.d());
   else
-    hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(256), 0, st, D, kmax, W->fro_part.d(),
+    hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(1024), 0, st, D, kmax, W->fro_part.d(),
                        4 * nblk, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), hz ? 1 : 0, 0.05,
                        sc, lam, W->scal.d(), nullptr, 0, nullptr, nullptr, W->uS.d(), W->uZ.d());
   W->last_hz = ready || hz;
