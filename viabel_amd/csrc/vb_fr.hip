@@ -474,51 +474,28 @@ __device__ double ns_alpha(double l) { return sqrt(3.0 / (1.0 + l + l * l)); }
 
 // One block: c, l_0 and the whole schedule; resets the per-step flags.
 // Also scal[0] = 0.5 log det Sigma = sum_i log L_ii, the free log-diagonal of lam.
-// Power vectors: y = Sigma x (x the previous unit vector; in a fused step the
-// Sigma GEMM's per-row partials ypart [nyp][D], summed here and saved to ysave),
-// v = Z_prev u.  Every sched also stores the unit vectors uS = y / ||y||,
-// uZ = v / ||v|| that the next fused step multiplies by.
+// Power vectors: y = Sigma x (x the previous unit vector), v = Z_prev u.  A
+// fused step instead passes qf_part, the Sigma GEMM's partials of x^T Sigma x for
+// x = y (the previous step's last kernel computed y = Sigma_prev uS): lambda_max
+// is estimated by the Rayleigh quotient x^T Sigma x / x^T x.  Every sched stores
+// the unit vectors uS = y / ||y||, uZ = v / ||v|| for the next power steps.
 __global__ __launch_bounds__(1024) void fr_sched_kernel(int D, int kmax, const double* fro_part,
                                                        int n_part, const double* y,
                                                        const double* v, int has_z,
                                                        double l_default, FrSched* sc,
                                                        const double* lam, double* scal,
-                                                       const double* ypart, int nyp, double* ysave,
-                                                       double* vsave, double* uS, double* uZ) {
+                                                       const double* qf_part, double* uS,
+                                                       double* uZ) {
   __shared__ double red[16];
   const int T = blockDim.x;
-  double f = 0.0, ly = 0.0, lv = 0.0, ld = 0.0;
-  for (int i = threadIdx.x; i < n_part; i += T) f += fro_part[i];
-  if (ypart) {
-    // TPR threads per row (all rows in one round when D <= T / 2), each summing
-    // every TPR-th partial with independent loads, then a fixed xor-shuffle tree:
-    // the same total in every run
-    const int TPR = D >= T / 2 ? 2 : (D >= T / 4 ? 4 : 8);
-    for (int base = 0; base < D; base += T / TPR) {
-      const int i = base + (int)threadIdx.x / TPR, sub = threadIdx.x & (TPR - 1);
-      double yp[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int t = sub + u * TPR;
-        yp[u] = (i < D && t < nyp) ? ypart[(long long)t * D + i] : 0.0;
-      }
-      double yi = 0.0;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) yi += yp[u];
-      for (int t = sub + 16 * TPR; t < nyp; t += TPR) yi += (i < D) ? ypart[(long long)t * D + i] : 0.0;
-      for (int o = 1; o < TPR; o <<= 1) yi += __shfl_xor(yi, o, 64);
-      if (sub == 0 && i < D) {
-        ysave[i] = yi;
-        ly += yi * yi;
-      }
-    }
+  double f = 0.0, ly = 0.0, lv = 0.0, ld = 0.0, qf = 0.0;
+  for (int i = threadIdx.x; i < n_part; i += T) {
+    f += fro_part[i];
+    if (qf_part) qf += qf_part[i];
   }
   for (int i = threadIdx.x; i < D; i += T) {
-    if (!ypart) ly += y[i] * y[i];
-    if (has_z) {
-      lv += v[i] * v[i];
-      if (vsave) vsave[i] = v[i];
-    }
+    ly += y[i] * y[i];
+    if (has_z) lv += v[i] * v[i];
     ld += lam[D + (long long)i * (i + 1) / 2 + i];
   }
   f = block_sum(f, red);
@@ -528,16 +505,21 @@ __global__ __launch_bounds__(1024) void fr_sched_kernel(int D, int kmax, const d
   lv = block_sum(lv, red);
   __syncthreads();
   ld = block_sum(ld, red);
+  if (qf_part) {
+    __syncthreads();
+    qf = block_sum(qf, red);
+  }
   {
     const double iy = ly > 0.0 ? 1.0 / sqrt(ly) : 0.0, iv = lv > 0.0 ? 1.0 / sqrt(lv) : 0.0;
     for (int i = threadIdx.x; i < D; i += T) {
-      uS[i] = (ypart ? ysave[i] : y[i]) * iy;
+      uS[i] = y[i] * iy;
       if (has_z && lv > 0.0) uZ[i] = v[i] * iv;
     }
   }
   if (threadIdx.x != 0) return;
   scal[0] = ld;
-  const double lmax = sqrt(ly);                  // ||Sigma x|| for unit x <= lambda_max
+  // ||Sigma x|| for unit x, or the Rayleigh quotient: both <= lambda_max
+  const double lmax = qf_part ? (ly > 0.0 ? qf / ly : 0.0) : sqrt(ly);
   const double c = fmin(1.25 * lmax, sqrt(f));   // ||Sigma||_F >= lambda_max
   double l = l_default;
   if (has_z && lv > 0.0) {
@@ -578,9 +560,10 @@ __global__ __launch_bounds__(1024) void fr_sched_kernel(int D, int kmax, const d
 // of fr_pack_kernel goes straight into the windowed adagrad step (adagrad_step,
 // as adagrad_update_kernel) and L of the new parameters is written for the next
 // step's Sigma GEMM (no unpack); extra blocks prepare the next step: its draws
-// (fr_noise_row, with zz) and one power step v = Z u on this step's root.
-// Blocks [0, npb): parameters (mu first, then the packed lower triangle),
-// [npb, npb + nrows): draw rows, then Z rows (8 per block).
+// (fr_noise_row, with zz) and one power step each on this step's Sigma and root
+// Z (pS = Sigma uS, pz = Z uZ).  Blocks [0, npb): parameters (mu first, then the
+// packed lower triangle), [npb, npb + nrows): draw rows, then nzb blocks of
+// Sigma rows and nzb of Z rows (8 per block).
 struct FrPackArgs {
   int D, npb, nrows, nzb;
   const double* GL;
@@ -601,9 +584,8 @@ struct FrPackArgs {
   uint32_t next_step;
   double df;
   double *z, *s, *zz;
-  const double* Zf;
-  const double* uZ;
-  double* pz;
+  const double *Zf, *uZ, *Sig, *uS;
+  double *pz, *pS;
 };
 
 __global__ __launch_bounds__(256) void fr_pack_update_kernel(FrPackArgs a) {
@@ -616,15 +598,22 @@ __global__ __launch_bounds__(256) void fr_pack_update_kernel(FrPackArgs a) {
       fr_noise_row(D, k, a.rng, a.next_step, a.df, a.z, a.s, a.zz, red);
       return;
     }
-    // v = Z u: two rows per wave
+    // power steps pS = Sigma uS (blocks [0, nzb)) and pz = Z uZ (the next nzb):
+    // two rows per wave
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int zb = k - a.nrows;
+    const bool zside = zb >= a.nzb;
+    if (zside) zb -= a.nzb;
+    const double* M = zside ? a.Zf : a.Sig;
+    const double* u = zside ? a.uZ : a.uS;
+    double* out = zside ? a.pz : a.pS;
     for (int rr = 0; rr < 2; ++rr) {
-      const int row = (k - a.nrows) * 8 + wv * 2 + rr;
+      const int row = zb * 8 + wv * 2 + rr;
       if (row >= D) break;
       double t = 0.0;
-      for (int j = lane; j < D; j += 64) t = fma(a.Zf[(long long)row * D + j], a.uZ[j], t);
+      for (int j = lane; j < D; j += 64) t = fma(M[(long long)row * D + j], u[j], t);
       t = wave_sum(t);
-      if (lane == 0) a.pz[row] = t;
+      if (lane == 0) out[row] = t;
     }
     return;
   }
@@ -913,7 +902,7 @@ struct FrWork {
   const void* prep_owner = nullptr;
   long long prep_step = -1;
   uint32_t prep_k0 = 0, prep_k1 = 0, prep_stream = 0;
-  Buf uS, uZ, pz, ypart, lp_part;
+  Buf uS, uZ, pS, pz, ypart, lp_part;
   // N x D / N
   Buf Z, X, G, s, logp, zz, r, rk;
   // pinned host staging for host-callback targets
@@ -953,9 +942,9 @@ int reserve_d(FrWork* W, int D, hipStream_t st) {
                          &W->Zb[0], &W->Zb[1], &W->Eh, &W->Xs, &W->R, &W->P, &W->C1, &W->C2})
     FR_HIP(b->reserve(dd));
   for (FrWork::Buf* b : {&W->w, &W->offd, &W->pv[0], &W->pv[1], &W->pv[2], &W->pv[3], &W->uS,
-                         &W->uZ, &W->pz})
+                         &W->uZ, &W->pS, &W->pz})
     FR_HIP(b->reserve(sizeof(double) * D));
-  FR_HIP(W->ypart.reserve(sizeof(double) * 2 * ((D + 31) / 32) * (size_t)D));
+  FR_HIP(W->ypart.reserve(sizeof(double) * 4 * ((D + 31) / 32) * ((D + 31) / 32)));
   FR_HIP(W->scal.reserve(sizeof(double) * 8));
   FR_HIP(W->info.reserve(sizeof(int) * 4));
   const size_t nblk = (size_t)((D + 31) / 32) * ((D + 31) / 32);
@@ -1053,25 +1042,24 @@ int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st) {
 // root; otherwise 8 power steps from ones and l_0 = 0.05.
 // Also: L, Sigma = L L^T, scal[0] = 0.5 log det Sigma = sum log L_ii.
 // `ready` (a fused step prepared by the previous one, see FrWork::prep_owner): L
-// is current, the power step on Sigma rides in the Sigma GEMM's epilogue (per-row
-// partials of Sigma uS) and the one on Z came from the previous step's last
-// kernel, so no unpack and no power launches.
+// is current and the power steps (pS = Sigma_prev uS, pz = Z_prev uZ) came from
+// the previous step's last kernel; the Sigma GEMM's epilogue gives the Rayleigh
+// quotient partials of pS, so no unpack and no power launches.
 int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, const void* owner,
             bool ready) {
   if (!ready) W->prep_owner = nullptr;   // L, Sigma, the root and uS change below
   if (int rc = reserve_d(W, D, st)) return rc;
   const long long dd = (long long)D * D;
   const int nblk = ((D + 31) / 32) * ((D + 31) / 32);
-  const int nyp = 2 * ((D + 31) / 32);
   FrSched* sc = static_cast<FrSched*>(W->sched.p);
   if (!ready)
     hipLaunchKernelGGL(fr_unpack_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, lam, W->L.d());
   {
     GemmOp g = mm(D, D, D, W->L.d(), false, W->L.d(), true, W->Sig.d());
     g.sq_part = W->fro_part.d();
-    if (ready) {
-      g.rp_x = W->uS.d();
-      g.rp_part = W->ypart.d();
+    if (ready) {   // Rayleigh quotient partials of the previous step's Sigma uS
+      g.qf_x = W->pS.d();
+      g.qf_part = W->ypart.d();
     }
     FR_HIP(gemm(g, st));
   }
@@ -1093,9 +1081,12 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
   for (int p = 0; p < n_pow; ++p) {
     const int a = W->pv_cur, b = 1 - a;
     const bool xfirst = p == 0 && !warm, ufirst = p == 0 && !W->zv_init;
+    // a warm start begins from the last sched's unit vectors (fused steps in
+    // between updated them, not pv)
+    const double* xin = xfirst ? nullptr : (p == 0 ? W->uS.d() : W->pv[a].d());
+    const double* uin = ufirst ? nullptr : (p == 0 && W->last_hz ? W->uZ.d() : W->pv[2 + a].d());
     hipLaunchKernelGGL(fr_power2_kernel, dim3(nb, hz ? 2 : 1), dim3(256), 0, st, D, W->Sig.d(),
-                       xfirst ? nullptr : W->pv[a].d(), W->pv[b].d(), W->Zf,
-                       ufirst ? nullptr : W->pv[2 + a].d(), W->pv[2 + b].d());
+                       xin, W->pv[b].d(), W->Zf, uin, W->pv[2 + b].d());
     W->pv_cur = b;
   }
   if (hz) W->zv_init = true;
@@ -1109,12 +1100,12 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
   W->last_kmax = kmax;
   if (ready)
     hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(1024), 0, st, D, kmax, W->fro_part.d(),
-                       4 * nblk, nullptr, W->pz.d(), 1, 0.05, sc, lam, W->scal.d(), W->ypart.d(),
-                       nyp, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), W->uS.d(), W->uZ.d());
+                       4 * nblk, W->pS.d(), W->pz.d(), 1, 0.05, sc, lam, W->scal.d(),
+                       W->ypart.d(), W->uS.d(), W->uZ.d());
   else
     hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(1024), 0, st, D, kmax, W->fro_part.d(),
                        4 * nblk, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), hz ? 1 : 0, 0.05,
-                       sc, lam, W->scal.d(), nullptr, 0, nullptr, nullptr, W->uS.d(), W->uZ.d());
+                       sc, lam, W->scal.d(), nullptr, W->uS.d(), W->uZ.d());
   W->last_hz = ready || hz;
   // iteration 0: Y_1 -> Yb[1], Z_1 -> Zb[1]
   {
@@ -1386,7 +1377,10 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
   a.Zf = W->Zf;
   a.uZ = W->uZ.d();
   a.pz = W->pz.d();
-  hipLaunchKernelGGL(fr_pack_update_kernel, dim3(a.npb + a.nrows + a.nzb), dim3(256), 0, st, a);
+  a.Sig = W->Sig.d();
+  a.uS = W->uS.d();
+  a.pS = W->pS.d();
+  hipLaunchKernelGGL(fr_pack_update_kernel, dim3(a.npb + a.nrows + 2 * a.nzb), dim3(256), 0, st, a);
   FR_HIP(hipGetLastError());
   if (prep) {
     W->prep_owner = owner;

@@ -98,6 +98,10 @@ struct GemmOp {
   const double* rp_x;
   const double* rp_w;
   double* rp_part;
+  // optional: per-wave partial sums of qf_x_i C_ij qf_x_j (a quadratic form of
+  // the written tile), 4 per block at qf_part[4 (by gridDim.x + bx) + wave]
+  const double* qf_x;
+  double* qf_part;
   // set by gemm_group: M, N multiples of 32, K of KTG, 16-byte aligned operand rows, no
   // kscale / dual product -> the LDS-DMA main loop
   int glds;
@@ -519,8 +523,9 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
       r4[r] += p;
     }
     const int col = j0 + wn * 16 + (lane & 15);
-    double sq = 0.0, dt = 0.0, rp[4] = {0.0, 0.0, 0.0, 0.0};
+    double sq = 0.0, dt = 0.0, qf = 0.0, rp[4] = {0.0, 0.0, 0.0, 0.0};
     const double rpx = (g.rp_x && col < g.N) ? g.rp_x[col] : 0.0;
+    const double qfx = (g.qf_x && col < g.N) ? g.qf_x[col] : 0.0;
     const double alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
     const double shift = g.sq_shift_dev ? *g.sq_shift_dev : g.sq_shift;
 #pragma unroll
@@ -539,6 +544,7 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
         double* c = g.C + (long long)row * g.ldc + col;
         if (g.dot_with) dt = fma(g.dot_with[(long long)row * g.ldc + col], v, dt);
         if (g.rp_x) rp[r] = v * rpx;
+        if (g.qf_x) qf = fma(g.qf_x[row] * v, qfx, qf);
         if (g.rp_w) rp[r] = v * g.rp_w[(long long)row * g.ldc + col];
         if (g.beta != 0.0) v += g.beta * *c;
         *c = v;
@@ -555,6 +561,11 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) dt += __shfl_xor(dt, off, 64);
       if (lane == 0) g.dot_part[4 * (by * ntx + bx) + q] = dt;
+    }
+    if (g.qf_part) {
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) qf += __shfl_xor(qf, off, 64);
+      if (lane == 0) g.qf_part[4 * (by * ntx + bx) + q] = qf;
     }
     if (g.rp_part) {
       // sum over the 16 lanes of a row (lanes 16 kq .. 16 kq + 15 hold row kq + 4 r)
