@@ -264,3 +264,33 @@ def test_fused_philox_steps_across_advances(objective, target, D):
     _close(vals[0], ovals, 1e-7)
     _close(hist[0], ohist, 1e-7)
     _close(lam[0], ohist[-1], 1e-7)
+
+
+def test_newton_schulz_retry_when_the_learnt_count_is_short(monkeypatch):
+    """Warm Newton-Schulz roots launch exactly the learnt iteration count; a step
+    that needs more makes the advance restore its snapshot (lambda, adagrad
+    window) and run again with a larger count (vb_capi.hip vb_run_advance,
+    vb_fr.hip fr_info).  Forced here by starting warm roots at 3 iterations: the
+    trajectory still equals the oracle's."""
+    vb, targets, fo, ro, vo = _mods()
+    monkeypatch.setenv('VIABEL_AMD_FR_NS_START', '3')
+    D, N, n_iters = 64, 16, 9
+    lam0 = _lam(D, 11)
+    fam = vb.t_variational_family(D, 30.0, rng='philox')
+    obj = vb.black_box_chivi(2.0, fam, targets.corr_gauss(D), N)
+    run = vb.DeviceRun(obj, n_iters, lam0, learning_rate=0.02)
+    run.advance_philox(6, 2, 4, 0)
+    run.advance_philox(3, 2, 4, 6)
+    lam, hist, vals, _ = run.result()
+    ofam = fo.FullRankT(D, 30.0)
+    otgt = fo.target_fn('corr_gauss', D)
+    step = [0]
+
+    def f(l):
+        draws = ro.fr_noise(2, 4, step[0], N, D, 30.0)
+        step[0] += 1
+        return fo.chivi_value_grad(ofam, otgt, l, N, 2.0, draws=draws)
+    osm, ohist, ovals, _ = vo.adagrad_optimize(n_iters, f, lam0, learning_rate=0.02)
+    _close(vals[0], ovals, 1e-7)
+    _close(hist[0], ohist, 1e-7)
+    _close(lam[0], ohist[-1], 1e-7)

@@ -720,6 +720,7 @@ struct vb_run {
   vbk::FrSpec spec{};
   vbk::MfSpec mspec{};
   DevBuf tparams, grad;
+  DevBuf backup;  // full rank: lambda and the adagrad window at the start of an advance
   // launch timing (vb_run_set_timing): event pairs, reused; `ev_used` recorded
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
@@ -857,42 +858,12 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
   return VB_OK;
 }
 
-int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
-  if (!r) return fail(VB_EINVAL, "null vb_run");
-  vb_ctx* c = r->ctx;
-  VB_TRY(check_ctx(c));
-  if (!noise) return fail(VB_EINVAL, "null noise");
-  if (n_steps < 0 || r->done + n_steps > r->n_iters)
-    return fail(VB_EINVAL, "advance(%lld) past n_iters=%lld (done %lld)", (long long)n_steps,
-                (long long)r->n_iters, (long long)r->done);
-  if (n_steps == 0) return VB_OK;
-  const bool host = noise->kind == VB_NOISE_HOST;
-  const int D = r->fi.D, N = r->N;
+// The per-step launches of full-rank / wide mean-field runs (one value_grad +
+// update per step and problem), for steps [r->done, r->done + n_steps).
+static int advance_fr_steps(vb_ctx* c, vb_run* r, int64_t n_steps, const vb_noise* noise,
+                            bool host, const double* noise_base, size_t per_step, uint32_t k0,
+                            uint32_t k1) {
   const size_t P = r->fi.P;
-  const size_t per_step = (size_t)N * D + (r->fr ? (size_t)N : 0);
-  if (host) {
-    if (!noise->eps) return fail(VB_EINVAL, "host noise requires eps");
-    if (ptr_class(noise->eps) < 0) return foreign_ptr_error(noise->eps);
-    const size_t tot = per_step * n_steps * r->nprob;
-    if (is_device_ptr(noise->eps)) {
-      // used in place
-    } else {
-      VB_TRY(r->noise.reserve(tot * sizeof(double)));
-      VB_HIP(hipMemcpyAsync(r->noise.p, noise->eps, tot * sizeof(double), hipMemcpyHostToDevice,
-                            c->stream));
-    }
-  }
-  const double* noise_base =
-      host ? (is_device_ptr(noise->eps) ? noise->eps : r->noise.d()) : nullptr;
-  uint32_t k0, k1;
-  key_of(noise->seed, &k0, &k1);
-
-  std::pair<hipEvent_t, hipEvent_t>* call_ev = nullptr;
-  if (!r->sep) {
-    VB_TRY(r->next_event(n_steps, &call_ev));
-    if (call_ev) VB_HIP(hipEventRecord(call_ev->first, c->stream));
-  }
-  if (r->fr || r->wide) {
     vbk::FrWork* W;
     VB_TRY(fr_work(c, &W));
     const uint32_t stride = noise->stream_stride ? noise->stream_stride : 1;
@@ -945,6 +916,73 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
                                             r->ring.d() + q * P * r->W, r->W, step, lr, r->eps,
                                             nullptr, c->stream, hrow));
         }
+      }
+    }
+  return VB_OK;
+}
+
+int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
+  if (!r) return fail(VB_EINVAL, "null vb_run");
+  vb_ctx* c = r->ctx;
+  VB_TRY(check_ctx(c));
+  if (!noise) return fail(VB_EINVAL, "null noise");
+  if (n_steps < 0 || r->done + n_steps > r->n_iters)
+    return fail(VB_EINVAL, "advance(%lld) past n_iters=%lld (done %lld)", (long long)n_steps,
+                (long long)r->n_iters, (long long)r->done);
+  if (n_steps == 0) return VB_OK;
+  const bool host = noise->kind == VB_NOISE_HOST;
+  const int D = r->fi.D, N = r->N;
+  const size_t P = r->fi.P;
+  const size_t per_step = (size_t)N * D + (r->fr ? (size_t)N : 0);
+  if (host) {
+    if (!noise->eps) return fail(VB_EINVAL, "host noise requires eps");
+    if (ptr_class(noise->eps) < 0) return foreign_ptr_error(noise->eps);
+    const size_t tot = per_step * n_steps * r->nprob;
+    if (is_device_ptr(noise->eps)) {
+      // used in place
+    } else {
+      VB_TRY(r->noise.reserve(tot * sizeof(double)));
+      VB_HIP(hipMemcpyAsync(r->noise.p, noise->eps, tot * sizeof(double), hipMemcpyHostToDevice,
+                            c->stream));
+    }
+  }
+  const double* noise_base =
+      host ? (is_device_ptr(noise->eps) ? noise->eps : r->noise.d()) : nullptr;
+  uint32_t k0, k1;
+  key_of(noise->seed, &k0, &k1);
+
+  std::pair<hipEvent_t, hipEvent_t>* call_ev = nullptr;
+  if (!r->sep) {
+    VB_TRY(r->next_event(n_steps, &call_ev));
+    if (call_ev) VB_HIP(hipEventRecord(call_ev->first, c->stream));
+  }
+  if (r->fr || r->wide) {
+    // one full-rank problem: a snapshot of lambda and the adagrad window lets the
+    // advance run again when a warm Newton-Schulz root launched too few
+    // iterations (they launch exactly the learnt count, no spares; vb_fr.hip
+    // fr_info)
+    const bool snap = r->fr && r->nprob == 1;
+    const size_t snap_n = P + P * (size_t)r->W;
+    if (snap) {
+      VB_TRY(r->backup.reserve(snap_n * sizeof(double)));
+      VB_HIP(hipMemcpyAsync(r->backup.d(), r->lam.d(), P * sizeof(double), hipMemcpyDeviceToDevice,
+                            c->stream));
+      VB_HIP(hipMemcpyAsync(r->backup.d() + P, r->ring.d(), P * r->W * sizeof(double),
+                            hipMemcpyDeviceToDevice, c->stream));
+    }
+    VB_TRY(advance_fr_steps(c, r, n_steps, noise, host, noise_base, per_step, k0, k1));
+    if (r->fr) {
+      VB_TRY(sync(c));
+      vbk::FrWork* W;
+      VB_TRY(fr_work(c, &W));
+      bool again = false;
+      if (int rc = vbk::fr_info(W, c->stream, snap ? &again : nullptr)) return rc;
+      if (again) {
+        VB_HIP(hipMemcpyAsync(r->lam.d(), r->backup.d(), P * sizeof(double),
+                              hipMemcpyDeviceToDevice, c->stream));
+        VB_HIP(hipMemcpyAsync(r->ring.d(), r->backup.d() + P, P * r->W * sizeof(double),
+                              hipMemcpyDeviceToDevice, c->stream));
+        VB_TRY(advance_fr_steps(c, r, n_steps, noise, host, noise_base, per_step, k0, k1));
       }
     }
   } else if (r->sep) {

@@ -32,6 +32,7 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <new>
 
@@ -891,6 +892,7 @@ struct FrWork {
   const void* owner = nullptr;    // the run whose root the warm state above holds
   int ns_kmax = 12, pcg_kmax = 14;  // iterations launched (device skips past convergence)
   int last_kmax = 12;             // Newton-Schulz iterations the last root launched
+  int retry_kmax = 0;             // floor for warm roots after an advance ran again (same owner)
   bool eig_pending = false;       // a dsyevd ran since the last fr_info
   bool sqrt_pending = false;      // a Newton-Schulz / PCG status to read at fr_info
   bool last_hz = false;           // the last root's schedule had a Z power vector (uZ valid)
@@ -1068,11 +1070,15 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
   // to the run that made it: any other caller's root (another run, a cold
   // log-weight or single-call root) invalidates it
   warm = warm && W->warm && owner != nullptr && W->owner == owner;
+  if (W->owner != owner) W->retry_kmax = 0;
   W->owner = owner;
   // a cold root starts a new problem: forget the iteration counts learnt on the
   // previous one (fr_info learns them again from this run's warm steps)
   if (!warm) {
-    W->ns_kmax = 12;
+    // (VIABEL_AMD_FR_NS_START: test hook -- the count warm roots start from before
+    // fr_info has learnt one, e.g. too few to exercise the advance retry)
+    const char* e = std::getenv("VIABEL_AMD_FR_NS_START");
+    W->ns_kmax = e ? std::max(1, std::atoi(e)) : 12;
     W->pcg_kmax = 14;
   }
   const bool hz = warm && W->have_z && W->Zf;
@@ -1090,12 +1096,17 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
     W->pv_cur = b;
   }
   if (hz) W->zv_init = true;
-  // warm roots launch the learnt count (fr_info) plus two spare iterations (the
-  // count drifts by one as Sigma moves, and a launched-but-skipped iteration
-  // costs only its launch); others at least 12 (l_0 = 0.05 needs ~9 at rounding
-  // level)
+  // warm roots launch exactly the learnt count (fr_info; a step that needs more
+  // sets the sticky status and, inside a run's advance, makes the advance run
+  // again with a larger count -- vb_run_advance keeps a snapshot), others at
+  // least 12 (l_0 = 0.05 needs ~9 at rounding level)
+  static const int spare = [] {   // VIABEL_AMD_FR_NS_SPARE: spare warm iterations (A/B)
+    const char* e = std::getenv("VIABEL_AMD_FR_NS_SPARE");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
   const int kmax =
-      std::min(warm ? std::max(W->ns_kmax + 2, 6) : std::max(W->ns_kmax + 1, 12), kFrNSMax);
+      std::min(warm ? std::max({W->ns_kmax + spare, W->retry_kmax, 3}) : std::max(W->ns_kmax + 1, 12),
+               kFrNSMax);
   W->last_warm = warm;
   W->last_kmax = kmax;
   if (ready)
@@ -1784,7 +1795,7 @@ int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, 
 // since the last call: dsyevd's info, and the sticky Newton-Schulz / PCG status;
 // adapts the iteration counts launched next (one spare Newton-Schulz
 // iteration; PCG: the largest converged count seen, see below).
-int fr_info(FrWork* W, hipStream_t st) {
+int fr_info(FrWork* W, hipStream_t st, bool* retry) {
   int info = 0;
   const bool eig = W->info.p && W->eig_pending, sq = W->sched.p && W->sqrt_pending;
   if (!eig && !sq) return 0;
@@ -1798,9 +1809,19 @@ int fr_info(FrWork* W, hipStream_t st) {
   const FrSched& h = *W->host_sched;
   FrSched* d = static_cast<FrSched*>(W->sched.p);
   FR_HIP(hipMemsetAsync(&d->status, 0, 3 * sizeof(int), st));
-  if ((h.status & 1) || (!h.ns_conv && !h.ns_fin))
+  if ((h.status & 1) || (!h.ns_conv && !h.ns_fin)) {
+    // warm roots launch exactly the learnt count: a step that needed more asks
+    // the caller to run its advance again with a larger count
+    if (retry && W->last_warm && W->last_kmax < kFrNSMax) {
+      *retry = true;
+      W->ns_kmax = std::min(kFrNSMax, W->last_kmax + 3);
+      W->retry_kmax = W->ns_kmax;   // kept through the cold first step of the rerun
+      W->prep_owner = nullptr;
+      return 0;
+    }
     return vb_set_error(-2, "Newton-Schulz square root of Sigma did not converge in %d iterations "
                             "(Sigma too ill-conditioned)", W->last_kmax);
+  }
   if (h.status & 2)
     return vb_set_error(-2, "conjugate gradients for the sqrtm gradient did not converge in %d "
                             "iterations", W->pcg_kmax);

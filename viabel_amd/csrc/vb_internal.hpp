@@ -260,7 +260,9 @@ int mf_wide_log_weights(FrWork* W, const MfSpec& f, const double* lam, long long
                         uint32_t step, double* lw, double* xs, hipStream_t st);
 // 0, or a VB_E* code with the message set (eigendecomposition / Newton-Schulz /
 // PCG failure since the last call); synchronises the stream.
-int fr_info(FrWork* W, hipStream_t st);
+// retry (non-null): a warm Newton-Schulz root that did not converge sets *retry,
+// raises the learnt count and returns 0 (the caller runs the steps again).
+int fr_info(FrWork* W, hipStream_t st, bool* retry = nullptr);
 hipError_t launch_fr_lw(int D, long long m, double df, double t_const, const double* logp,
                         const double* zz, const double* s, const double* scal, double* lw,
                         hipStream_t st);
