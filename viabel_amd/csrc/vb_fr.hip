@@ -1052,12 +1052,15 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
   if (!ready) W->prep_owner = nullptr;   // L, Sigma, the root and uS change below
   if (int rc = reserve_d(W, D, st)) return rc;
   const long long dd = (long long)D * D;
-  const int nblk = ((D + 31) / 32) * ((D + 31) / 32);
+  // every product here is symmetric (polynomials in Sigma): upper-triangle tiles
+  // only (GemmOp::sym), with gemm_parts(D, true) partial sums
+  const int nparts = gemm_parts(D, true);
   FrSched* sc = static_cast<FrSched*>(W->sched.p);
   if (!ready)
     hipLaunchKernelGGL(fr_unpack_kernel, dim3(blocks(dd)), dim3(256), 0, st, D, lam, W->L.d());
   {
     GemmOp g = mm(D, D, D, W->L.d(), false, W->L.d(), true, W->Sig.d());
+    g.sym = 1;
     g.sq_part = W->fro_part.d();
     if (ready) {   // Rayleigh quotient partials of the previous step's Sigma uS
       g.qf_x = W->pS.d();
@@ -1111,16 +1114,17 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
   W->last_kmax = kmax;
   if (ready)
     hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(1024), 0, st, D, kmax, W->fro_part.d(),
-                       4 * nblk, W->pS.d(), W->pz.d(), 1, 0.05, sc, lam, W->scal.d(),
+                       nparts, W->pS.d(), W->pz.d(), 1, 0.05, sc, lam, W->scal.d(),
                        W->ypart.d(), W->uS.d(), W->uZ.d());
   else
     hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(1024), 0, st, D, kmax, W->fro_part.d(),
-                       4 * nblk, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), hz ? 1 : 0, 0.05,
+                       nparts, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), hz ? 1 : 0, 0.05,
                        sc, lam, W->scal.d(), nullptr, W->uS.d(), W->uZ.d());
   W->last_hz = ready || hz;
   // iteration 0: Y_1 -> Yb[1], Z_1 -> Zb[1]
   {
     GemmOp g = mm(D, D, D, W->Sig.d(), false, W->Sig.d(), false, W->Yb[1].d());
+    g.sym = 1;
     g.ns0 = sc->ns0;
     g.ns0_z = W->Zb[1].d();
     FR_HIP(gemm(g, st));
@@ -1129,6 +1133,7 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
     const double *Yk = W->Yb[k & 1].d(), *Zk = W->Zb[k & 1].d();
     double* tp = W->tpart[k & 1].d();
     GemmOp t = mm(D, D, D, Zk, false, Yk, false, W->T.d());
+    t.sym = 1;
     t.alpha_dev = &sc->nalpha2[k];
     t.diag = 3.0;
     t.sq_part = tp;
@@ -1141,6 +1146,7 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
                     mm(D, D, D, W->T.d(), false, Zk, false, W->Zb[(k + 1) & 1].d())};
     for (int o = 0; o < 2; ++o) {
       GemmOp& g = yz[o];
+      g.sym = 1;
       g.alpha_dev = &sc->halpha[k];
       g.skip_flag = &sc->ns_conv;
       g.skip_tag = 2 * k + 2;
@@ -1149,7 +1155,7 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
       g.copy_src = ((k & 1) != ((kmax + 1) & 1)) ? (o == 0 ? Yk : Zk) : nullptr;
       g.copy_if_iter = k;
       g.conv_part = tp;
-      g.conv_n = 4 * nblk;
+      g.conv_n = nparts;
       g.conv_scale_dev = &sc->inv_a4[k];
       g.conv_tol2 = 1e-20 * D;
       // ||I - Z_k Y_k||_F <= tau: the residual after this update is at most

@@ -18,6 +18,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 namespace vbk {
 
 struct GemmOp {
@@ -102,6 +104,12 @@ struct GemmOp {
   // the written tile), 4 per block at qf_part[4 (by gridDim.x + bx) + wave]
   const double* qf_x;
   double* qf_part;
+  // symmetric result (M == N, the caller's guarantee that C is symmetric in exact
+  // arithmetic): only the tiles (bi <= bj) of the upper triangle are computed, one
+  // block each, and every off-diagonal tile is also stored transposed into
+  // (bj, bi); partial sums (sq_part, qf_part, dot_part) weight off-diagonal tiles
+  // twice and are indexed by the triangular block index (4 nt (nt + 1) / 2 in all)
+  int sym;
   // set by gemm_group: M, N multiples of 32, K of KTG, 16-byte aligned operand rows, no
   // kscale / dual product -> the LDS-DMA main loop
   int glds;
@@ -408,11 +416,22 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
   __syncthreads();
 }
 
-// One BT x BT output tile (bx, by) of g (the whole block, NTH threads).  ntx =
-// tiles per row (partial-sum index).  sA / sB: the block's LDS operand buffers.
+// One BT x BT output tile (bx, by) of g (the whole block, NTH threads).  slot =
+// the block's partial-sum index.  sA / sB: the block's LDS operand buffers.
 // Ends with a barrier, so a caller may run further tiles on the same buffers.
+// Upper-triangle tile (bi <= bj) of triangular block index b (row-major over bi).
+__device__ __forceinline__ void tri_tile(int b, int nt, int& bi, int& bj) {
+  int i = 0;
+  while (b >= nt - i) {
+    b -= nt - i;
+    ++i;
+  }
+  bi = i;
+  bj = i + b;
+}
+
 template <bool TA, bool TB, bool KS, bool DUAL>
-__device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int ntx,
+__device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int slot,
                                           double (*sA)[BUF], double (*sB)[BUF], double* lds) {
   // A is k-contiguous when not transposed; B is k-contiguous when transposed.
   constexpr bool AK = !TA, BK = TB;
@@ -524,6 +543,7 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
     }
     const int col = j0 + wn * 16 + (lane & 15);
     double sq = 0.0, dt = 0.0, qf = 0.0, rp[4] = {0.0, 0.0, 0.0, 0.0};
+    const bool mirror = g.sym && bx != by;   // also store the tile transposed
     const double rpx = (g.rp_x && col < g.N) ? g.rp_x[col] : 0.0;
     const double qfx = (g.qf_x && col < g.N) ? g.qf_x[col] : 0.0;
     const double alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
@@ -548,24 +568,29 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int n
         if (g.rp_w) rp[r] = v * g.rp_w[(long long)row * g.ldc + col];
         if (g.beta != 0.0) v += g.beta * *c;
         *c = v;
+        if (mirror) {
+          g.C[(long long)col * g.ldc + row] = v;
+          if (g.ns0) g.ns0_z[(long long)col * g.ldc + row] = g.ns0_z[(long long)row * g.ldc + col];
+        }
         const double e = row == col ? v - shift : v;
         sq += e * e;
       }
     }
+    const double pw = mirror ? 2.0 : 1.0;   // the transposed tile's share of a sum
     if (g.sq_part) {
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off, 64);
-      if (lane == 0) g.sq_part[4 * (by * ntx + bx) + q] = sq;
+      if (lane == 0) g.sq_part[4 * slot + q] = pw * sq;
     }
     if (g.dot_part) {
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) dt += __shfl_xor(dt, off, 64);
-      if (lane == 0) g.dot_part[4 * (by * ntx + bx) + q] = dt;
+      if (lane == 0) g.dot_part[4 * slot + q] = pw * dt;
     }
     if (g.qf_part) {
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) qf += __shfl_xor(qf, off, 64);
-      if (lane == 0) g.qf_part[4 * (by * ntx + bx) + q] = qf;
+      if (lane == 0) g.qf_part[4 * slot + q] = pw * qf;
     }
     if (g.rp_part) {
       // sum over the 16 lanes of a row (lanes 16 kq .. 16 kq + 15 hold row kq + 4 r)
@@ -587,6 +612,11 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   __shared__ __attribute__((aligned(16))) double smem[SMEM];
   double(*sA)[BUF] = reinterpret_cast<double(*)[BUF]>(smem);
   double(*sB)[BUF] = reinterpret_cast<double(*)[BUF]>(smem + 2 * BUF);
+  int bx = blockIdx.x, by = blockIdx.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
+  if (g.sym) {
+    tri_tile(blockIdx.x, (g.N + BT - 1) / BT, by, bx);
+    slot = blockIdx.x;
+  }
   if (const int sk = gemm_skip(g, sB[1])) {
     // the copy decision uses this block's own test (sk == 2) or state written
     // by earlier launches (sk == 1), never a peer block's stores in this launch
@@ -599,14 +629,17 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
     }
     if (first) {
       for (int e = threadIdx.x; e < BT * BT; e += NTH) {
-        const int row = blockIdx.y * BT + e / BT, col = blockIdx.x * BT + e % BT;
-        if (row < g.M && col < g.N)
+        const int row = by * BT + e / BT, col = bx * BT + e % BT;
+        if (row < g.M && col < g.N) {
           g.C[(long long)row * g.ldc + col] = g.copy_src[(long long)row * g.ldc + col];
+          if (g.sym && bx != by)
+            g.C[(long long)col * g.ldc + row] = g.copy_src[(long long)col * g.ldc + row];
+        }
       }
     }
     return;
   }
-  gemm_tile<TA, TB, KS, DUAL>(g, blockIdx.x, blockIdx.y, gridDim.x, sA, sB, smem);
+  gemm_tile<TA, TB, KS, DUAL>(g, bx, by, slot, sA, sB, smem);
 }
 
 }  // namespace gemm_detail
@@ -626,19 +659,39 @@ inline bool glds_ok(const GemmOp& o) {
 #endif
 }
 
+// VIABEL_AMD_GEMM_SYM=0: symmetric results computed in full (A/B switch); callers
+// size their partial-sum reductions with gemm_parts
+inline bool gemm_sym_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("VIABEL_AMD_GEMM_SYM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// number of 4-per-block partial sums of an n x n result (sym: upper triangle)
+inline int gemm_parts(int n, bool sym) {
+  const int t = (n + gemm_detail::BT - 1) / gemm_detail::BT;
+  return 4 * ((sym && gemm_sym_enabled()) ? t * (t + 1) / 2 : t * t);
+}
+
 // Launch n (1 or 2) GEMMs of equal shape and transposes; dual products (A2/B2)
 // must not use kscale.
 inline hipError_t gemm_group(const GemmOp* ops, int n, hipStream_t s) {
   using namespace gemm_detail;
   const GemmOp& g = ops[0];
   if (g.M <= 0 || g.N <= 0 || n < 1 || n > 2) return n < 1 ? hipSuccess : hipErrorInvalidValue;
+  const bool sym_on = gemm_sym_enabled();
   GemmGroup gg{};
   for (int i = 0; i < n; ++i) {
     gg.op[i] = ops[i];
     const GemmOp& o = ops[i];
     gg.op[i].glds = glds_ok(o) ? 1 : 0;
+    if (!sym_on) gg.op[i].sym = 0;
   }
-  const dim3 grid((unsigned)((g.N + BT - 1) / BT), (unsigned)((g.M + BT - 1) / BT), (unsigned)n);
+  if (gg.op[0].sym && g.M != g.N) return hipErrorInvalidValue;
+  const unsigned ntn = (unsigned)((g.N + BT - 1) / BT);
+  const dim3 grid = gg.op[0].sym ? dim3(ntn * (ntn + 1) / 2, 1, (unsigned)n)
+                          : dim3(ntn, (unsigned)((g.M + BT - 1) / BT), (unsigned)n);
   const bool ks = g.kscale != nullptr, dual = g.A2 != nullptr;
   if (ks && dual) return hipErrorInvalidValue;
 #define VB_GEMM(TA, TB)                                                                 \
