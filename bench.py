@@ -342,8 +342,9 @@ def leg_cfg1(cpu):
     out = {'config': 1, 'workload': 'mixture D=2 mf-Gauss KLVI N=100, 5000 iters (adagrad_optimize '
                                    'incl. result copy)', 'ms_per_step': dt * 1e3,
            'steps_per_s': 1 / dt, 'value': n * Dm / dt, 'unit': 'MC-samples/s',
-           'roofline': {'bound': 'latency', 'note': 'one 256-thread workgroup per problem; '
-                        'D=2 moves 64 B of parameters per step'}}
+           'roofline': latency_roofline(dt, Dm, n, chivi=False, host_layout=False, n_problems=1,
+                                        note='one workgroup per problem; D=2 moves 64 B of '
+                                             'parameters per step')}
     if cpu:
         from oracle import vb_oracle
         ofam = vb_oracle.Family('gauss', Dm)
@@ -377,8 +378,10 @@ def leg_cfg2(cpu):
     dt = (time.perf_counter() - t0) / iters
     out = {'config': 2, 'workload': 'funnel D=10 mf-t(40) CHIVI a=2 N=128, 10000 iters',
            'ms_per_step': dt * 1e3, 'value': n * Dm / dt, 'unit': 'MC-samples/s',
-           'roofline': {'bound': 'latency', 'note': 'one workgroup; draw waves (normal + '
-                        'Marsaglia-Tsang gamma per item) are the critical path'}}
+           'roofline': latency_roofline(dt, Dm, n, chivi=True, host_layout=True, n_problems=1,
+                                        note='one workgroup; t draws pre-drawn chunk by chunk '
+                                             'over the chip (pre-draw kernels inside the timed '
+                                             'run), the block consumes them')}
     if cpu:
         from oracle import vb_oracle
         ofam = vb_oracle.Family('t', Dm, 40.0)
@@ -394,6 +397,21 @@ def leg_cfg2(cpu):
                                'sample': 'median of 5 x 400 oracle adagrad steps'}
         out['speedup_vs_cpu'] = _median(ts) / dt
     return out
+
+
+def latency_roofline(step_s, d, n, chivi, host_layout, n_problems, note):
+    """Roofline of a latency-bound block-kernel leg: the measured floor of its step
+    skeleton (vb_block_floor: the same block shape, barriers, reductions and
+    adagrad update, no draws and no target, on the same grid) against the
+    achieved time per step; frac = floor / achieved."""
+    from viabel_amd import _native as nat
+    fl = min(nat.block_floor_us(d, n, chivi=chivi, host_layout=host_layout, n_steps=2000,
+                                n_problems=n_problems) for _ in range(3))
+    us = step_s * 1e6
+    return {'bound': 'latency', 'floor_us': fl, 'achieved_us': us, 'unit': 'us/step',
+            'achieved_over_floor': us / fl, 'frac': fl / us,
+            'floor_source': 'vb_block_floor, best of 3 x 2000 steps',
+            'note': note}
 
 
 def _cfg4_problem():
@@ -545,7 +563,13 @@ def leg_cfg5(cpu, host, rank, world, n_restarts=64, iters=5000, M=1_000_000):
                         'achieved': ach, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                         'frac': ach / HBM_PEAK_GBS if ach else None,
                         'algorithmic_bytes_per_rank': b_stage,
-                        'note': 'fitting is latency-bound (one workgroup per restart)'}}
+                        'note': 'fitting is latency-bound (one workgroup per restart): fit_roofline'},
+           'fit_roofline': (latency_roofline(tm['fit_s'] / iters, 10, 100, chivi=False,
+                                             host_layout=True, n_problems=local,
+                                             note='one workgroup per restart, %d restarts on this '
+                                                  'rank; the fit (pre-draw + block kernels) per '
+                                                  'step' % local)
+                            if tm.get('fit_s') else None)}
     if cpu:
         t0 = time.perf_counter()
         _cfg5_cpu_restart(0, iters, M)

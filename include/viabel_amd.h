@@ -224,6 +224,14 @@ int vb_run_steps_done(vb_run* run, int64_t* out);
 int vb_run_set_timing(vb_run* run, int enable);
 int vb_run_launch_times(vb_run* run, int64_t max, int64_t* steps_out, float* ms_out,
                         int64_t* n_out);
+/* Latency floor of the block-per-problem step (measurement support, no reference
+ * counterpart): runs n_steps of the block kernel's step skeleton -- the same
+ * block shape for (D <= 16, N, objective; host_layout != 0: the device-noise /
+ * pre-drawn layout of row waves only), barriers, reductions and adagrad update,
+ * but no draws and no target -- on n_problems blocks, and returns the device
+ * microseconds per step (HIP events on the context's stream). */
+int vb_block_floor(vb_ctx* ctx, int32_t D, int32_t N, int32_t chivi, int32_t host_layout,
+                   int64_t n_steps, int64_t n_problems, double* us_per_step);
 /* Results (all nullable): lam_out [n_problems][P]; hist_out
  * [n_problems][n_hist][P] (n_hist per vb_adagrad_config); values_out [n_problems][n_iters];
  * smoothed_out [n_problems][P] = mean of the history rows (vb.py:386-387). */

@@ -198,3 +198,28 @@ def test_config5_full_size_records():
         # elbo, d2, W1, W2, mean/std/cov error, k-hat
         np.testing.assert_allclose(got[1:9], expect[1:9], rtol=1e-6, atol=1e-9,
                                    err_msg='restart %d' % r)
+
+
+@pytest.mark.parametrize('D,N,chivi,host_layout', [(2, 100, False, False), (10, 128, True, True),
+                                                   (10, 100, False, True)])
+def test_block_floor_bounds_the_block_step(D, N, chivi, host_layout):
+    """vb_block_floor (the block step's skeleton without draws or target) is a
+    positive time per step below the block kernel's own step at that shape."""
+    import time
+    from viabel_amd import vb, targets, _native as nat
+    nat.block_floor_us(D, N, chivi=chivi, host_layout=host_layout, n_steps=10)   # code load
+    fl = min(nat.block_floor_us(D, N, chivi=chivi, host_layout=host_layout, n_steps=500)
+             for _ in range(3))
+    assert 0.0 < fl < 50.0
+    fam = (vb.mean_field_t_variational_family(D, 40.0, rng='philox') if host_layout
+           else vb.mean_field_gaussian_variational_family(D, rng='philox'))
+    tgt = targets.funnel(D) if D > 2 else targets.mixture(D)
+    obj = vb.black_box_chivi(2.0, fam, tgt, N) if chivi else vb.black_box_klvi(fam, tgt, N)
+    run = vb.DeviceRun(obj, 2200, np.zeros(2 * D)[None, :])
+    run.advance_philox(200, 0, 1, 0)
+    nat.context().synchronize()
+    t0 = time.perf_counter()
+    run.advance_philox(2000, 0, 1, 200)
+    nat.context().synchronize()
+    us = (time.perf_counter() - t0) / 2000 * 1e6
+    assert fl < us, (fl, us)

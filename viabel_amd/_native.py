@@ -85,6 +85,8 @@ _SIGNATURES = {
     'vb_run_set_timing': ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     'vb_run_launch_times': ([ctypes.c_void_p, ctypes.c_int64, c_int64_p,
                              P(ctypes.c_float), c_int64_p], ctypes.c_int),
+    'vb_block_floor': ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                        ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, c_double_p], ctypes.c_int),
     'vb_run_result': ([ctypes.c_void_p, c_double_p, c_double_p, c_double_p, c_double_p],
                       ctypes.c_int),
     'vb_run_destroy': ([ctypes.c_void_p], ctypes.c_int),
@@ -299,3 +301,14 @@ def use_stream(device, stream_handle):
     _ctx[int(device)] = c
     _default_device[0] = int(device)
     return c
+
+
+def block_floor_us(D, N, chivi=False, host_layout=False, n_steps=2000, n_problems=1):
+    """Device microseconds per step of the block kernel's step skeleton (same
+    block shape, barriers, reductions and adagrad update; no draws, no target):
+    the latency floor of configs 1, 2 and 5's fit (vb_block_floor)."""
+    out = ctypes.c_double()
+    check(lib().vb_block_floor(context().handle, int(D), int(N), 1 if chivi else 0,
+                               1 if host_layout else 0, int(n_steps), int(n_problems),
+                               ctypes.byref(out)))
+    return out.value

@@ -1124,6 +1124,30 @@ int vb_run_launch_times(vb_run* r, int64_t max, int64_t* steps_out, float* ms_ou
   return VB_OK;
 }
 
+int vb_block_floor(vb_ctx* c, int32_t D, int32_t N, int32_t chivi, int32_t host_layout,
+                   int64_t n_steps, int64_t n_problems, double* us_per_step) {
+  VB_TRY(check_ctx(c));
+  if (!us_per_step) return fail(VB_EINVAL, "null output pointer");
+  if (D < 1 || D > vbk::kBlockDMax || N < 1 || n_steps < 1 || n_problems < 1 || n_problems > 65535)
+    return fail(VB_EINVAL, "vb_block_floor: D in [1, %d], N >= 1, n_steps >= 1", vbk::kBlockDMax);
+  DevBuf out;
+  VB_TRY(out.reserve(sizeof(double) * n_problems));
+  hipEvent_t e0, e1;
+  VB_HIP(hipEventCreate(&e0));
+  VB_HIP(hipEventCreate(&e1));
+  VB_HIP(hipEventRecord(e0, c->stream));
+  VB_HIP(vbk::launch_block_floor(D, N, host_layout != 0, chivi != 0, (int)n_steps,
+                                 (int)n_problems, out.d(), c->stream));
+  VB_HIP(hipEventRecord(e1, c->stream));
+  VB_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  VB_HIP(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  *us_per_step = (double)ms * 1e3 / (double)n_steps;
+  return VB_OK;
+}
+
 int vb_run_steps_done(vb_run* r, int64_t* out) {
   if (!r || !out) return fail(VB_EINVAL, "null argument");
   *out = r->done;

@@ -69,6 +69,9 @@ struct BlockArgs {
 
 // family kind 0 = mf gaussian, 1 = mf t; target kind per vb_target_kind.
 hipError_t launch_sep(int fam, int tgt, bool host_noise, const SepArgs& a, hipStream_t s);
+// block step skeleton without draws / target (vb_block_floor)
+hipError_t launch_block_floor(int D, int N, bool host_layout, bool chivi, int n_steps, int nprob,
+                              double* out, hipStream_t s);
 hipError_t launch_block(int fam, int tgt, bool host_noise, const BlockArgs& a, int n_problems,
                         hipStream_t s);
 bool target_separable(int tgt);

@@ -926,6 +926,99 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   }
 }
 
+// Latency floor of the block kernel's step (measurement only, vb_block_floor):
+// the same block shape, barriers, reductions and adagrad update as block_kernel,
+// with no draws and no target -- every row thread's accumulators are a cheap
+// function of the current parameters (so each step still depends on the last
+// update).  Its time per step bounds what any block_kernel step can reach.
+template <int DMAX>
+__global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, int N, int NT_rows,
+                                                                     int chivi, int n_steps,
+                                                                     int W, double* out) {
+  constexpr int K = 2 * DMAX + 2;
+  __shared__ double s_lam[2 * DMAX];
+  __shared__ double s_sg[DMAX];
+  __shared__ double s_ring[64 * 2 * DMAX];
+  __shared__ double s_red[kBlockMaxRowWaves][K];
+  __shared__ double s_max[kBlockMaxRowWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int NT = blockDim.x, P = 2 * D, RW = NT_rows / 64;
+  const bool row_wave = wid < RW;
+  const double dN = (double)N;
+  for (int p = tid; p < P; p += NT) s_lam[p] = 0.01 * p;
+  for (int q = tid; q < W * P; q += NT) s_ring[q] = 0.0;
+  for (int d = tid; d < D; d += NT) s_sg[d] = 1.0;
+  __syncthreads();
+  int slot = 0;
+  double val = 0.0;
+  for (int s = 0; s < n_steps; ++s) {
+    double sl = 0.0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) sl += d < D ? s_lam[D + d] : 0.0;
+    double acc[K];
+    const double t = (double)(tid + 1) * 1e-3;
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = (tid < N) ? t * s_lam[k % P] : 0.0;
+    double M = 0.0;
+    if (chivi) {
+      if (row_wave) {
+        const double wm = wave_max_dpp(tid < N ? t + sl : -INFINITY);
+        if (lane == 0) s_max[wid] = wm;
+      }
+      __syncthreads();
+      M = s_max[0];
+      for (int q = 1; q < RW; ++q) M = fmax(M, s_max[q]);
+    }
+    if (row_wave) wave_reduce_scatter<K>(acc, s_red[wid]);
+    __syncthreads();
+    if (tid < K) {
+      double u = s_red[0][tid];
+      for (int q = 1; q < RW; ++q) u += s_red[q][tid];
+      s_red[0][tid] = u;
+    }
+    __syncthreads();
+    if (tid < P) {
+      const int p = tid;
+      const double gp = p < D ? -(s_red[0][p] / dN)
+                              : -(1.0 + s_sg[p - D] * (s_red[0][DMAX + (p - D)] / dN));
+      s_ring[slot * P + p] = gp;
+      const int cnt = (s + 1 < W) ? s + 1 : W;
+      const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;
+      double q = 0.0;
+      for (int k = 0; k < cnt; ++k) {
+        int Lk = oldest + k;
+        if (Lk >= W) Lk -= W;
+        const double v = s_ring[Lk * P + p];
+        q = __dadd_rn(q, __dmul_rn(v, v));
+      }
+      const double nl = __dsub_rn(s_lam[p], __dmul_rn(1e-6, gp) / sqrt(__dadd_rn(0.1, q)));
+      s_lam[p] = nl;
+      if (p >= D) s_sg[p - D] = exp(nl);
+    }
+    if (tid == (NT > 64 ? NT - 64 : 0)) val += chivi ? log(s_red[0][2 * DMAX] / dN) + M : s_red[0][2 * DMAX];
+    slot = slot + 1 == W ? 0 : slot + 1;
+    __syncthreads();
+  }
+  if (tid == (NT > 64 ? NT - 64 : 0)) out[blockIdx.x] = val;
+}
+
+hipError_t launch_block_floor(int D, int N, bool host_layout, bool chivi, int n_steps, int nprob,
+                              double* out, hipStream_t s) {
+  if (D < 1 || D > kBlockDMax || N < 1 || n_steps < 0 || nprob < 1) return hipErrorInvalidValue;
+  const BlockLayout L = block_layout(N, D, host_layout, chivi);
+  const dim3 grid(nprob), block(L.nt);
+  const int rows = 64 * L.rw, W = 10;
+  if (D <= 2)
+    hipLaunchKernelGGL((block_floor_kernel<2>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out);
+  else if (D <= 4)
+    hipLaunchKernelGGL((block_floor_kernel<4>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out);
+  else if (D <= 10)
+    hipLaunchKernelGGL((block_floor_kernel<10>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out);
+  else
+    hipLaunchKernelGGL((block_floor_kernel<kBlockDMax>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out);
+  return hipGetLastError();
+}
+
 // Pre-drawn noise for the block kernel's device-noise path (launch_block_predraw):
 // one thread per (problem, step, sample) walks the sample's column pairs with the
 // draw items' counters, transforms and log q partials (block_kernel's draw_item),
