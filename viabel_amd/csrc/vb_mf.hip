@@ -1352,6 +1352,21 @@ __device__ __forceinline__ void draw_pair(const Rng& rng, const double* noise, i
   }
 }
 
+// logq1 with sigma = exp(ls) given (the same bits)
+template <bool TFAM, bool HOST>
+__device__ __forceinline__ double logq1s(double x, double mu, double ls, double sg, double df,
+                                         double t_const, const double2* lt) {
+  const double z = (x - mu) / sg;
+  if constexpr (TFAM) {
+    const double y = z * z / df;
+    double l1;
+    if constexpr (HOST) l1 = log1p(y);
+    else l1 = log1p_pos_tab(y, lt);
+    return t_const - l1 * (0.5 * (df + 1.0)) - ls;
+  }
+  return -0.5 * z * z - ls - 0.5 * kLog2Pi;
+}
+
 template <bool TFAM, bool HOST>
 __device__ __forceinline__ double logq1(double x, double mu, double ls, double df,
                                         double t_const, const double2* lt) {
@@ -1420,10 +1435,7 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
                                                        double* xs) {
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
-  if constexpr (!HOST) {
-    load_bm_tables(s_sct, s_lt);
-    __syncthreads();
-  }
+  __shared__ double s_mu[DMAX], s_ls[DMAX], s_sg[DMAX];
   // row q of a batched launch (vb_log_weights_rows): its own lambda, output
   // row, noise rows and Philox stream (stream + q * stride)
   const int q = blockIdx.y;
@@ -1432,12 +1444,22 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
   if (xs) xs += (long long)q * m * D;
   if (noise) noise += (long long)q * m * D;
   rng.stream += (uint32_t)q * stride;
+  // the block's lambda row and sigma = exp(log sigma) once per block (the same
+  // bits as per draw), with the Box-Muller tables
+  if ((int)threadIdx.x < D) {
+    const double ls = lam[D + threadIdx.x];
+    s_mu[threadIdx.x] = lam[threadIdx.x];
+    s_ls[threadIdx.x] = ls;
+    s_sg[threadIdx.x] = exp(ls);
+  }
+  if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
+  __syncthreads();
   const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
   if (r >= m) return;
   double x[DMAX], g[DMAX];
   double lq = 0.0;
 #pragma unroll
-  for (int j = 0; j < DMAX / 2; ++j) {
+  for (int j = 0; j < (DMAX + 1) / 2; ++j) {
     double e0 = 0.0, e1 = 0.0;
     if (2 * j < D)
       draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e0, e1, s_sct, s_lt);
@@ -1445,12 +1467,13 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int d = 2 * j + c;
+      if (d >= DMAX) continue;
       x[d] = 0.0;
       g[d] = 0.0;
       if (d < D) {
-        const double mu = lam[d], ls = lam[D + d];
-        x[d] = e[c] * exp(ls) + mu;
-        lq += logq1<TFAM, HOST>(x[d], mu, ls, df, t_const, s_lt);
+        const double mu = s_mu[d], sg = s_sg[d];
+        x[d] = e[c] * sg + mu;
+        lq += logq1s<TFAM, HOST>(x[d], mu, s_ls[d], sg, df, t_const, s_lt);
         if (xs) xs[r * D + d] = x[d];
       }
     }
@@ -1886,9 +1909,16 @@ static void logw_launch(int D, long long m, const double* lam, double t_scale, d
     }
   }
   {
-    hipLaunchKernelGGL((logw_row_kernel<TGT, TFAM, HOST, kBlockDMax>),
-                       dim3((unsigned)((m + 255) / 256), (unsigned)rows), dim3(256), 0, s, D, m,
-                       lam, t_scale, shape, df, t_const, noise, rng, step, stride, lw, xs);
+    // register arrays sized by the smallest instance >= D (as block_dispatch)
+    const dim3 g((unsigned)((m + 255) / 256), (unsigned)rows);
+#define VB_LOGW(DM)                                                                            \
+  hipLaunchKernelGGL((logw_row_kernel<TGT, TFAM, HOST, DM>), g, dim3(256), 0, s, D, m, lam,   \
+                     t_scale, shape, df, t_const, noise, rng, step, stride, lw, xs)
+    if (D <= 2) VB_LOGW(2);
+    else if (D <= 4) VB_LOGW(4);
+    else if (D <= 10) VB_LOGW(10);
+    else VB_LOGW(kBlockDMax);
+#undef VB_LOGW
   }
 }
 
