@@ -532,7 +532,9 @@ def leg_cfg5(cpu, host, rank, world, n_restarts=64, iters=5000, M=1_000_000):
     from viabel_amd import vb, targets, restarts
     fac = lambda: vb.mean_field_t_variational_family(10, 40.0, rng='philox')
     tgt = targets.eight_schools_ncp()
-    restarts.run_restarts(fac, tgt, world, 20, n_bounds=1000)      # warm-up (code objects)
+    # warm-up: code objects, and the same [restarts][M] buffer shapes for the
+    # device allocator (a 20-iteration fit)
+    restarts.run_restarts(fac, tgt, n_restarts, 20, n_bounds=M)
     _sync()
     dist = torch.distributed if world > 1 else None
     if dist:

@@ -319,8 +319,9 @@ int vb_weighted_covariance_logw(vb_ctx* ctx, const double* x, int64_t n, int64_t
                                 double* cov_out);
 
 /* ---- PSIS (psis.py:112-395) ------------------------------------------ */
-/* lw [n, m] C order (m columns of n log weights).  lw_out same layout.
- * k_out [m].  tail_idx_out (nullable) [m, tail_cap]: the tail indices in
+/* lw [n, m] C order (m columns of n log weights).  lw_out same layout, or null
+ * for k (and the tails) only: the smoothing and renormalisation, which feed only
+ * lw_out, are skipped.  k_out [m].  tail_idx_out (nullable) [m, tail_cap]: the tail indices in
  * ascending order of the tail values (tailinds[x2si]); n_tail_out (nullable) [m]. */
 int vb_psislw(vb_ctx* ctx, const double* lw, int64_t n, int64_t m, double reff,
               double* lw_out, double* k_out, int64_t* tail_idx_out,

@@ -417,3 +417,24 @@ def test_divergence_rows_matches_per_row(device):
             assert res.keys() == ref.keys()
             for k in ref:
                 assert res[k] == ref[k], k
+
+
+@pytest.mark.parametrize('layout', ['1d', 'c', 'f', 'device_t'])
+def test_psis_khat_equals_psislw_k(layout):
+    """psis_khat (vb_psislw with a null lw_out: the pipeline stops after the GPD
+    fit, the shift applied on the fly) gives psislw's k bit for bit."""
+    import torch
+    from viabel_amd import psis
+    rs = np.random.RandomState(5)
+    lw = rs.standard_t(3, size=(20000, 4))
+    if layout == '1d':
+        x = lw[:, 0].copy()
+    elif layout == 'c':
+        x = np.ascontiguousarray(lw)
+    elif layout == 'f':
+        x = np.asfortranarray(lw)
+    else:
+        x = torch.tensor(lw.T.copy(), dtype=torch.float64, device='cuda').t()
+    k_full = psis.psislw(x)[1]
+    k_only = psis.psis_khat(x)
+    np.testing.assert_array_equal(np.atleast_1d(k_only), np.atleast_1d(k_full))

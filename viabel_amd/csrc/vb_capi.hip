@@ -1506,7 +1506,8 @@ static int psislw_impl(vb_ctx* c, const double* lw, int64_t n, int64_t m, long l
   VB_TRY(dnt.stage(c, 5, reinterpret_cast<long long*>(n_tail_out), n_tail_out ? (size_t)m : 0));
   for (int64_t c0 = 0; c0 < m; c0 += group) {
     const int g = (int)std::min<int64_t>(group, m - c0);
-    VB_HIP(vbk::psis_columns(dlw.d + c0 * cs, dout.d + c0 * cs, n, g, rs, cs, Mt, c->slot[3].p,
+    VB_HIP(vbk::psis_columns(dlw.d + c0 * cs, dout.d ? dout.d + c0 * cs : nullptr, n, g, rs, cs,
+                             Mt, c->slot[3].p,
                              dk.d + c0, dti.d ? dti.d + (size_t)c0 * tail_cap : nullptr,
                              (long long)tail_cap, dnt.d ? dnt.d + c0 : nullptr, c->stream));
   }
@@ -1520,7 +1521,7 @@ static int psislw_impl(vb_ctx* c, const double* lw, int64_t n, int64_t m, long l
 int vb_psislw(vb_ctx* c, const double* lw, int64_t n, int64_t m, double reff, double* lw_out,
               double* k_out, int64_t* tail_idx_out, int64_t tail_cap, int64_t* n_tail_out) {
   VB_TRY(check_ctx(c));
-  if (!lw || !lw_out || !k_out || m < 1) return fail(VB_EINVAL, "invalid argument");
+  if (!lw || !k_out || m < 1) return fail(VB_EINVAL, "invalid argument");
   if (n <= 1) return fail(VB_EINVAL, "More than one log-weight needed.");  // psis.py:143-144
   const long long Mt = psis_tail_len(n, reff);
   if (Mt > vbk::psis_tail_max())
@@ -1535,7 +1536,7 @@ int vb_psislw_colmajor(vb_ctx* c, const double* lw, int64_t n, int64_t m, double
                        double* lw_out, double* k_out, int64_t* tail_idx_out, int64_t tail_cap,
                        int64_t* n_tail_out) {
   VB_TRY(check_ctx(c));
-  if (!lw || !lw_out || !k_out || m < 1) return fail(VB_EINVAL, "invalid argument");
+  if (!lw || !k_out || m < 1) return fail(VB_EINVAL, "invalid argument");
   if (n <= 1) return fail(VB_EINVAL, "More than one log-weight needed.");  // psis.py:143-144
   const long long Mt = psis_tail_len(n, reff);
   if (Mt > vbk::psis_tail_max())

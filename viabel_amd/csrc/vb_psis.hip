@@ -194,16 +194,21 @@ __global__ __launch_bounds__(256) void shift_kernel(const double* lw, double* ou
     out[i * rs] = lw[i * rs] - mx;
 }
 
+// x: the shifted copy lw - max (unshifted = 0), or lw itself with the shift
+// applied here (unshifted = 1; the same bits: one subtraction either way)
 __global__ __launch_bounds__(256) void tail_count_kernel(const double* x, long long n,
                                                          long long rs, long long cs,
                                                          long long chunk, const PsisState* ps,
-                                                         unsigned* cnt, long long sb) {
+                                                         unsigned* cnt, long long sb,
+                                                         int unshifted) {
   __shared__ unsigned wc[4];
   const double xc = colp(ps, sb)->xcut;
+  const double mx = unshifted ? colp(ps, sb)->mx : 0.0;
   x += (long long)blockIdx.y * cs;
   const long long r0 = (long long)blockIdx.x * chunk, r1 = min(n, r0 + chunk);
   unsigned c = 0;
-  for (long long i = r0 + threadIdx.x; i < r1; i += 256) c += (x[i * rs] > xc) ? 1u : 0u;
+  for (long long i = r0 + threadIdx.x; i < r1; i += 256)
+    c += ((unshifted ? x[i * rs] - mx : x[i * rs]) > xc) ? 1u : 0u;
   // wave + block sum of integers
   for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
   if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
@@ -228,9 +233,10 @@ __global__ __launch_bounds__(256) void tail_compact_kernel(const double* x, long
                                                            long long chunk, const PsisState* ps,
                                                            const unsigned* off, long long cap,
                                                            double* tv, long long* ti,
-                                                           long long sb) {
+                                                           long long sb, int unshifted) {
   __shared__ unsigned wtot[4];
   const double xc = colp(ps, sb)->xcut;
+  const double mx = unshifted ? colp(ps, sb)->mx : 0.0;
   x += (long long)blockIdx.y * cs;
   tv = colp(tv, sb);
   ti = colp(ti, sb);
@@ -242,7 +248,7 @@ __global__ __launch_bounds__(256) void tail_compact_kernel(const double* x, long
     double v = 0.0;
     bool f = false;
     if (i < r1) {
-      v = x[i * rs];
+      v = unshifted ? x[i * rs] - mx : x[i * rs];
       f = v > xc;
     }
     const unsigned long long bal = __ballot(f);
@@ -697,15 +703,20 @@ hipError_t psis_columns(const double* lw, double* out, long long n, int m, long 
   // 3. shifted copy + stable tail compaction
   const long long chunk = ((n + g - 1) / g + 255) / 256 * 256;
   const int gc = (int)((n + chunk - 1) / chunk);
-  hipLaunchKernelGGL(shift_kernel, dim3(g, m), dim3(256), 0, s, lw, out, n, rs, cs, S.ps, sb);
-  hipLaunchKernelGGL(tail_count_kernel, dim3(gc, m), dim3(256), 0, s, out, n, rs, cs, chunk, S.ps,
-                     S.cnt, sb);
+  // (out null: k and the tails only -- the shift is applied on the fly and the
+  // smoothing / renormalisation below, which only feed out, are skipped)
+  const int unshifted = out ? 0 : 1;
+  const double* sx = out ? out : lw;
+  if (out)
+    hipLaunchKernelGGL(shift_kernel, dim3(g, m), dim3(256), 0, s, lw, out, n, rs, cs, S.ps, sb);
+  hipLaunchKernelGGL(tail_count_kernel, dim3(gc, m), dim3(256), 0, s, sx, n, rs, cs, chunk, S.ps,
+                     S.cnt, sb, unshifted);
   hipLaunchKernelGGL(tail_scan_kernel, dim3(1, m), dim3(64), 0, s, S.cnt, gc, S.ps, sb);
   if (cap > kTailMax)
     hipLaunchKernelGGL(fill_inf_kernel, dim3((unsigned)((cap + 255) / 256), m), dim3(256), 0, s,
                        S.tv, cap, sb);
-  hipLaunchKernelGGL(tail_compact_kernel, dim3(gc, m), dim3(256), 0, s, out, n, rs, cs, chunk,
-                     S.ps, S.cnt, cap, S.tv, S.ti, sb);
+  hipLaunchKernelGGL(tail_compact_kernel, dim3(gc, m), dim3(256), 0, s, sx, n, rs, cs, chunk,
+                     S.ps, S.cnt, cap, S.tv, S.ti, sb, unshifted);
   // 4. sort the tails
   hipError_t e = sort_tail(S, cap, m, sb, s);
   if (e != hipSuccess) return e;
@@ -717,6 +728,12 @@ hipError_t psis_columns(const double* lw, double* out, long long n, int m, long 
   hipLaunchKernelGGL(gpd_final_kernel, dim3(1, m), dim3(256), 0, s, S.y, S.ps, 0LL, S.bs, S.ks,
                      S.Lw, nullptr, nullptr, sb);
   hipLaunchKernelGGL(k_inf_kernel, dim3(1, m), dim3(64), 0, s, S.ps, sb);
+  if (!out) {
+    const unsigned go = (unsigned)std::max<long long>(1, std::min<long long>(32, (Mt + 255) / 256));
+    hipLaunchKernelGGL(psis_out_kernel, dim3(go, m), dim3(256), 0, s, S.ps, S.si, Mt, k_dev,
+                       n_tail_dev, tail_idx_dev, tail_cap, sb);
+    return hipGetLastError();
+  }
   // 6. smoothing
   hipLaunchKernelGGL(smooth_kernel, dim3(32, m), dim3(256), 0, s, out, rs, cs, S.ps, S.si, cap, sb);
   // 7. renormalise: x -= sumlogs(x)

@@ -39,6 +39,31 @@ def _colmajor(lw):
     return None
 
 
+def psis_khat(lw, Reff=1.0):
+    """The Pareto shape estimates kss of `psislw(lw, Reff)` alone (ndarray [m],
+    or a scalar for 1-D input): the device pipeline stops after the GPD fit --
+    the smoothed log weights, which only the first output of psislw carries, are
+    never formed (vb_psislw with a null lw_out)."""
+    cm = _colmajor(lw)
+    src, rs_cm = cm, True
+    if cm is None:
+        dev = nat.device_tensor(lw)
+        src, rs_cm = (dev if dev is not None else nat.as_f64(np.asarray(lw, dtype=float))), False
+    if lw.ndim == 2:
+        n, m = lw.shape
+    elif lw.ndim == 1:
+        n, m = len(lw), 1
+    else:
+        raise ValueError("Argument `lw` must be 1 or 2 dimensional.")
+    if n <= 1:
+        raise ValueError("More than one log-weight needed.")
+    k = np.empty(m)
+    fn = nat.lib().vb_psislw_colmajor if rs_cm else nat.lib().vb_psislw
+    nat.check(fn(nat.context().handle, nat.dptr(src), n, m, float(Reff), None, nat.dptr(k),
+                 None, 0, None))
+    return k[0] if lw.ndim == 1 else k
+
+
 def psislw_with_tail(lw, Reff=1.0):
     """psislw plus the tail order of each column.  A float64 device tensor
     input stays in HBM: the smoothed log weights come back as a device tensor

@@ -134,7 +134,8 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
                          res['mean_error'], res['std_error'], res['cov_error']])
     else:
         recs = bounds_records(ids, div, smooth, bfam)
-    khat = psis.psislw(lw.t())[1] if len(ids) > 1 else np.array([psis.psislw(lw[0])[1]])
+    # k-hat only (psis.py:112-208's kss): the smoothed weights are not needed here
+    khat = psis.psis_khat(lw.t()) if len(ids) > 1 else np.array([psis.psis_khat(lw[0])])
     if timings is not None:
         _sync()
         t2 = time.perf_counter()
