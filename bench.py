@@ -414,6 +414,27 @@ def latency_roofline(step_s, d, n, chivi, host_layout, n_problems, note):
             'note': note}
 
 
+def cfg5_stage_valu(stage_s, local, n_restarts):
+    """VALU issue fraction of config 5's bounds / PSIS stage: the stage's
+    SQ_INSTS_VALU from a committed counter pass over the same stage
+    (profiles/r03/cfg5/bounds_stage_pmc.json, scripts/gpu_cfg5_pmc.sh; 64
+    restarts x M = 1e6, scaled to this rank's restarts) over the live stage time."""
+    p = os.path.join(ROOT, 'profiles', 'r03', 'cfg5', 'bounds_stage_pmc.json')
+    try:
+        prof = json.load(open(p))
+    except (OSError, ValueError):
+        return None
+    if not stage_s:
+        return None
+    vi = prof['stage']['valu_instr'] * local / n_restarts
+    k = prof['kernels'].get('logw_row_kernel<vbd::EightSchools, true, false, 10>', {})
+    return {'valu_instr': vi, 'achieved': vi / stage_s / 1e9, 'peak': VALU_PEAK_GINSTR,
+            'unit': 'G wave-instr/s', 'frac': vi / stage_s / 1e9 / VALU_PEAK_GINSTR,
+            'logw_kernel_valu_frac': k.get('valu_frac'),
+            'source': 'SQ_INSTS_VALU of the stage (profiles/r03/cfg5/bounds_stage_pmc.json) / '
+                      'live stage seconds; the log-weight kernel fraction is from the profile'}
+
+
 def _cfg4_problem():
     import numpy as np
     Dm = 512
@@ -566,6 +587,7 @@ def leg_cfg5(cpu, host, rank, world, n_restarts=64, iters=5000, M=1_000_000):
                         'frac': ach / HBM_PEAK_GBS if ach else None,
                         'algorithmic_bytes_per_rank': b_stage,
                         'note': 'fitting is latency-bound (one workgroup per restart): fit_roofline'},
+           'bounds_valu': cfg5_stage_valu(tm.get('bounds_psis_s'), local, n_restarts),
            'fit_roofline': (latency_roofline(tm['fit_s'] / iters, 10, 100, chivi=False,
                                              host_layout=True, n_problems=local,
                                              note='one workgroup per restart, %d restarts on this '
