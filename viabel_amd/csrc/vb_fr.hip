@@ -305,6 +305,10 @@ __global__ __launch_bounds__(256) void fr_pack_kernel(int D, const double* GL, c
     if (sc->warm_step) {
       sc->hint_ns = max(sc->hint_ns, sc->ns_iter);
       sc->hint_pcg = max(sc->hint_pcg, sc->pcg_iter);
+      // launches a root needs: through the final update (fin: ns_iter - 1) or
+      // through the detecting one (ns_iter)
+      if (sc->ns_fin) sc->hint_fin = max(sc->hint_fin, sc->ns_iter - 1);
+      else sc->hint_det = max(sc->hint_det, sc->ns_iter);
     }
   }
   if (idx >= (long long)D * D) return;
@@ -439,6 +443,8 @@ struct FrSched {
   int ns_fin;                    // the last Newton-Schulz update was final (see fr_sqrt)
   int status;                    // sticky: 1 NS not converged, 2 PCG not converged
   int hint_ns, hint_pcg;         // sticky maxima of the iteration counts
+  int hint_fin, hint_det;        // sticky maxima of the launches needed (final update /
+                                 // detection), see fr_info
   int warm_step;                 // this root was warm-started (its count feeds hint_ns)
 };
 
@@ -630,6 +636,10 @@ __global__ __launch_bounds__(256) void fr_pack_update_kernel(FrPackArgs a) {
     if (sc->warm_step) {
       sc->hint_ns = max(sc->hint_ns, sc->ns_iter);
       sc->hint_pcg = max(sc->hint_pcg, sc->pcg_iter);
+      // launches a root needs: through the final update (fin: ns_iter - 1) or
+      // through the detecting one (ns_iter)
+      if (sc->ns_fin) sc->hint_fin = max(sc->hint_fin, sc->ns_iter - 1);
+      else sc->hint_det = max(sc->hint_det, sc->ns_iter);
     }
   }
   const long long P = D + (long long)D * (D + 1) / 2;
@@ -1821,7 +1831,7 @@ int fr_info(FrWork* W, hipStream_t st, bool* retry) {
   if (!sq) return 0;
   const FrSched& h = *W->host_sched;
   FrSched* d = static_cast<FrSched*>(W->sched.p);
-  FR_HIP(hipMemsetAsync(&d->status, 0, 3 * sizeof(int), st));
+  FR_HIP(hipMemsetAsync(&d->status, 0, 5 * sizeof(int), st));   // status and the hints
   if ((h.status & 1) || (!h.ns_conv && !h.ns_fin)) {
     // warm roots launch exactly the learnt count: a step that needed more asks
     // the caller to run its advance again with a larger count
@@ -1838,8 +1848,12 @@ int fr_info(FrWork* W, hipStream_t st, bool* retry) {
   if (h.status & 2)
     return vb_set_error(-2, "conjugate gradients for the sqrtm gradient did not converge in %d "
                             "iterations", W->pcg_kmax);
-  if (W->last_warm && h.hint_ns > 0)
-    W->ns_kmax = std::min(kFrNSMax, std::max(h.hint_ns, h.ns_iter));
+  // Newton-Schulz: launch exactly the iterations the hardest warm step needed --
+  // up to its final update when the finish rule ended it (the root is then in
+  // the output buffer already: no detection T and no copying launch), or up to
+  // the launch that detected convergence
+  if (W->last_warm && std::max(h.hint_fin, h.hint_det) > 0)
+    W->ns_kmax = std::min(kFrNSMax, std::max(h.hint_fin, h.hint_det));
   // PCG: the learnt count is the index of the converged iteration, so + 1
   // launches exactly the iterations the hardest warm step so far needed (a later
   // step needing one more stops one iteration short: ~10x the 1e-9 target
