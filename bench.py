@@ -40,6 +40,8 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X dense fp64 MFMA spec peak
 # wave64 fp64 VALU issue: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per instruction
 # (profiles/r01/ubench_instr_costs.txt)
 VALU_PEAK_GINSTR = 256 * 4 * 2.4 / 4
+# config 4: products of 2 D^3 one profiled step executes (see leg_cfg4)
+EXEC_PRODUCTS_CFG4 = 14 * 136 / 256 + 3 * 0.25 + 11 + 1
 CHUNK = 256                    # steps per sep_kernel launch (vb_capi.hip max_chunk)
 
 
@@ -480,15 +482,18 @@ def leg_cfg4(cpu, host, steps=30):
            'roofline': {'bound': 'mfma', 'achieved': ach, 'peak': FP64_PEAK_TFLOPS,
                         'unit': 'TFLOP/s', 'frac': ach / FP64_PEAK_TFLOPS,
                         'algorithmic_flops_per_step': flops,
-                        # GEMMs one step executes (rocprofv3 timeline of a config-4 step,
-                        # profiles/r02/cfg4/step_timeline.txt: Sigma, Newton-Schulz
-                        # iteration 0 + 4 x (T, Y|Z), x / grad / G_S, PCG 1 + 7 + 6,
-                        # G_L): 29.75 products of 2 D^3
-                        'executed_flops_per_step': 29.75 * 2 * Dm ** 3,
-                        'executed_tflops': 29.75 * 2 * Dm ** 3 / dt / 1e12,
+                        # ESTIMATE from one profiled step, not counted in this run
+                        # (rocprofv3 timeline, profiles/r03/cfg4/step_timeline.txt): Sigma
+                        # and the Newton-Schulz products are symmetric (upper-triangle
+                        # tiles, 136/256 of a product): Sigma + iteration 0 + 4 x (T, Y, Z)
+                        # = 14 x 0.531; x / grad / G_S 3 x 0.25; PCG 1 + 5 x 2; G_L 1:
+                        # 20.19 products of 2 D^3
+                        'executed_flops_per_step_est': EXEC_PRODUCTS_CFG4 * 2 * Dm ** 3,
+                        'executed_tflops_est': EXEC_PRODUCTS_CFG4 * 2 * Dm ** 3 / dt / 1e12,
                         'note': 'whole step (all launches) timed on the host clock; flops = '
-                                '8 N D^2 + 20 D^3 (SURVEY §8d); executed = the GEMM flops the '
-                                'Newton-Schulz + PCG step runs (profiled count)'}}
+                                '8 N D^2 + 20 D^3 (SURVEY §8d); executed_*_est = the GEMM '
+                                'flops of one profiled step (a fixed estimate: the counts the '
+                                'device learns can differ by an iteration)'}}
     if cpu:
         from oracle import fullrank_oracle as fo
         ofam = fo.FullRankT(Dm, 100.0)
