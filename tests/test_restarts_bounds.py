@@ -37,3 +37,13 @@ def test_bounds_records_match_per_restart(make):
                         res['mean_error'], res['std_error'], res['cov_error']])
     np.testing.assert_allclose(new, np.array(old), rtol=1e-14, atol=0)
     assert [str(x.message) for x in w_new] == [str(x.message) for x in w_old]
+
+
+def test_default_inits_are_the_per_restart_randomstate_streams():
+    """default_inits re-seeds one generator per restart: bit for bit
+    base + RandomState(r).randn(P) * scale."""
+    import numpy as np
+    from viabel_amd import restarts
+    base = np.linspace(-1, 1, 6)
+    want = np.stack([base + np.random.RandomState(r).randn(6) * 0.3 for r in range(9)])
+    np.testing.assert_array_equal(restarts.default_inits(9, 6, scale=0.3, base=base), want)

@@ -37,7 +37,14 @@ def default_inits(n_restarts, P, scale=0.5, base=None):
     """init_r = base + RandomState(r).randn(P) * scale (SURVEY §8d config 5,
     the fixed-scale variant of vb.py:420-421)."""
     base = np.zeros(P) if base is None else np.asarray(base, dtype=float)
-    return np.stack([base + np.random.RandomState(r).randn(P) * scale for r in range(n_restarts)])
+    # one generator re-seeded per restart: the same streams as RandomState(r),
+    # without constructing 64 generator objects (~15 ms of host time)
+    rs = np.random.RandomState(0)
+    out = np.empty((n_restarts, P))
+    for r in range(n_restarts):
+        rs.seed(r)
+        out[r] = base + rs.randn(P) * scale
+    return out
 
 
 def bind_local_device(rank=0):
