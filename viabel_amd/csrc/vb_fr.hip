@@ -596,6 +596,9 @@ struct FrPackArgs {
 };
 
 __global__ __launch_bounds__(256) void fr_pack_update_kernel(FrPackArgs a) {
+#ifndef VB_NO_KWARM
+  kernarg_warm(a);
+#endif
   __shared__ double red[16];
   const int D = a.D;
   const int b = blockIdx.x;

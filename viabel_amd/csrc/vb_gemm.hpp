@@ -22,6 +22,21 @@
 
 namespace vbk {
 
+// Touch every 64-byte line of a kernel's by-value argument struct at once.
+// The fields are read later behind data-dependent scalar branches, and each
+// line's first read is a scalar-cache miss (kernel arguments live in HBM) that
+// the wave waits on; one overlapped round of misses replaces several serial
+// ones (about 0.5 us each; measured on the fp64 GEMM, profiles/r03/cfg4).
+template <class T>
+__device__ __forceinline__ void kernarg_warm(const T& a) {
+  constexpr int W = (int)(sizeof(T) / 4), NL = (W + 15) / 16 + 1;
+  const int* p = reinterpret_cast<const int*>(&a);
+  int x = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) x ^= p[16 * i < W ? 16 * i : W - 1];
+  asm volatile("" ::"s"(x));
+}
+
 struct GemmOp {
   bool ta, tb;
   int M, N, K;
@@ -332,6 +347,20 @@ __device__ __forceinline__ void vm_wait_tiles(int pending) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+#ifdef VB_GEMM_PROF
+// phase timestamps (s_memrealtime, 100 MHz) of thread 0 of every block of the
+// last launch: [0] entry, [1] after the skip test, [2] main loop start,
+// [3..3+nt) after each k stage's barrier, [14] main loop end, [15] epilogue end
+__device__ unsigned long long g_gemm_ts[1024][16];
+#define VB_GEMM_TS(k)                                                                \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x + blockIdx.y * gridDim.x < 1024)              \
+      g_gemm_ts[blockIdx.x + blockIdx.y * gridDim.x][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define VB_GEMM_TS(k) do {} while (0)
+#endif
+
 template <bool TA, bool TB>
 __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, double* lds,
                                               d4 (&acc)[4]) {
@@ -382,11 +411,15 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
     xa[f] = la + 8u * (unsigned)(AK ? glds_at<true>(ra, kk) : glds_at<false>(kk, ra));
     xb[f] = lb + 8u * (unsigned)(BK ? glds_at<true>(cb, kk) : glds_at<false>(kk, cb));
   }
+  VB_GEMM_TS(2);
   for (int it = 0; it < nt; ++it) {
     const int last_issued = it + GS - 2 < nt - 1 ? it + GS - 2 : nt - 1;
     vm_wait_tiles(last_issued - it);
     __builtin_amdgcn_s_barrier();            // tile it is in LDS; stage (it - 1) % GS is free
+    if (it < 11) VB_GEMM_TS(3 + it);
+#ifndef VB_GEMM_NOLOAD
     if (it + GS - 1 < nt) issue(it + GS - 1);
+#endif
     // fragment reads as inline asm: the compiler would otherwise guard every
     // ds_read behind vmcnt(0) (it cannot tell which LDS-DMA tile a read
     // aliases), draining the tiles in flight; the waits below are explicit.
@@ -406,7 +439,11 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
       else if (ahead == 2) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(fa[f]), "+v"(fb[f]));
       else if (ahead == 1) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(fa[f]), "+v"(fb[f]));
       else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[f]), "+v"(fb[f]));
+#ifdef VB_GEMM_NOMFMA
+      acc[f & 3][0] += fa[f] * fb[f];
+#else
       acc[f & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[f], fb[f], acc[f & 3], 0, 0, 0);
+#endif
       if (f + 4 < NST) {
         asm volatile("ds_read_b64 %0, %1" : "=v"(fa[f + 4]) : "v"(xa[f + 4] + so));
         asm volatile("ds_read_b64 %0, %1" : "=v"(fb[f + 4]) : "v"(xb[f + 4] + so));
@@ -414,6 +451,7 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
     }
   }
   __syncthreads();
+  VB_GEMM_TS(14);
 }
 
 // One BT x BT output tile (bx, by) of g (the whole block, NTH threads).  slot =
@@ -609,14 +647,29 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
 template <bool TA, bool TB, bool KS, bool DUAL>
 __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   const GemmOp& g = gg.op[blockIdx.z];
+#ifndef VB_NO_KWARM
+  kernarg_warm(g);   // (every line of the op)
+#endif
   __shared__ __attribute__((aligned(16))) double smem[SMEM];
   double(*sA)[BUF] = reinterpret_cast<double(*)[BUF]>(smem);
   double(*sB)[BUF] = reinterpret_cast<double(*)[BUF]>(smem + 2 * BUF);
+  VB_GEMM_TS(0);
   int bx = blockIdx.x, by = blockIdx.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
   if (g.sym) {
     tri_tile(blockIdx.x, (g.N + BT - 1) / BT, by, bx);
     slot = blockIdx.x;
   }
+#ifdef VB_GEMM_XCD
+  else if (gridDim.x == 16 && gridDim.y == 16) {
+    // experiment: block b runs on XCD b % 8 (round-robin dispatch); give XCD x the
+    // 4 x 8 rectangle of tiles rows 4 (x / 2) .., columns 8 (x % 2) .., so its L2
+    // holds 4 A row panels and 8 B column panels
+    const int b = blockIdx.y * 16 + blockIdx.x, x = b & 7, i = b >> 3;
+    by = 4 * (x >> 1) + (i >> 3);
+    bx = 8 * (x & 1) + (i & 7);
+    slot = by * 16 + bx;
+  }
+#endif
   if (const int sk = gemm_skip(g, sB[1])) {
     // the copy decision uses this block's own test (sk == 2) or state written
     // by earlier launches (sk == 1), never a peer block's stores in this launch
@@ -639,7 +692,9 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
     }
     return;
   }
+  VB_GEMM_TS(1);
   gemm_tile<TA, TB, KS, DUAL>(g, bx, by, slot, sA, sB, smem);
+  VB_GEMM_TS(15);
 }
 
 }  // namespace gemm_detail
