@@ -206,6 +206,17 @@ bool fr_fuse_enabled() {
   return !(e && e[0] == '0');
 }
 
+// VIABEL_AMD_BLOCK_PF=0: the block kernel's device-noise rows are read straight
+// from HBM by the row threads instead of staged into LDS by a copy wave (A/B
+// switch; same bits)
+int block_pf_enabled() {
+  static const int on = [] {
+    const char* e = std::getenv("VIABEL_AMD_BLOCK_PF");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on;
+}
+
 int check_ctx(vb_ctx* c) {
   if (!c) return fail(VB_EINVAL, "null vb_ctx");
   VB_HIP(hipSetDevice(c->device));
@@ -644,6 +655,7 @@ int vb_objective_value_grad(vb_ctx* c, const vb_family* fam, const vb_target* tg
     VB_HIP(vbk::launch_sep_values(a.vpart, 1, a.n_waves, sep_c0(fi, pd), dval, c->stream));
   } else if (D <= vbk::kBlockDMax && !cb) {
     vbk::BlockArgs a{};
+    a.pf = block_pf_enabled();
     a.D = D;
     a.N = N;
     a.W = 1;
@@ -1025,6 +1037,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
     }
   } else {
     vbk::BlockArgs a{};
+    a.pf = block_pf_enabled();
     a.D = D;
     a.N = N;
     a.W = r->W;
@@ -1137,7 +1150,7 @@ int vb_block_floor(vb_ctx* c, int32_t D, int32_t N, int32_t chivi, int32_t host_
   VB_HIP(hipEventCreate(&e1));
   VB_HIP(hipEventRecord(e0, c->stream));
   VB_HIP(vbk::launch_block_floor(D, N, host_layout != 0, chivi != 0, (int)n_steps,
-                                 (int)n_problems, out.d(), c->stream));
+                                 (int)n_problems, out.d(), c->stream, block_pf_enabled() != 0));
   VB_HIP(hipEventRecord(e1, c->stream));
   VB_HIP(hipEventSynchronize(e1));
   float ms = 0.f;

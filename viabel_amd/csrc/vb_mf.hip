@@ -23,6 +23,7 @@
 
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 using namespace vbd;
 
@@ -458,15 +459,28 @@ __global__ __launch_bounds__(kValThreads) void sep_values_kernel(const double* v
 }
 
 // out[q][p] = mean_r hist[q][r][p]; sequential over r like numpy's axis-0 reduce.
-__global__ __launch_bounds__(256) void row_mean_kernel(const double* hist, long long rows,
-                                                       long long P, long long nprob,
-                                                       double* out) {
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+// np.mean(hist, axis=0) per problem: numpy adds the rows in order, so each
+// thread keeps that order; 64-thread blocks spread the few columns over many
+// CUs and batches of 16 independent loads keep them in flight (the adds stay
+// sequential).
+constexpr int kRowMeanThreads = 64, kRowMeanU = 16;
+__global__ __launch_bounds__(kRowMeanThreads) void row_mean_kernel(const double* hist, long long rows,
+                                                                   long long P, long long nprob,
+                                                                   double* out) {
+  const long long idx = (long long)blockIdx.x * kRowMeanThreads + threadIdx.x;
   if (idx >= P * nprob) return;
   const long long q = idx / P, p = idx % P;
   const double* h = hist + q * rows * P + p;
   double acc = 0.0;
-  for (long long r = 0; r < rows; ++r) acc += h[r * P];
+  long long r = 0;
+  for (; r + kRowMeanU <= rows; r += kRowMeanU) {
+    double v[kRowMeanU];
+#pragma unroll
+    for (int u = 0; u < kRowMeanU; ++u) v[u] = h[(r + u) * P];
+#pragma unroll
+    for (int u = 0; u < kRowMeanU; ++u) acc += v[u];
+  }
+  for (; r < rows; ++r) acc += h[r * P];
   out[idx] = acc / (double)rows;
 }
 
@@ -532,11 +546,36 @@ constexpr int kBlockMaxThreads = 512;
 constexpr int kBlockDrawLds = 4096;  // doubles of LDS for the draw records
 constexpr int kBlockMaxRowWaves = 4;
 
+// Device-noise path: a copy wave stages step s + 2's noise rows (and log q
+// partials) into a 3-slot LDS ring with LDS-DMA loads while the row waves work
+// on step s, so no step waits on an HBM round trip for its rows.  Slot layout:
+// [N D noise | N lq], each part rounded up to whole 128-double DMA instructions.
+constexpr int kBlockPfLds = 4608;    // doubles of LDS for the 3-slot ring (36 KB)
+constexpr int kPfUnit = 128;         // doubles per wave-wide 16-byte DMA instruction
+
+// e[I] = LDS double at addr + 8 I (inline-asm reads with immediate offsets)
+template <int I>
+__device__ __forceinline__ double lds_ld_off(unsigned addr) {
+  double t;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(t) : "v"(addr), "i"(8 * I));
+  return t;
+}
+template <int DMAX, int... Is>
+__device__ __forceinline__ void lds_row(unsigned addr, double (&e)[DMAX],
+                                        std::integer_sequence<int, Is...>) {
+  ((e[Is] = lds_ld_off<Is>(addr)), ...);
+}
+
 struct BlockLayout {
   int nt, rw, pipe, rec;  // threads, row waves, overlapped draws, doubles per sample record
+  int pf;                 // device noise prefetched by a copy wave (the last wave)
+  int pf_lq, pf_slot;     // doubles offset of the lq part in a slot, doubles per slot
 };
 
-__host__ __device__ inline BlockLayout block_layout(int N, int D, bool host, bool need_lq) {
+__host__ __device__ inline int pf_round(int n) { return (n + kPfUnit - 1) / kPfUnit * kPfUnit; }
+
+__host__ __device__ inline BlockLayout block_layout(int N, int D, bool host, bool need_lq,
+                                                   bool pf_ok = false) {
   const int NP = (D + 1) / 2;
   const int rw = std::min(kBlockMaxRowWaves, std::max(1, (N + 63) / 64));
   BlockLayout L{};
@@ -545,6 +584,10 @@ __host__ __device__ inline BlockLayout block_layout(int N, int D, bool host, boo
   if (host) {
     L.nt = 64 * rw;
     L.pipe = 0;
+    L.pf_lq = pf_round(N * D);
+    L.pf_slot = L.pf_lq + (need_lq ? pf_round(N) : 0);
+    L.pf = pf_ok && 3 * L.pf_slot <= kBlockPfLds;
+    if (L.pf) L.nt += 64;
     return L;
   }
   const long long iw = ((long long)N * NP + 63) / 64;  // waves of draw items
@@ -559,7 +602,7 @@ __host__ __device__ inline BlockLayout block_layout(int N, int D, bool host, boo
   return L;
 }
 
-template <class TGT, bool TFAM, bool HOST, int DMAX>
+template <class TGT, bool TFAM, bool HOST, int DMAX, bool PF = false>
 __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   constexpr int K = 2 * DMAX + 2;   // G[DMAX], H[DMAX], V/S, spare
   constexpr int WMAX = 64;
@@ -571,6 +614,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
   __shared__ double s_e[HOST ? 1 : kBlockDrawLds + DMAX];  // + slack for the row loads
+  __shared__ __attribute__((aligned(16))) double s_pf[HOST && PF ? kBlockPfLds + kBlockDMax : 1];
   if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
 
   using Row = RowOf<TGT>;
@@ -579,10 +623,43 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   const int prob = blockIdx.x;
   const int D = a.D, N = a.N, W = a.W, P = a.P;
   const bool need_lq = a.chivi || a.pd;
-  const BlockLayout L = block_layout(N, D, HOST, need_lq);
+  const BlockLayout L = block_layout(N, D, HOST, need_lq, HOST && PF);
   const int RW = L.rw, RT = 64 * RW, R = L.rec;
   const bool row_wave = wid < RW;
-  const int val_tid = NT > 64 ? NT - 64 : 0;  // value on another wave than the update
+  // PF instances are launched exactly when the layout has the copy wave (block_dispatch_dm)
+  constexpr bool kPF = HOST && PF;
+  const bool copy_wave = kPF && wid == RW;   // the last wave (block_layout)
+  const int NTw = kPF ? NT - 64 : NT;        // threads of the row / draw waves
+  const int val_tid = NTw > 64 ? NTw - 64 : 0;  // value on another wave than the update
+  const bool pre_lq = HOST && a.noise_lq != nullptr;
+  // copy wave: noise rows (and log q partials) of step s -> ring slot s % 3, as
+  // wave-wide 16-byte LDS-DMA loads (4-byte ones when a source is not 16-byte
+  // aligned); lanes past the end re-read the first element into the slot's slack
+  auto pf_copy = [&](const double* src, double* dst, int nd) __attribute__((always_inline)) {
+    if ((((uintptr_t)src) & 15) == 0 && (nd & 1) == 0) {
+      for (int o = 0; o < nd; o += kPfUnit) {
+        const int e = o + 2 * lane;
+        __builtin_amdgcn_global_load_lds((const void*)(src + (e < nd ? e : 0)), (void*)(dst + o),
+                                         16, 0, 0);
+      }
+    } else {
+      const int* s4 = reinterpret_cast<const int*>(src);
+      int* d4 = reinterpret_cast<int*>(dst);
+      for (int o = 0; o < 2 * nd; o += 64) {
+        const int e = o + lane;
+        __builtin_amdgcn_global_load_lds((const void*)(s4 + (e < 2 * nd ? e : 0)), (void*)(d4 + o),
+                                         4, 0, 0);
+      }
+    }
+  };
+  auto pf_issue = [&](int s) __attribute__((always_inline)) {
+    if constexpr (kPF) {
+      const long long rix = ((long long)prob * a.n_steps + s) * N;
+      double* slot_p = s_pf + (s % 3) * L.pf_slot;
+      pf_copy(a.noise + rix * D, slot_p, N * D);
+      if (need_lq && pre_lq) pf_copy(a.noise_lq + rix, slot_p + L.pf_lq, N);
+    }
+  };
   const double dN = (double)N;
   double* lam_g = a.lam + (long long)prob * P;
   double* ring_g = a.ring ? a.ring + (long long)prob * W * P : nullptr;
@@ -642,7 +719,12 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
     }
   };
 
-  __syncthreads();  // Box-Muller tables, lam, ring and sigma are in LDS
+  if (copy_wave && a.n_steps > 0) {
+    pf_issue(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.n_steps > 1) pf_issue(1);
+  }
+  __syncthreads();  // Box-Muller tables, lam, ring and sigma (and step 0's rows) are in LDS
   if constexpr (!HOST) {
     if (L.pipe && a.n_steps > 0) {
       draw_item(tid, NT, N * NP, 0, a.rng_step0, s_e);
@@ -727,8 +809,40 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
       }
     };
 
-    if constexpr (HOST) {
-      const bool pre_lq = a.noise_lq != nullptr;
+    if constexpr (kPF) {
+      if (rows) {
+        typedef __attribute__((address_space(3))) double lds_f64;
+        const double* buf = s_pf + (s % 3) * L.pf_slot;
+        const unsigned base = (unsigned)(uintptr_t)((const lds_f64*)buf);
+        for (int n = tid; n < N; n += RT) {
+          double e[DMAX];
+          double lqs = 0.0;
+          // LDS reads as inline asm: the compiler cannot tell these slots from
+          // the copy wave's DMA targets and would wait vmcnt(0) (this wave's
+          // own outstanding stores) before each; the barriers order them.  One
+          // row address + immediate offsets (d >= D reads the next row or the
+          // ring's slack, discarded by the select below)
+          lds_row(base + 8u * (unsigned)(n * D), e, std::make_integer_sequence<int, DMAX>{});
+          double tl = 0.0;
+          if (need_lq && pre_lq)
+            asm volatile("ds_read_b64 %0, %1" : "=v"(tl) : "v"(base + 8u * (unsigned)(L.pf_lq + n)));
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(tl) :: "memory");
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            asm volatile("" : "+v"(e[d]));
+            e[d] = d < D ? e[d] : 0.0;
+            if (need_lq && !pre_lq && d < D) {
+              if constexpr (TFAM)
+                lqs += a.t_const - log1p(e[d] * e[d] / a.df) * lq_half;
+              else
+                lqs += -0.5 * e[d] * e[d] - 0.5 * kLog2Pi;
+            }
+          }
+          if (need_lq && pre_lq) lqs = tl;
+          row_of(e, lqs);
+        }
+      }
+    } else if constexpr (HOST) {
       for (int n = tid; n < N; n += RT) {
         const long long rix = ((long long)prob * a.n_steps + s) * N + n;
         const double* row = a.noise + rix * D;
@@ -900,7 +1014,22 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
   // (the t family runs only with pre-drawn noise: one loop of row waves)
   bool split = false;
   if constexpr (!HOST && !TFAM) split = L.pipe;
-  if (split) {
+  if (copy_wave) {
+    // The copy wave's own loop: per step, wait for its last prefetch (step s + 1,
+    // issued one step ago, so it has landed before this wave's first barrier of
+    // step s), stage step s + 2 into slot (s + 2) % 3 (read in step s - 1, before
+    // that step's last barrier), then join the step's barriers -- raw s_barrier:
+    // __syncthreads' release fence would wait for the new prefetch (vmcnt(0))
+    // and hold every wave at the step's first barrier.  The count matches the
+    // row waves' step: the CHIVI max barrier, the two reduction barriers and the
+    // end-of-step barrier.
+    const int nbar = a.chivi ? 4 : 3;
+    for (int s = 0; s < a.n_steps; ++s) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (s + 2 < a.n_steps) pf_issue(s + 2);
+      for (int b = 0; b < nbar; ++b) __builtin_amdgcn_s_barrier();
+    }
+  } else if (split) {
     if constexpr (!HOST && !TFAM) {
       if (row_wave) {
         for (int s = 0; s < a.n_steps; ++s) step(s, std::integral_constant<int, 1>{});
@@ -1003,9 +1132,11 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
 }
 
 hipError_t launch_block_floor(int D, int N, bool host_layout, bool chivi, int n_steps, int nprob,
-                              double* out, hipStream_t s) {
+                              double* out, hipStream_t s, bool pf) {
   if (D < 1 || D > kBlockDMax || N < 1 || n_steps < 0 || nprob < 1) return hipErrorInvalidValue;
-  const BlockLayout L = block_layout(N, D, host_layout, chivi);
+  // the same block shape as block_kernel's (with the device-noise copy wave, which
+  // only joins the barriers here)
+  const BlockLayout L = block_layout(N, D, host_layout, chivi, pf);
   const dim3 grid(nprob), block(L.nt);
   const int rows = 64 * L.rw, W = 10;
   if (D <= 2)
@@ -1569,17 +1700,24 @@ hipError_t launch_sep(int fam, int tgt, bool host, const SepArgs& a, hipStream_t
 // Threads per problem: host noise -> one thread per sample (<= 4 waves); Philox ->
 // enough waves for the (sample, pair) draw items of a step (<= 8 waves).
 inline unsigned block_threads(const BlockArgs& a, bool host) {
-  return (unsigned)block_layout(a.N, a.D, host, a.chivi || a.pd).nt;
+  return (unsigned)block_layout(a.N, a.D, host, a.chivi || a.pd, a.pf != 0).nt;
 }
 
 template <class TGT, int DM>
 static hipError_t block_dispatch_dm(int fam, bool host, const BlockArgs& a, int nprob,
                                     hipStream_t s) {
   const dim3 grid(nprob), block(block_threads(a, host));
+  const bool pf = host && block_layout(a.N, a.D, true, a.chivi || a.pd, a.pf != 0).pf;
   if (host && fam == 1) {
-    hipLaunchKernelGGL((block_kernel<TGT, true, true, DM>), grid, block, 0, s, a);
+    if (pf)
+      hipLaunchKernelGGL((block_kernel<TGT, true, true, DM, true>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((block_kernel<TGT, true, true, DM>), grid, block, 0, s, a);
   } else if (host) {
-    hipLaunchKernelGGL((block_kernel<TGT, false, true, DM>), grid, block, 0, s, a);
+    if (pf)
+      hipLaunchKernelGGL((block_kernel<TGT, false, true, DM, true>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((block_kernel<TGT, false, true, DM>), grid, block, 0, s, a);
   } else if (fam == 1) {
     // (runs pre-draw the t family's Philox noise by default: launch_block_predraw)
     hipLaunchKernelGGL((block_kernel<TGT, true, false, DM>), grid, block, 0, s, a);
@@ -1648,8 +1786,8 @@ hipError_t launch_sep_values(const double* vpart, int n_steps, int n_waves, doub
 hipError_t launch_row_mean(const double* hist, long long rows, long long P, long long nprob,
                            double* out, hipStream_t s) {
   const long long tot = P * nprob;
-  hipLaunchKernelGGL(row_mean_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, hist,
-                     rows, P, nprob, out);
+  hipLaunchKernelGGL(row_mean_kernel, dim3((unsigned)((tot + kRowMeanThreads - 1) / kRowMeanThreads)),
+                     dim3(kRowMeanThreads), 0, s, hist, rows, P, nprob, out);
   return hipGetLastError();
 }
 

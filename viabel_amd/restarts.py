@@ -101,7 +101,7 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
     run = vb.DeviceRun(obj, n_iters, inits, window=window, learning_rate=learning_rate,
                        learning_rate_end=learning_rate_end)
     run.advance_philox(n_iters, seed, stream_base, 0, stream_stride=stride)
-    _, _, vals, smooth = run.result()
+    _, _, vals, smooth = run.result(history=False)
     t1 = time.perf_counter()
     # the M log weights of every restart stay in HBM from the draws through the
     # bounds and PSIS: row j of one [restarts][M] buffer; PSIS then runs all
