@@ -51,8 +51,8 @@ int main(int argc, char** argv) {
   }
   printf("entry after first block: mean %.2f us\n", ent / nb);
   const char* nm[16] = {"entry", "skip done", "loop start", "k0", "k1", "k2", "k3", "k4", "k5", "k6", "k7",
-                        "k8", "k9", "k10", "loop end", "epilogue end"};
-  for (int k = 1; k < 16; ++k)
-    if (k < 11 || k >= 14) printf("  %-14s %7.2f us after entry (mean over blocks)\n", nm[k], ph[k] / nb);
+                        "k-part reduced", "tile stored", "partials done", "loop end", "epilogue end"};
+  const int order[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 14, 11, 12, 13, 15};
+  for (int k : order) printf("  %-14s %7.2f us after entry (mean over blocks)\n", nm[k], ph[k] / nb);
   return 0;
 }

@@ -350,7 +350,8 @@ __device__ __forceinline__ void vm_wait_tiles(int pending) {
 #ifdef VB_GEMM_PROF
 // phase timestamps (s_memrealtime, 100 MHz) of thread 0 of every block of the
 // last launch: [0] entry, [1] after the skip test, [2] main loop start,
-// [3..3+nt) after each k stage's barrier, [14] main loop end, [15] epilogue end
+// [3..10] after each of the first 8 k stages' barriers, [14] main loop end, [11]
+// k parts reduced, [12] tile stored, [13] partial sums stored, [15] epilogue end
 __device__ unsigned long long g_gemm_ts[1024][16];
 #define VB_GEMM_TS(k)                                                                \
   do {                                                                               \
@@ -416,7 +417,7 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
     const int last_issued = it + GS - 2 < nt - 1 ? it + GS - 2 : nt - 1;
     vm_wait_tiles(last_issued - it);
     __builtin_amdgcn_s_barrier();            // tile it is in LDS; stage (it - 1) % GS is free
-    if (it < 11) VB_GEMM_TS(3 + it);
+    if (it < 8) VB_GEMM_TS(3 + it);
 #ifndef VB_GEMM_NOLOAD
     if (it + GS - 1 < nt) issue(it + GS - 1);
 #endif
@@ -571,6 +572,7 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
     for (int r = 0; r < 4; ++r) red[((h - 1) * 16 + q * 4 + r) * 64 + lane] = r4[r];
   }
   __syncthreads();
+  VB_GEMM_TS(11);
   if (h == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -614,6 +616,7 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
         sq += e * e;
       }
     }
+    VB_GEMM_TS(12);
     const double pw = mirror ? 2.0 : 1.0;   // the transposed tile's share of a sum
     if (g.sq_part) {
 #pragma unroll
@@ -640,6 +643,7 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
         if ((lane & 15) == 0 && row < g.M) g.rp_part[(long long)(2 * bx + wn) * g.M + row] = rp[r];
       }
     }
+    VB_GEMM_TS(13);
   }
   __syncthreads();
 }
