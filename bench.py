@@ -344,9 +344,12 @@ def leg_cfg1(cpu):
     out = {'config': 1, 'workload': 'mixture D=2 mf-Gauss KLVI N=100, 5000 iters (adagrad_optimize '
                                    'incl. result copy)', 'ms_per_step': dt * 1e3,
            'steps_per_s': 1 / dt, 'value': n * Dm / dt, 'unit': 'MC-samples/s',
-           'roofline': latency_roofline(dt, Dm, n, chivi=False, host_layout=False, n_problems=1,
+           'roofline': latency_roofline(dt, Dm, n, chivi=False,
+                                        host_layout=gauss_runs_predraw(), n_problems=1,
                                         note='one workgroup per problem; D=2 moves 64 B of '
-                                             'parameters per step')}
+                                             'parameters per step; the Gaussian draws are '
+                                             'pre-drawn and staged by the copy wave unless '
+                                             'VIABEL_AMD_PREDRAW is 0 or t')}
     if cpu:
         from oracle import vb_oracle
         ofam = vb_oracle.Family('gauss', Dm)
@@ -399,6 +402,14 @@ def leg_cfg2(cpu):
                                'sample': 'median of 5 x 400 oracle adagrad steps'}
         out['speedup_vs_cpu'] = _median(ts) / dt
     return out
+
+
+def gauss_runs_predraw():
+    """Whether Gaussian-family runs pre-draw their noise (vb_capi.hip
+    predraw_enabled: the default unless VIABEL_AMD_PREDRAW is 0 or t), so the
+    block kernel runs its device-noise layout (row waves + copy wave)."""
+    e = os.environ.get('VIABEL_AMD_PREDRAW', '')
+    return not (e.startswith('0') or e.startswith('t'))
 
 
 def latency_roofline(step_s, d, n, chivi, host_layout, n_problems, note):

@@ -189,13 +189,18 @@ int sync(vb_ctx* c) {
 // kPredrawBytes of draws and kPredrawMaxSteps steps.
 constexpr size_t kPredrawBytes = size_t(256) << 20;
 constexpr long long kPredrawMaxSteps = 512;
-// VIABEL_AMD_PREDRAW: unset / "t" -> the t family pre-draws (default), "all" ->
-// every family, "0" -> in-kernel draws for every family (same bits either way)
-bool predraw_enabled(int fam_kind) {
+int block_pf_enabled();
+// VIABEL_AMD_PREDRAW: unset -> the t family pre-draws, and the Gaussian family in
+// optimisation runs whose rows the block kernel's copy wave stages (block_pf_layout);
+// "t" -> the t family only; "all" -> every family and call; "0" -> in-kernel draws
+// for every family (same bits either way)
+bool predraw_enabled(int fam_kind, bool run = false, int N = 0, int D = 0, bool need_lq = false) {
   const char* e = std::getenv("VIABEL_AMD_PREDRAW");
   if (e && e[0] == '0') return false;
   if (fam_kind == VB_FAMILY_MF_T) return true;
-  return e && e[0] == 'a';
+  if (e && e[0] == 'a') return true;
+  if (e && e[0] == 't') return false;
+  return run && block_pf_enabled() && vbk::block_pf_layout(N, D, need_lq);
 }
 
 // VIABEL_AMD_FR_FUSE=0: the full-rank step keeps its separate unpack / power /
@@ -1070,7 +1075,7 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
     a.k1 = k1;
     a.stream = noise->stream;
     a.stream_stride = noise->stream_stride ? noise->stream_stride : 1;
-    if (!host && predraw_enabled(r->fi.kind)) {
+    if (!host && predraw_enabled(r->fi.kind, true, N, D, a.chivi || a.pd)) {
       // Philox draws pre-drawn chunk by chunk by a throughput kernel over the
       // whole chip, then consumed through the device-noise path: the same
       // draws and log q partials, off the per-step critical path

@@ -75,6 +75,8 @@ hipError_t launch_block_floor(int D, int N, bool host_layout, bool chivi, int n_
                               double* out, hipStream_t s, bool pf = false);
 hipError_t launch_block(int fam, int tgt, bool host_noise, const BlockArgs& a, int n_problems,
                         hipStream_t s);
+// whether device-noise blocks of this shape get the copy wave (its LDS ring fits)
+bool block_pf_layout(int N, int D, bool need_lq);
 bool target_separable(int tgt);
 // Pre-drawn block-kernel noise: the standardized draws of n_steps steps of
 // n_problems problems, [q][s][N][D], bit-identical to the block kernel's own

@@ -1696,6 +1696,10 @@ hipError_t launch_sep(int fam, int tgt, bool host, const SepArgs& a, hipStream_t
   }
 }
 
+bool block_pf_layout(int N, int D, bool need_lq) {
+  return N >= 1 && D >= 1 && D <= kBlockDMax && block_layout(N, D, true, need_lq, true).pf;
+}
+
 // Threads per problem: the draws of one step spread over ceil(N/64) waves (<= 4).
 // Threads per problem: host noise -> one thread per sample (<= 4 waves); Philox ->
 // enough waves for the (sample, pair) draw items of a step (<= 8 waves).
