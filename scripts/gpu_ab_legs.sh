@@ -1,0 +1,34 @@
+#!/bin/bash
+# Interleaved A/B of library builds on bench.py legs (default cfg1,cfg2,cfg5), fresh
+# processes: LIBS="base new" (viabel_amd/libviabel_amd_<name>.so; "new" = the
+# default build).  Optional TESTS: a pytest selection run first on the new build.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+if [ -n "${TESTS:-}" ]; then
+  timeout -k 10 600 python -u -m pytest $TESTS -x -q -m gpu --timeout 200 --timeout-method thread \
+    > gpurun_out/pytest_ab.log 2>&1
+  rc=$?; tail -3 gpurun_out/pytest_ab.log; [ $rc -ne 0 ] && exit $rc
+fi
+for i in $(seq 1 ${ROUNDS:-3}); do
+  for L in ${LIBS:-base new}; do
+    lib=$PWD/viabel_amd/libviabel_amd_$L.so; [ "$L" = new ] && lib=$PWD/viabel_amd/libviabel_amd.so
+    VIABEL_AMD_LIB=$lib timeout -k 10 200 python bench.py --legs ${LEGS:-cfg1,cfg2,cfg5} --no-cpu-baseline \
+      --steps 20 --warmup 5 > gpurun_out/ab_legs.json 2> gpurun_out/ab_legs.err || exit $?
+    python - "$L" <<'PY'
+import json, sys
+d = json.loads([l for l in open('gpurun_out/ab_legs.json') if l.startswith('{')][-1])
+c = d['configs']
+out = {'lib': sys.argv[1], 'headline_us': round(d['ms_per_step'] * 1e3, 3)}
+for k in ('cfg1', 'cfg2'):
+    if k in c: out[k + '_us'] = round(c[k].get('ms_per_step', float('nan')) * 1e3, 3)
+if 'cfg4' in c:
+    out['cfg4_ms'] = round(c['cfg4']['ms_per_step'], 4)
+if 'cfg5' in c:
+    out.update(cfg5_ms=round(c['cfg5']['seconds'] * 1e3, 2), fit_ms=round(c['cfg5']['fit_s'] * 1e3, 2),
+               bounds_ms=round(c['cfg5']['bounds_psis_s'] * 1e3, 2))
+print(json.dumps(out), flush=True)
+PY
+  done
+done
