@@ -13,6 +13,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    flag = int(sys.argv[3]) if len(sys.argv) > 3 else -1   # hipSetDeviceFlags before the context
+    if flag >= 0:
+        import ctypes
+        ctypes.CDLL('libamdhip64.so').hipSetDeviceFlags(ctypes.c_uint(flag))
     import torch
     from viabel_amd import _native as nat, targets, vb
     torch.cuda.set_device(0)
@@ -27,6 +31,7 @@ def main():
     run = vb.DeviceRun(obj, 30 * (K + W), init[None, :])
     run.set_timing(True)
     calls = int(sys.argv[1]) if len(sys.argv) > 1 else 1   # warm-up advance calls per W steps
+    idle = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0  # seconds idle before each timed call
     step, walls, spans = 0, [], []
     for rep in range(21):
         for c in range(calls):
@@ -36,6 +41,8 @@ def main():
         torch.cuda.synchronize(dev)
         run.launch_times()
         torch.cuda.synchronize(dev)
+        if idle:
+            time.sleep(idle)
         t0 = time.perf_counter()
         run.advance_philox(K, 0, 1, step)
         t1 = time.perf_counter()
@@ -46,7 +53,7 @@ def main():
         spans.append(run.launch_times()[-1][1])
     first = walls[0]
     rest = np.array(walls[1:])
-    print(json.dumps({'warmup_calls': calls, 'first_us_per_step': round(first[0] / K * 1e6, 3),
+    print(json.dumps({'warmup_calls': calls, 'idle_s': idle, 'flag': flag, 'first_us_per_step': round(first[0] / K * 1e6, 3),
                       'first_submit_us': round(first[1] * 1e6, 2),
                       'first_span_us': round(spans[0] * 1e6, 2),
                       'rest_us_per_step_median': round(float(np.median(rest[:, 0])) / K * 1e6, 3),

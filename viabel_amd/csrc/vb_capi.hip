@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdarg>
@@ -190,6 +191,33 @@ int sync(vb_ctx* c) {
 constexpr size_t kPredrawBytes = size_t(256) << 20;
 constexpr long long kPredrawMaxSteps = 512;
 int block_pf_enabled();
+
+// VIABEL_AMD_HOST_TRACE=1: per-call host timestamps of a launch path to stderr
+// (measurement only; one getenv per process)
+struct HostTrace {
+  static bool on() {
+    static const bool v = [] {
+      const char* e = std::getenv("VIABEL_AMD_HOST_TRACE");
+      return e && e[0] == '1';
+    }();
+    return v;
+  }
+  std::chrono::steady_clock::time_point t[8];
+  int n = 0;
+  HostTrace() {
+    if (on()) t[n++] = std::chrono::steady_clock::now();
+  }
+  void mark() {
+    if (on() && n < 8) t[n++] = std::chrono::steady_clock::now();
+  }
+  void print(const char* what) const {
+    if (!on()) return;
+    std::fprintf(stderr, "[host] %s:", what);
+    for (int i = 1; i < n; ++i)
+      std::fprintf(stderr, " %.2f", std::chrono::duration<double, std::micro>(t[i] - t[i - 1]).count());
+    std::fprintf(stderr, " us\n");
+  }
+};
 // VIABEL_AMD_PREDRAW: unset -> the t family pre-draws, and the Gaussian family in
 // optimisation runs whose rows the block kernel's copy wave stages (block_pf_layout);
 // "t" -> the t family only; "all" -> every family and call; "0" -> in-kernel draws
@@ -939,6 +967,7 @@ static int advance_fr_steps(vb_ctx* c, vb_run* r, int64_t n_steps, const vb_nois
 }
 
 int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
+  HostTrace ht0;
   if (!r) return fail(VB_EINVAL, "null vb_run");
   vb_ctx* c = r->ctx;
   VB_TRY(check_ctx(c));
@@ -1003,6 +1032,8 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
       }
     }
   } else if (r->sep) {
+    ht0.mark();
+    ht0.print("advance entry -> sep branch");
     long long off = 0;
     while (off < n_steps) {
       const int cs = (int)std::min<long long>(r->max_chunk, n_steps - off);
@@ -1032,12 +1063,19 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
       a.k1 = k1;
       a.stream = noise->stream;
       std::pair<hipEvent_t, hipEvent_t>* ev;
+      HostTrace ht;
       VB_TRY(r->next_event(cs, &ev));
+      ht.mark();
       if (ev) VB_HIP(hipEventRecord(ev->first, c->stream));
+      ht.mark();
       VB_HIP(vbk::launch_sep(r->fi.kind, r->tgt, host, a, c->stream));
+      ht.mark();
       VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, sep_c0(r->fi, a.pd != 0), r->values.d() + a.step0,
                                     c->stream));
+      ht.mark();
       if (ev) VB_HIP(hipEventRecord(ev->second, c->stream));
+      ht.mark();
+      ht.print("sep advance: next_event | record | launch_sep | launch_values | record");
       off += cs;
     }
   } else {
