@@ -10,6 +10,8 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-me
   > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_gpu.log
 [ $rc -ge 2 ] && exit $rc
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
+tail -1 gpurun_out/smoke.log
 timeout -k 10 500 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || exit $?
 tail -c 300 gpurun_out/bench.log
 rm -rf gpurun_out/prof3
