@@ -259,7 +259,7 @@ def run_cfg3(torch, stream, dev, n, steps, warmup, rank, dist):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     launches, s0 = [], warmup
@@ -267,6 +267,16 @@ def run_cfg3(torch, stream, dev, n, steps, warmup, rank, dist):
         launches.append((k, max(0, s0 + k - max(s0, hist_start)), sec))
         s0 += k
     return elapsed, launches, run
+
+
+COLL_CPU = False   # collectives on host tensors (gloo rehearsal, see main)
+
+
+def coll_device(dev):
+    """Device of the tensors handed to collectives: the rank's GPU under RCCL, the
+    host under the gloo rehearsal backend."""
+    import torch
+    return torch.device('cpu') if COLL_CPU else dev
 
 
 def load_traffic():
@@ -584,7 +594,8 @@ def leg_cfg5(cpu, host, rank, world, n_restarts=64, iters=5000, M=1_000_000):
     dt = time.perf_counter() - t0
     if dist:
         t = torch.tensor([dt, tm.get('bounds_psis_s', 0.0), tm.get('fit_s', 0.0)],
-                         dtype=torch.float64, device=torch.device('cuda', torch.cuda.current_device()))
+                         dtype=torch.float64,
+                         device=coll_device(torch.device('cuda', torch.cuda.current_device())))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, tm['bounds_psis_s'], tm['fit_s'] = t.tolist()
     local = len(restarts.shard(n_restarts, rank, world))
@@ -696,19 +707,29 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     dist = None
+    # one GPU per rank (LOCAL_RANK mod the visible devices, as restarts.bind_local_device);
+    # VIABEL_AMD_BENCH_BACKEND=gloo rehearses the N > 1 path on fewer GPUs than ranks
+    # (RCCL refuses two ranks on one GPU) -- the driver's runs use nccl (= RCCL)
+    global COLL_CPU
+    backend = os.environ.get('VIABEL_AMD_BENCH_BACKEND', 'nccl')
+    local_dev = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        torch.cuda.set_device(local_dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local_dev))
+        else:
+            dist.init_process_group(backend)
+            COLL_CPU = True
     else:
         torch.cuda.set_device(0)
-    dev = torch.device('cuda', local)
+    dev = torch.device('cuda', local_dev)
 
     from viabel_amd import _native as nat
     # a dedicated (non-NULL) stream: the kernels and the timing events share it
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-    nat.use_stream(local, stream.cuda_stream)
+    nat.use_stream(local_dev, stream.cuda_stream)
     traffic = load_traffic()
 
     K, W, NS = args.steps, args.warmup, args.n_samples
@@ -718,7 +739,8 @@ def main():
     # restart summaries gathered over RCCL (the only collective)
     lam, hist, vals, smooth = run.result()
     summary = torch.tensor([float(vals[0, -1]), float(np.mean(vals[0, -100:])),
-                            float(np.linalg.norm(smooth[0]))], dtype=torch.float64, device=dev)
+                            float(np.linalg.norm(smooth[0]))], dtype=torch.float64,
+                           device=coll_device(dev))
     if dist:
         gathered = [torch.empty_like(summary) for _ in range(world)]
         dist.all_gather(gathered, summary)
