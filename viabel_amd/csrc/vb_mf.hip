@@ -793,6 +793,20 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
         acc[2 * DMAX] += lp;
       } else {
         const double lw = lp - lq;
+        if (mloc == -INFINITY && lw > -INFINITY && lw < INFINITY) {
+          // a thread's first sample (the only one when N <= the row threads): the
+          // general path below rescales zero accumulators by 0 and weights the
+          // sample by exp(0) = 1 -- the same bits without the exp and the K-wide
+          // rescale
+          mloc = lw;
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            acc[d] += g[d];
+            acc[DMAX + d] += g[d] * e[d];
+          }
+          acc[2 * DMAX] += 1.0;
+          return;
+        }
         if (lw > mloc) {
           const double f = (mloc == -INFINITY) ? 0.0 : exp(a.alpha * (mloc - lw));
 #pragma unroll
@@ -1084,10 +1098,13 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
     double sl = 0.0;
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) sl += d < D ? s_lam[D + d] : 0.0;
+    // accumulators: a cheap function of the last update (one LDS read and K adds; a
+    // per-k read of s_lam[k % P] spent an integer division per accumulator and made
+    // the floor grow with K by ~0.06 us per accumulator)
     double acc[K];
-    const double t = (double)(tid + 1) * 1e-3;
+    const double t = (double)(tid + 1) * 1e-3 * s_lam[0];
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = (tid < N) ? t * s_lam[k % P] : 0.0;
+    for (int k = 0; k < K; ++k) acc[k] = (tid < N) ? t + (double)k : 0.0;
     double M = 0.0;
     if (chivi) {
       if (row_wave) {
