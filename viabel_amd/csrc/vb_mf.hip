@@ -586,7 +586,9 @@ __host__ __device__ inline BlockLayout block_layout(int N, int D, bool host, boo
     L.pipe = 0;
     L.pf_lq = pf_round(N * D);
     L.pf_slot = L.pf_lq + (need_lq ? pf_round(N) : 0);
-    L.pf = pf_ok && 3 * L.pf_slot <= kBlockPfLds;
+    // at most 3 row waves + the copy wave: the PF instances launch with <= 256
+    // threads (one wave per SIMD), so their registers may reach the whole file
+    L.pf = pf_ok && rw <= 3 && 3 * L.pf_slot <= kBlockPfLds;
     if (L.pf) L.nt += 64;
     return L;
   }
@@ -603,7 +605,10 @@ __host__ __device__ inline BlockLayout block_layout(int N, int D, bool host, boo
 }
 
 template <class TGT, bool TFAM, bool HOST, int DMAX, bool PF = false>
-__global__ __launch_bounds__(kBlockMaxThreads) void block_kernel(BlockArgs a) {
+// device-noise (HOST) instances launch <= 256 threads (<= 4 row waves, or <= 3 and the
+// copy wave): one wave per SIMD, so their registers may use the whole file instead of
+// spilling at the 256-VGPR cap a 512-thread bound implies (the DMAX = 16 instances)
+__global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(BlockArgs a) {
   constexpr int K = 2 * DMAX + 2;   // G[DMAX], H[DMAX], V/S, spare
   constexpr int WMAX = 64;
   __shared__ double s_lam[2 * DMAX];
