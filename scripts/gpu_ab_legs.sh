@@ -11,8 +11,14 @@ if [ -n "${TESTS:-}" ]; then
     > gpurun_out/pytest_ab.log 2>&1
   rc=$?; tail -3 gpurun_out/pytest_ab.log; [ $rc -ne 0 ] && exit $rc
 fi
+# rounds alternate the order (A B, B A, ...): the second process of a back-to-back pair
+# measured ~0.15-0.2 us/step slower on the headline with identical libraries
+# (profiles/r03/headline_host/ab_position_bias.log)
+LIBS_FWD=${LIBS:-base new}
+LIBS_REV=$(echo $LIBS_FWD | awk '{for (i = NF; i > 0; i--) printf "%s ", $i}')
 for i in $(seq 1 ${ROUNDS:-3}); do
-  for L in ${LIBS:-base new}; do
+  if [ $((i % 2)) -eq 1 ]; then ORDER=$LIBS_FWD; else ORDER=$LIBS_REV; fi
+  for L in $ORDER; do
     lib=$PWD/viabel_amd/libviabel_amd_$L.so; [ "$L" = new ] && lib=$PWD/viabel_amd/libviabel_amd.so
     VIABEL_AMD_LIB=$lib timeout -k 10 200 python bench.py --legs ${LEGS:-cfg1,cfg2,cfg5} --no-cpu-baseline \
       --steps 20 --warmup 5 > gpurun_out/ab_legs.json 2> gpurun_out/ab_legs.err || exit $?
