@@ -943,12 +943,14 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
     VB_PH(3);
     if (rows) wave_reduce_scatter<K>(acc, s_red[wid]);
     __syncthreads();
-    if (RO != 2 && tid < K) {
-      double t = s_red[0][tid];
-      for (int q = 1; q < RW; ++q) t += s_red[q][tid];
-      s_red[0][tid] = t;  // each thread only touches its own column
-    }
-    __syncthreads();
+    // block total of column k: the row waves' rows summed in order by each reader
+    // (the update threads and the value thread read their own columns, so no
+    // separate column pass and barrier)
+    auto colsum = [&](int k) {
+      double t = s_red[0][k];
+      for (int q = 1; q < RW; ++q) t += s_red[q][k];
+      return t;
+    };
     VB_PH(4);
 
     // gradient + update: thread p owns parameter p (wave 0, a row wave)
@@ -956,12 +958,12 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
       const int p = tid;
       double gp;
       if (!a.chivi) {
-        gp = p < D ? -(s_red[0][p] / dN)
-                   : -(1.0 + s_sg[p - D] * (s_red[0][DMAX + (p - D)] / dN));
+        gp = p < D ? -(colsum(p) / dN)
+                   : -(1.0 + s_sg[p - D] * (colsum(DMAX + (p - D)) / dN));
       } else {
-        const double Ssum = s_red[0][2 * DMAX];
-        gp = p < D ? a.alpha * s_red[0][p] / dN
-                   : a.alpha * (s_sg[p - D] * s_red[0][DMAX + (p - D)] + Ssum) / dN;
+        const double Ssum = colsum(2 * DMAX);
+        gp = p < D ? a.alpha * colsum(p) / dN
+                   : a.alpha * (s_sg[p - D] * colsum(DMAX + (p - D)) + Ssum) / dN;
       }
       if (a.emit_grad) {
         a.grad[(long long)prob * P + p] = gp;
@@ -1011,9 +1013,10 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
       double val;
       if (!a.chivi) {
         // entropy uses the pre-update lam: sum_d log sigma_d
-        val = a.pd ? -(s_red[0][2 * DMAX] / dN) : -(c0 + sl + s_red[0][2 * DMAX] / dN);
+        const double st = colsum(2 * DMAX);
+        val = a.pd ? -(st / dN) : -(c0 + sl + st / dN);
       } else {
-        val = log(s_red[0][2 * DMAX] / dN) / a.alpha + M;
+        val = log(colsum(2 * DMAX) / dN) / a.alpha + M;
       }
       a.values[(long long)prob * a.n_iters + (a.emit_grad ? 0 : i)] = val;
     }
@@ -1040,9 +1043,9 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
     // that step's last barrier), then join the step's barriers -- raw s_barrier:
     // __syncthreads' release fence would wait for the new prefetch (vmcnt(0))
     // and hold every wave at the step's first barrier.  The count matches the
-    // row waves' step: the CHIVI max barrier, the two reduction barriers and the
+    // row waves' step: the CHIVI max barrier, the reduction barrier and the
     // end-of-step barrier.
-    const int nbar = a.chivi ? 4 : 3;
+    const int nbar = a.chivi ? 3 : 2;
     for (int s = 0; s < a.n_steps; ++s) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (s + 2 < a.n_steps) pf_issue(s + 2);
@@ -1122,16 +1125,15 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
     }
     if (row_wave) wave_reduce_scatter<K>(acc, s_red[wid]);
     __syncthreads();
-    if (tid < K) {
-      double u = s_red[0][tid];
-      for (int q = 1; q < RW; ++q) u += s_red[q][tid];
-      s_red[0][tid] = u;
-    }
-    __syncthreads();
+    auto colsum = [&](int k) {   // as block_kernel: each reader sums its column
+      double u = s_red[0][k];
+      for (int q = 1; q < RW; ++q) u += s_red[q][k];
+      return u;
+    };
     if (tid < P) {
       const int p = tid;
-      const double gp = p < D ? -(s_red[0][p] / dN)
-                              : -(1.0 + s_sg[p - D] * (s_red[0][DMAX + (p - D)] / dN));
+      const double gp = p < D ? -(colsum(p) / dN)
+                              : -(1.0 + s_sg[p - D] * (colsum(DMAX + (p - D)) / dN));
       s_ring[slot * P + p] = gp;
       const int cnt = (s + 1 < W) ? s + 1 : W;
       const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;
@@ -1146,7 +1148,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
       s_lam[p] = nl;
       if (p >= D) s_sg[p - D] = exp(nl);
     }
-    if (tid == (NT > 64 ? NT - 64 : 0)) val += chivi ? log(s_red[0][2 * DMAX] / dN) + M : s_red[0][2 * DMAX];
+    if (tid == (NT > 64 ? NT - 64 : 0)) val += chivi ? log(colsum(2 * DMAX) / dN) + M : colsum(2 * DMAX);
     slot = slot + 1 == W ? 0 : slot + 1;
     __syncthreads();
   }
