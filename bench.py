@@ -254,9 +254,8 @@ def run_cfg3(torch, stream, dev, n, steps, warmup, rank, dist):
         run.advance_philox(cs, seed, strm, warmup + done)
         done += cs
     torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    # no closing barrier: every rank stops its own clock when its work is done, and
+    # the MAX all-reduce below gives the job's wall time from the aligned start
     elapsed = time.perf_counter() - t0
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_device(dev))
@@ -329,6 +328,35 @@ def leg_cfg3_n256(torch, stream, dev, traffic, steps=2048, warmup=64):
             'steps': steps, 'warmup': warmup, 'ms_per_step': elapsed / steps * 1e3,
             'value': steps * n * D / elapsed, 'unit': 'MC-samples/s', 'roofline': roof,
             'valu': valu}
+
+
+def measure_peaks():
+    """the roofline peaks confirmed with microbenchmarks on this box
+    (vb_peak_probe, best of 5 launches each): HBM copy and read over 1 GiB buffers
+    (4x the Infinity Cache), the fp64 MFMA loop, and the VALU issue rate of fp64
+    FMA and u64 multiply chains (4 waves per SIMD)."""
+    from viabel_amd import _native as nat
+    out = {}
+    for k, n in (('hbm_copy', 1 << 30), ('hbm_read', 1 << 30), ('mfma_f64', 20000),
+                 ('valu_fma_f64', 20000), ('valu_mad_u64', 20000)):
+        try:
+            out[k] = nat.peak_probe(k, n)
+        except Exception as e:      # reported, never hidden
+            out[k] = None
+            out[k + '_error'] = str(e)
+    out['units'] = {'hbm_copy': 'GB/s (read + written)', 'hbm_read': 'GB/s', 'mfma_f64': 'TFLOP/s',
+                    'valu_fma_f64': 'G wave-instr/s', 'valu_mad_u64': 'G wave-instr/s'}
+    out['source'] = 'vb_peak_probe (viabel_amd/csrc/vb_probe.hip), measured in this run'
+    return out
+
+
+def add_measured(roof, measured, key):
+    """frac against the measured peak beside the spec one."""
+    m = measured.get(key) if measured else None
+    if roof and m and roof.get('achieved'):
+        roof['measured_peak'] = m
+        roof['measured_peak_source'] = key
+        roof['frac_of_measured_peak'] = roof['achieved'] / m
 
 
 def _sync():
@@ -779,6 +807,15 @@ def main():
             print('[bench] leg %s done in %.1f s' % (leg, configs[leg]['leg_seconds']),
                   file=sys.stderr, flush=True)
 
+    measured = measure_peaks() if rank == 0 else None
+    add_measured(roof, measured, 'hbm_copy')
+    if valu and measured and measured.get('valu_fma_f64'):
+        valu['measured_fma_f64_peak'] = measured['valu_fma_f64']
+        valu['frac_of_measured_fma_f64_peak'] = valu['achieved'] / measured['valu_fma_f64']
+    for leg, key in (('cfg3_256', 'hbm_copy'), ('cfg4', 'mfma_f64'), ('cfg5', 'hbm_copy')):
+        if isinstance(configs.get(leg), dict):
+            add_measured(configs[leg].get('roofline'), measured, key)
+
     if rank == 0:
         line = {
             'metric': METRIC,
@@ -792,6 +829,7 @@ def main():
                        'parallelism': 'restarts sharded 1/GPU, RCCL all_gather of summaries'},
             'roofline': roof,
             'valu': valu,
+            'measured_peaks': measured,
             'restart_summaries': gathered.tolist(),
         }
         if cpu:

@@ -215,6 +215,16 @@ int vb_run_create(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,
  * [n_problems][n_steps][N][D]. */
 int vb_run_advance(vb_run* run, int64_t n_steps, const vb_noise* noise);
 int vb_run_steps_done(vb_run* run, int64_t* out);
+/* Full-rank runs (measurement / test support, no reference counterpart): how many
+ * advances ran again because a warm Newton-Schulz root launched too few
+ * iterations (the rerun restores lambda, the adagrad window and the warm state). */
+int vb_run_fr_retries(vb_run* run, int64_t* out);
+/* Peak-rate microbenchmarks (measurement support, no reference counterpart;
+ * BASELINE.md §2 asks for the roofline peaks to be confirmed on the box): kind 0
+ * HBM copy and 1 HBM read over n bytes (GB/s of bytes moved), 2 fp64 MFMA
+ * (TFLOP/s), 3 fp64 FMA and 4 u64 multiply VALU issue (G wave-instructions/s)
+ * over n iterations; best of reps timed launches on the context's stream. */
+int vb_peak_probe(vb_ctx* ctx, int32_t kind, int64_t n, int32_t reps, double* out);
 /* Launch timing (measurement support, no reference counterpart): with enable
  * != 0 every later vb_run_advance brackets its device work with HIP events on
  * the context's stream, one pair per kernel chunk (column-pair path) or per

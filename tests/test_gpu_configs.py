@@ -91,6 +91,47 @@ def test_config1_numpy_stream_5000_steps():
 
 
 # ---------------------------------------------------------------------------
+# config 2
+@pytest.mark.parametrize('predraw', ['', '0'])
+def test_config2_philox_1100_steps(monkeypatch, predraw):
+    """Config 2's exact path (funnel D = 10, mf-t(40), CHIVI alpha = 2, N = 128,
+    Philox, lr .01 -> .001) through adagrad_optimize as the bench runs it:
+    1 100 steps = advances of 1 000 + 100, the pre-draw kernel's 512-step chunks
+    (two boundaries) and many wraps of the copy wave's 3-slot LDS ring, against
+    the oracle's adagrad on the C oracle's draws: values, history and the
+    result to 1e-7.  VIABEL_AMD_PREDRAW=0: the in-kernel t draw waves instead."""
+    from viabel_amd import vb, targets
+    from oracle import vb_oracle as vo, rng_oracle as ro
+    if predraw:
+        monkeypatch.setenv('VIABEL_AMD_PREDRAW', predraw)
+    else:
+        monkeypatch.delenv('VIABEL_AMD_PREDRAW', raising=False)
+    Dm, N, iters = 10, 128, 1100
+    lam0 = np.concatenate([np.zeros(Dm), np.ones(Dm)])
+    lam0[1] = -1.0
+    fam = vb.mean_field_t_variational_family(Dm, 40.0, rng='philox')
+    obj = vb.black_box_chivi(2.0, fam, targets.funnel(Dm), N)
+    seed, stream, step0 = fam.seed, fam.stream, fam.step
+    sm, hist, vals, _ = vb.adagrad_optimize(iters, obj, lam0, learning_rate=.01,
+                                            learning_rate_end=.001)
+    assert fam.step == step0 + iters
+
+    ofam = vo.Family('t', Dm, 40.0)
+    step = [0]
+
+    def f(lam):
+        eps = ro.noise(seed, stream, step0 + step[0], N, Dm, 't', 40.0)
+        step[0] += 1
+        return vo.chivi_value_grad(ofam, 'funnel', lam, N, 2.0, eps=eps)
+    osm, ohist, ovals, _ = vo.adagrad_optimize(iters, f, lam0, learning_rate=.01,
+                                               learning_rate_end=.001)
+    assert hist.shape == ohist.shape
+    np.testing.assert_allclose(vals, ovals, rtol=1e-7, atol=1e-7)
+    _close(hist, ohist, 1e-7)
+    _close(sm, osm, 1e-7)
+
+
+# ---------------------------------------------------------------------------
 # config 4
 def _cfg4_problem():
     Dm = 512
@@ -141,6 +182,30 @@ def test_config4_1000_steps_one_advance():
                                  draws=ro.fr_noise(seed, fam.stream, 0, N, Dm, 100.0))
     assert abs(v - ov) <= 1e-7 * max(1.0, abs(ov)), (v, ov)
     _close(g, og, 1e-7)
+
+
+def test_config4_120_step_trajectory_vs_oracle():
+    """Config 4 (the bench's workload: D = 512, df 100, CHIVI alpha 2, N = 128,
+    corr_gauss, Philox seed 0 stream 1) for 120 steps in advances of 50 + 70, with
+    the warm Newton-Schulz counts and the warm PCG tolerance (relative residual
+    1e-8) the optimisation path uses, against the oracle's trajectory on the same
+    draws (scipy sqrtm + solve_sylvester, tests/golden/cfg4_trajectory.npz made by
+    make_cfg4_trajectory.py): every step's value and lambda at every third of the
+    last 30 steps (sampled entries) to 1e-7."""
+    import os
+    from viabel_amd import vb, targets
+    g = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'cfg4_trajectory.npz'))
+    n_iters = int(g['n_iters'])
+    Dm, lam0 = _cfg4_problem()
+    fam = vb.t_variational_family(Dm, 100.0, rng='philox')
+    obj = vb.black_box_chivi(2.0, fam, targets.corr_gauss(Dm), 128)
+    run = vb.DeviceRun(obj, n_iters, lam0, window=10, learning_rate=0.01, epsilon=0.1)
+    run.advance_philox(50, 0, 1, 0)
+    run.advance_philox(n_iters - 50, 0, 1, 50)
+    lam, hist, vals, _ = run.result()
+    np.testing.assert_allclose(vals[0], g['values'], rtol=1e-7, atol=1e-7)
+    _close(hist[0][g['tail_rows']][:, g['index']], g['tail'], 1e-7)
+    _close(lam[0][g['index']], g['tail'][-1], 1e-7)
 
 
 # ---------------------------------------------------------------------------

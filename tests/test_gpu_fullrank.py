@@ -271,17 +271,32 @@ def test_newton_schulz_retry_when_the_learnt_count_is_short(monkeypatch):
     that needs more makes the advance restore its snapshot (lambda, adagrad
     window) and run again with a larger count (vb_capi.hip vb_run_advance,
     vb_fr.hip fr_info).  Forced here by starting warm roots at 3 iterations: the
-    trajectory still equals the oracle's."""
+    retry counter shows the rerun happened, the trajectory equals the unforced
+    run's bit for bit and the oracle's to 1e-7."""
     vb, targets, fo, ro, vo = _mods()
-    monkeypatch.setenv('VIABEL_AMD_FR_NS_START', '3')
     D, N, n_iters = 64, 16, 9
     lam0 = _lam(D, 11)
-    fam = vb.t_variational_family(D, 30.0, rng='philox')
-    obj = vb.black_box_chivi(2.0, fam, targets.corr_gauss(D), N)
-    run = vb.DeviceRun(obj, n_iters, lam0, learning_rate=0.02)
-    run.advance_philox(6, 2, 4, 0)
-    run.advance_philox(3, 2, 4, 6)
-    lam, hist, vals, _ = run.result()
+
+    def device_run():
+        fam = vb.t_variational_family(D, 30.0, rng='philox')
+        obj = vb.black_box_chivi(2.0, fam, targets.corr_gauss(D), N)
+        run = vb.DeviceRun(obj, n_iters, lam0, learning_rate=0.02)
+        run.advance_philox(6, 2, 4, 0)
+        run.advance_philox(3, 2, 4, 6)
+        return run.fr_retries(), run.result()
+
+    # the unforced run: warm roots start from the default count
+    n_plain, (lam_p, hist_p, vals_p, _) = device_run()
+    monkeypatch.setenv('VIABEL_AMD_FR_NS_START', '3')
+    retries, (lam, hist, vals, _) = device_run()
+    assert retries > 0, 'the forced short count did not make an advance run again'
+    # the rerun restores lambda, the window AND the warm state (previous root,
+    # power vectors, schedule block): it is the run that would have happened
+    # with the larger count, bit for bit (iterations past convergence are
+    # skipped on the device, so the launched count does not change the bits)
+    assert np.array_equal(vals[0], vals_p[0]), np.max(np.abs(vals[0] - vals_p[0]))
+    assert np.array_equal(hist[0], hist_p[0]), np.max(np.abs(hist[0] - hist_p[0]))
+    assert np.array_equal(lam[0], lam_p[0])
     ofam = fo.FullRankT(D, 30.0)
     otgt = fo.target_fn('corr_gauss', D)
     step = [0]
@@ -291,6 +306,43 @@ def test_newton_schulz_retry_when_the_learnt_count_is_short(monkeypatch):
         step[0] += 1
         return fo.chivi_value_grad(ofam, otgt, l, N, 2.0, draws=draws)
     osm, ohist, ovals, _ = vo.adagrad_optimize(n_iters, f, lam0, learning_rate=0.02)
+    _close(vals[0], ovals, 1e-7)
+    _close(hist[0], ohist, 1e-7)
+    _close(lam[0], ohist[-1], 1e-7)
+
+
+def test_ill_conditioned_sigma_trajectory():
+    """Warm PCG steps stop at a relative residual of 1e-8, tightened by kappa / 2
+    once the preconditioned condition number kappa = (2 + k + 1/k) / 4 (k =
+    cond(S)) passes 2 (vb_fr.hip fr_sched_kernel, FrSched::ee_scale).  Sigma with
+    cond ~1e4 (log-diagonal of L spread over [-2.3, 2.3]: k ~ 100, kappa ~ 25):
+    the adagrad trajectory still equals the oracle's (scipy sqrtm +
+    solve_sylvester) to 1e-7."""
+    vb, targets, fo, ro, vo = _mods()
+    D, N, n_iters = 64, 32, 12
+    rs = np.random.RandomState(21)
+    tri = np.tril_indices(D)
+    free = rs.randn(len(tri[0])) * 0.01
+    free[tri[0] == tri[1]] = np.linspace(-2.3, 2.3, D)[rs.permutation(D)]
+    lam0 = np.concatenate([rs.randn(D) * 0.3, free])
+    _, _, Sig = fo.unpack(lam0, D)
+    ev = np.linalg.eigvalsh(Sig)
+    assert ev[-1] / ev[0] > 5e3
+    fam = vb.t_variational_family(D, 30.0, rng='philox')
+    obj = vb.black_box_chivi(2.0, fam, targets.corr_gauss(D), N)
+    run = vb.DeviceRun(obj, n_iters, lam0, learning_rate=0.01)
+    run.advance_philox(8, 6, 2, 0)
+    run.advance_philox(4, 6, 2, 8)
+    lam, hist, vals, _ = run.result()
+    ofam = fo.FullRankT(D, 30.0)
+    otgt = fo.target_fn('corr_gauss', D)
+    step = [0]
+
+    def f(l):
+        draws = ro.fr_noise(6, 2, step[0], N, D, 30.0)
+        step[0] += 1
+        return fo.chivi_value_grad(ofam, otgt, l, N, 2.0, draws=draws)
+    osm, ohist, ovals, _ = vo.adagrad_optimize(n_iters, f, lam0, learning_rate=0.01)
     _close(vals[0], ovals, 1e-7)
     _close(hist[0], ohist, 1e-7)
     _close(lam[0], ohist[-1], 1e-7)

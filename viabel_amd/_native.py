@@ -82,6 +82,9 @@ _SIGNATURES = {
                        ctypes.c_int64, c_double_p, P(ctypes.c_void_p)], ctypes.c_int),
     'vb_run_advance': ([ctypes.c_void_p, ctypes.c_int64, P(Noise)], ctypes.c_int),
     'vb_run_steps_done': ([ctypes.c_void_p, c_int64_p], ctypes.c_int),
+    'vb_run_fr_retries': ([ctypes.c_void_p, c_int64_p], ctypes.c_int),
+    'vb_peak_probe': ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+                       c_double_p], ctypes.c_int),
     'vb_run_set_timing': ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     'vb_run_launch_times': ([ctypes.c_void_p, ctypes.c_int64, c_int64_p,
                              P(ctypes.c_float), c_int64_p], ctypes.c_int),
@@ -311,4 +314,17 @@ def block_floor_us(D, N, chivi=False, host_layout=False, n_steps=2000, n_problem
     check(lib().vb_block_floor(context().handle, int(D), int(N), 1 if chivi else 0,
                                1 if host_layout else 0, int(n_steps), int(n_problems),
                                ctypes.byref(out)))
+    return out.value
+
+
+PROBE_KINDS = {'hbm_copy': 0, 'hbm_read': 1, 'mfma_f64': 2, 'valu_fma_f64': 3, 'valu_mad_u64': 4}
+
+
+def peak_probe(kind, n, reps=5):
+    """Measured peak of one resource (vb_peak_probe): 'hbm_copy' / 'hbm_read' over n
+    bytes (GB/s), 'mfma_f64' (TFLOP/s), 'valu_fma_f64' / 'valu_mad_u64' (G
+    wave-instructions/s) over n iterations; best of `reps` launches."""
+    out = ctypes.c_double()
+    check(lib().vb_peak_probe(context().handle, PROBE_KINDS[kind], int(n), int(reps),
+                              ctypes.byref(out)))
     return out.value

@@ -766,6 +766,7 @@ struct vb_run {
   vbk::MfSpec mspec{};
   DevBuf tparams, grad;
   DevBuf backup;  // full rank: lambda and the adagrad window at the start of an advance
+  long long fr_retries = 0;  // full rank: advances run again after a short warm root
   // launch timing (vb_run_set_timing): event pairs, reused; `ev_used` recorded
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
@@ -1007,29 +1008,37 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
     // advance run again when a warm Newton-Schulz root launched too few
     // iterations (they launch exactly the learnt count, no spares; vb_fr.hip
     // fr_info)
+    // (and the workspace's warm state: the rerun's first step starts from the
+    // same previous root, power vectors and schedule as the failed pass did)
     const bool snap = r->fr && r->nprob == 1;
     const size_t snap_n = P + P * (size_t)r->W;
+    vbk::FrWork* W = nullptr;
+    if (r->fr) VB_TRY(fr_work(c, &W));
     if (snap) {
       VB_TRY(r->backup.reserve(snap_n * sizeof(double)));
       VB_HIP(hipMemcpyAsync(r->backup.d(), r->lam.d(), P * sizeof(double), hipMemcpyDeviceToDevice,
                             c->stream));
       VB_HIP(hipMemcpyAsync(r->backup.d() + P, r->ring.d(), P * r->W * sizeof(double),
                             hipMemcpyDeviceToDevice, c->stream));
+      if (int rc = vbk::fr_warm_save(W, c->stream)) return rc;
     }
-    VB_TRY(advance_fr_steps(c, r, n_steps, noise, host, noise_base, per_step, k0, k1));
-    if (r->fr) {
+    for (bool rerun = false;; rerun = true) {
+      VB_TRY(advance_fr_steps(c, r, n_steps, noise, host, noise_base, per_step, k0, k1));
+      if (!r->fr) break;
       VB_TRY(sync(c));
-      vbk::FrWork* W;
-      VB_TRY(fr_work(c, &W));
       bool again = false;
       if (int rc = vbk::fr_info(W, c->stream, snap ? &again : nullptr)) return rc;
-      if (again) {
-        VB_HIP(hipMemcpyAsync(r->lam.d(), r->backup.d(), P * sizeof(double),
-                              hipMemcpyDeviceToDevice, c->stream));
-        VB_HIP(hipMemcpyAsync(r->ring.d(), r->backup.d() + P, P * r->W * sizeof(double),
-                              hipMemcpyDeviceToDevice, c->stream));
-        VB_TRY(advance_fr_steps(c, r, n_steps, noise, host, noise_base, per_step, k0, k1));
+      if (!again) {
+        if (rerun) vbk::fr_retry_done(W);
+        break;
       }
+      // fr_info raised the count (bounded by kFrNSMax, then it reports an error)
+      ++r->fr_retries;
+      VB_HIP(hipMemcpyAsync(r->lam.d(), r->backup.d(), P * sizeof(double),
+                            hipMemcpyDeviceToDevice, c->stream));
+      VB_HIP(hipMemcpyAsync(r->ring.d(), r->backup.d() + P, P * r->W * sizeof(double),
+                            hipMemcpyDeviceToDevice, c->stream));
+      if (int rc = vbk::fr_warm_restore(W, c->stream)) return rc;
     }
   } else if (r->sep) {
     ht0.mark();
@@ -1204,9 +1213,22 @@ int vb_block_floor(vb_ctx* c, int32_t D, int32_t N, int32_t chivi, int32_t host_
   return VB_OK;
 }
 
+int vb_peak_probe(vb_ctx* c, int32_t kind, int64_t n, int32_t reps, double* out) {
+  VB_TRY(check_ctx(c));
+  if (!out) return fail(VB_EINVAL, "null output pointer");
+  if (int rc = vbk::probe_rate(kind, (long long)n, reps, c->stream, out)) return rc;
+  return VB_OK;
+}
+
 int vb_run_steps_done(vb_run* r, int64_t* out) {
   if (!r || !out) return fail(VB_EINVAL, "null argument");
   *out = r->done;
+  return VB_OK;
+}
+
+int vb_run_fr_retries(vb_run* r, int64_t* out) {
+  if (!r || !out) return fail(VB_EINVAL, "null argument");
+  *out = r->fr_retries;
   return VB_OK;
 }
 

@@ -439,6 +439,8 @@ struct FrSched {
   double inv_a4[kFrNSMax + 1];   // 1 / a_k^4 (residual scale)
   double rz[2], ee;              // PCG: <R, M^-1 R> (by iteration parity), ||E||^2
   double l0, lmax_est;
+  double ee_scale;               // PCG: (2 / kappa)^2 when the preconditioned condition
+                                 // number kappa > 2, else 1 (see fr_sched_kernel)
   int ns_conv, ns_iter, pcg_done, pcg_iter;
   int ns_fin;                    // the last Newton-Schulz update was final (see fr_sqrt)
   int status;                    // sticky: 1 NS not converged, 2 PCG not converged
@@ -529,10 +531,21 @@ __global__ __launch_bounds__(1024) void fr_sched_kernel(int D, int kmax, const d
   const double lmax = qf_part ? (ly > 0.0 ? qf / ly : 0.0) : sqrt(ly);
   const double c = fmin(1.25 * lmax, sqrt(f));   // ||Sigma||_F >= lambda_max
   double l = l_default;
+  double ee_scale = 1.0;
   if (has_z && lv > 0.0) {
     const double lmin = sc->c_prev / lv;        // lambda_min(Sigma_prev)
     l = 0.8 * sqrt(lmin / c);
+    // the PCG's X carries up to kappa x its relative residual, kappa = (2 + k +
+    // 1/k) / 4 the preconditioned condition number, k = cond(S) = sqrt(lmax /
+    // lmin): past kappa = 2 the stopping test tightens by kappa / 2, so X's
+    // relative error stays <= 2 x the tolerance however ill-conditioned Sigma is
+    // (config 4: kappa ~1.2, unchanged)
+    if (lmin > 0.0 && lmax > lmin) {
+      const double k = sqrt(lmax / lmin), kap = 0.25 * (2.0 + k + 1.0 / k);
+      if (kap > 2.0) ee_scale = 4.0 / (kap * kap);
+    }
   }
+  sc->ee_scale = ee_scale;
   l = fmin(fmax(l, 1e-4), 1.0);
   sc->l0 = l;
   sc->lmax_est = lmax;
@@ -862,7 +875,7 @@ __global__ __launch_bounds__(256) void pcg_p_kernel(int D, int it, const double*
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     sc->rz[(it + 1) & 1] = rz;
-    if (it < 0) sc->ee = ee;
+    if (it < 0) sc->ee = ee * sc->ee_scale;
   }
 }
 
@@ -918,6 +931,15 @@ struct FrWork {
   long long prep_step = -1;
   uint32_t prep_k0 = 0, prep_k1 = 0, prep_stream = 0;
   Buf uS, uZ, pS, pz, ypart, lp_part;
+  // fr_warm_save / fr_warm_restore: the warm state an advance starts from
+  // (device: uS, uZ, pv[0..3], the previous root Z, the schedule block; host:
+  // the flags below), so an advance that runs again starts where it started
+  Buf wsnap;
+  struct WarmHost {
+    bool warm, have_z, zv_init, last_hz, valid;
+    int pv_cur, zf_slot;
+    const void* owner;
+  } wsnap_h{};
   // N x D / N
   Buf Z, X, G, s, logp, zz, r, rk;
   // pinned host staging for host-callback targets
@@ -1814,6 +1836,63 @@ int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, 
     if (int rc = fr_prepare(W, D, lam, st)) return rc;
     FR_HIP(hipMemcpyAsync(eig, W->w.d(), sizeof(double) * D, hipMemcpyDeviceToDevice, st));
   }
+  return 0;
+}
+
+// Snapshot of the warm state a run's next advance starts from (its first step
+// reads the previous root Z, the power vectors and the schedule block), taken on
+// the stream before the advance; fr_warm_restore puts it back, so a rerun
+// (vb_run_advance after a short warm root) starts from the same state as the
+// failed pass did, not from where that pass ended.
+int fr_warm_save(FrWork* W, hipStream_t st) {
+  W->wsnap_h = FrWork::WarmHost{W->warm, W->have_z, W->zv_init, W->last_hz, false, W->pv_cur, -1,
+                                W->owner};
+  if (W->D == 0 || !W->sched.p) return 0;   // nothing warm yet: the first step is cold
+  const size_t D = (size_t)W->D, vec = sizeof(double) * D;
+  FR_HIP(W->wsnap.reserve(6 * vec + vec * D + sizeof(FrSched)));
+  char* p = static_cast<char*>(W->wsnap.p);
+  const FrWork::Buf* v[6] = {&W->uS, &W->uZ, &W->pv[0], &W->pv[1], &W->pv[2], &W->pv[3]};
+  for (int i = 0; i < 6; ++i)
+    FR_HIP(hipMemcpyAsync(p + i * vec, v[i]->p, vec, hipMemcpyDeviceToDevice, st));
+  if (W->have_z && W->Zf) {
+    W->wsnap_h.zf_slot = W->Zf == W->Zb[0].d() ? 0 : 1;
+    FR_HIP(hipMemcpyAsync(p + 6 * vec, W->Zf, vec * D, hipMemcpyDeviceToDevice, st));
+  }
+  FR_HIP(hipMemcpyAsync(p + 6 * vec + vec * D, W->sched.p, sizeof(FrSched),
+                        hipMemcpyDeviceToDevice, st));
+  W->wsnap_h.valid = true;
+  return 0;
+}
+
+void fr_retry_done(FrWork* W) { W->retry_kmax = 0; }
+
+int fr_warm_restore(FrWork* W, hipStream_t st) {
+  const FrWork::WarmHost h = W->wsnap_h;
+  W->warm = h.warm;
+  W->have_z = h.have_z;
+  W->zv_init = h.zv_init;
+  W->last_hz = h.last_hz;
+  W->pv_cur = h.pv_cur;
+  W->owner = h.owner;
+  W->prep_owner = nullptr;
+  if (!h.valid) {
+    W->warm = false;
+    return 0;
+  }
+  const size_t D = (size_t)W->D, vec = sizeof(double) * D;
+  const char* p = static_cast<const char*>(W->wsnap.p);
+  FrWork::Buf* v[6] = {&W->uS, &W->uZ, &W->pv[0], &W->pv[1], &W->pv[2], &W->pv[3]};
+  for (int i = 0; i < 6; ++i)
+    FR_HIP(hipMemcpyAsync(v[i]->p, p + i * vec, vec, hipMemcpyDeviceToDevice, st));
+  if (h.zf_slot >= 0) {
+    W->Zf = W->Zb[h.zf_slot].d();
+    FR_HIP(hipMemcpyAsync(W->Zb[h.zf_slot].p, p + 6 * vec, vec * D, hipMemcpyDeviceToDevice, st));
+  }
+  // the schedule block, then its sticky status / hint words cleared (fr_info
+  // clears them after every read-back)
+  FR_HIP(hipMemcpyAsync(W->sched.p, p + 6 * vec + vec * D, sizeof(FrSched),
+                        hipMemcpyDeviceToDevice, st));
+  FR_HIP(hipMemsetAsync(&static_cast<FrSched*>(W->sched.p)->status, 0, 5 * sizeof(int), st));
   return 0;
 }
 

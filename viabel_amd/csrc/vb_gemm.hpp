@@ -748,6 +748,11 @@ inline hipError_t gemm_group(const GemmOp* ops, int n, hipStream_t s) {
     if (!sym_on) gg.op[i].sym = 0;
   }
   if (gg.op[0].sym && g.M != g.N) return hipErrorInvalidValue;
+  // the grid follows op[0]: a group is all-symmetric or all-full, and the row
+  // partials (rp_*) are not mirrored into the lower triangle of a sym product
+  for (int i = 0; i < n; ++i)
+    if (gg.op[i].sym != gg.op[0].sym || (gg.op[i].sym && gg.op[i].rp_part))
+      return hipErrorInvalidValue;
   const unsigned ntn = (unsigned)((g.N + BT - 1) / BT);
   const dim3 grid = gg.op[0].sym ? dim3(ntn * (ntn + 1) / 2, 1, (unsigned)n)
                           : dim3(ntn, (unsigned)((g.M + BT - 1) / BT), (unsigned)n);

@@ -269,6 +269,17 @@ int mf_wide_log_weights(FrWork* W, const MfSpec& f, const double* lam, long long
 // retry (non-null): a warm Newton-Schulz root that did not converge sets *retry,
 // raises the learnt count and returns 0 (the caller runs the steps again).
 int fr_info(FrWork* W, hipStream_t st, bool* retry = nullptr);
+// Warm state of the next full-rank step (previous root, power vectors, schedule
+// block): saved before a run's advance, restored when the advance runs again.
+// Peak-rate microbenchmarks (vb_probe.hip): kind 0 HBM copy / 1 HBM read (GB/s,
+// n bytes), 2 fp64 MFMA (TFLOP/s), 3 fp64 FMA / 4 u64 multiply VALU issue (G
+// wave-instructions/s; n iterations).
+int probe_rate(int kind, long long n, int reps, hipStream_t st, double* out);
+int fr_warm_save(FrWork* W, hipStream_t st);
+int fr_warm_restore(FrWork* W, hipStream_t st);
+// Clears the Newton-Schulz floor a rerun set (the rerun's own warm steps have
+// taught fr_info the count they need).
+void fr_retry_done(FrWork* W);
 hipError_t launch_fr_lw(int D, long long m, double df, double t_const, const double* logp,
                         const double* zz, const double* s, const double* scal, double* lw,
                         hipStream_t st);

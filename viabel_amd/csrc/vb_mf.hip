@@ -553,18 +553,145 @@ constexpr int kBlockMaxRowWaves = 4;
 constexpr int kBlockPfLds = 4608;    // doubles of LDS for the 3-slot ring (36 KB)
 constexpr int kPfUnit = 128;         // doubles per wave-wide 16-byte DMA instruction
 
-// e[I] = LDS double at addr + 8 I (inline-asm reads with immediate offsets)
-template <int I>
-__device__ __forceinline__ double lds_ld_off(unsigned addr) {
-  double t;
-  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(t) : "v"(addr), "i"(8 * I));
-  return t;
-}
-template <int DMAX, int... Is>
-__device__ __forceinline__ void lds_row(unsigned addr, double (&e)[DMAX],
-                                        std::integer_sequence<int, Is...>) {
-  ((e[Is] = lds_ld_off<Is>(addr)), ...);
-}
+// Row reads of the copy wave's ring: DMAX ds_read_b64 at immediate offsets from
+// one row address [+ the row's log q partial], and the lgkmcnt(0) wait, in ONE
+// asm statement.  Every destination is an output of the statement that also
+// waits, so the compiler cannot copy or spill a register whose LDS load is still
+// in flight (the hardware has no interlock for that).  Generated per DMAX
+// instance (2, 4, 10, 16) with and without the log q read.
+template <int DMAX> struct LdsRowWait;
+template <> struct LdsRowWait<2> {
+  static __device__ __forceinline__ void run(unsigned a, unsigned q, bool lq, double (&e)[2],
+                                               double& tl) {
+    if (lq) {
+      asm volatile("ds_read_b64 %[e0], %[a] offset:0\n"
+                   "ds_read_b64 %[e1], %[a] offset:8\n"
+                   "ds_read_b64 %[t], %[q]\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : [e0] "=&v"(e[0]), [e1] "=&v"(e[1]), [t] "=&v"(tl)
+                   : [a] "v"(a), [q] "v"(q)
+                   : "memory");
+    } else {
+      asm volatile("ds_read_b64 %[e0], %[a] offset:0\n"
+                   "ds_read_b64 %[e1], %[a] offset:8\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : [e0] "=&v"(e[0]), [e1] "=&v"(e[1])
+                   : [a] "v"(a)
+                   : "memory");
+    }
+  }
+};
+template <> struct LdsRowWait<4> {
+  static __device__ __forceinline__ void run(unsigned a, unsigned q, bool lq, double (&e)[4],
+                                               double& tl) {
+    if (lq) {
+      asm volatile("ds_read_b64 %[e0], %[a] offset:0\n"
+                   "ds_read_b64 %[e1], %[a] offset:8\n"
+                   "ds_read_b64 %[e2], %[a] offset:16\n"
+                   "ds_read_b64 %[e3], %[a] offset:24\n"
+                   "ds_read_b64 %[t], %[q]\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : [e0] "=&v"(e[0]), [e1] "=&v"(e[1]), [e2] "=&v"(e[2]), [e3] "=&v"(e[3]), [t] "=&v"(tl)
+                   : [a] "v"(a), [q] "v"(q)
+                   : "memory");
+    } else {
+      asm volatile("ds_read_b64 %[e0], %[a] offset:0\n"
+                   "ds_read_b64 %[e1], %[a] offset:8\n"
+                   "ds_read_b64 %[e2], %[a] offset:16\n"
+                   "ds_read_b64 %[e3], %[a] offset:24\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : [e0] "=&v"(e[0]), [e1] "=&v"(e[1]), [e2] "=&v"(e[2]), [e3] "=&v"(e[3])
+                   : [a] "v"(a)
+                   : "memory");
+    }
+  }
+};
+template <> struct LdsRowWait<10> {
+  static __device__ __forceinline__ void run(unsigned a, unsigned q, bool lq, double (&e)[10],
+                                               double& tl) {
+    if (lq) {
+      asm volatile("ds_read_b64 %[e0], %[a] offset:0\n"
+                   "ds_read_b64 %[e1], %[a] offset:8\n"
+                   "ds_read_b64 %[e2], %[a] offset:16\n"
+                   "ds_read_b64 %[e3], %[a] offset:24\n"
+                   "ds_read_b64 %[e4], %[a] offset:32\n"
+                   "ds_read_b64 %[e5], %[a] offset:40\n"
+                   "ds_read_b64 %[e6], %[a] offset:48\n"
+                   "ds_read_b64 %[e7], %[a] offset:56\n"
+                   "ds_read_b64 %[e8], %[a] offset:64\n"
+                   "ds_read_b64 %[e9], %[a] offset:72\n"
+                   "ds_read_b64 %[t], %[q]\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : [e0] "=&v"(e[0]), [e1] "=&v"(e[1]), [e2] "=&v"(e[2]), [e3] "=&v"(e[3]), [e4] "=&v"(e[4]), [e5] "=&v"(e[5]), [e6] "=&v"(e[6]), [e7] "=&v"(e[7]), [e8] "=&v"(e[8]), [e9] "=&v"(e[9]), [t] "=&v"(tl)
+                   : [a] "v"(a), [q] "v"(q)
+                   : "memory");
+    } else {
+      asm volatile("ds_read_b64 %[e0], %[a] offset:0\n"
+                   "ds_read_b64 %[e1], %[a] offset:8\n"
+                   "ds_read_b64 %[e2], %[a] offset:16\n"
+                   "ds_read_b64 %[e3], %[a] offset:24\n"
+                   "ds_read_b64 %[e4], %[a] offset:32\n"
+                   "ds_read_b64 %[e5], %[a] offset:40\n"
+                   "ds_read_b64 %[e6], %[a] offset:48\n"
+                   "ds_read_b64 %[e7], %[a] offset:56\n"
+                   "ds_read_b64 %[e8], %[a] offset:64\n"
+                   "ds_read_b64 %[e9], %[a] offset:72\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : [e0] "=&v"(e[0]), [e1] "=&v"(e[1]), [e2] "=&v"(e[2]), [e3] "=&v"(e[3]), [e4] "=&v"(e[4]), [e5] "=&v"(e[5]), [e6] "=&v"(e[6]), [e7] "=&v"(e[7]), [e8] "=&v"(e[8]), [e9] "=&v"(e[9])
+                   : [a] "v"(a)
+                   : "memory");
+    }
+  }
+};
+template <> struct LdsRowWait<16> {
+  static __device__ __forceinline__ void run(unsigned a, unsigned q, bool lq, double (&e)[16],
+                                               double& tl) {
+    if (lq) {
+      asm volatile("ds_read_b64 %[e0], %[a] offset:0\n"
+                   "ds_read_b64 %[e1], %[a] offset:8\n"
+                   "ds_read_b64 %[e2], %[a] offset:16\n"
+                   "ds_read_b64 %[e3], %[a] offset:24\n"
+                   "ds_read_b64 %[e4], %[a] offset:32\n"
+                   "ds_read_b64 %[e5], %[a] offset:40\n"
+                   "ds_read_b64 %[e6], %[a] offset:48\n"
+                   "ds_read_b64 %[e7], %[a] offset:56\n"
+                   "ds_read_b64 %[e8], %[a] offset:64\n"
+                   "ds_read_b64 %[e9], %[a] offset:72\n"
+                   "ds_read_b64 %[e10], %[a] offset:80\n"
+                   "ds_read_b64 %[e11], %[a] offset:88\n"
+                   "ds_read_b64 %[e12], %[a] offset:96\n"
+                   "ds_read_b64 %[e13], %[a] offset:104\n"
+                   "ds_read_b64 %[e14], %[a] offset:112\n"
+                   "ds_read_b64 %[e15], %[a] offset:120\n"
+                   "ds_read_b64 %[t], %[q]\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : [e0] "=&v"(e[0]), [e1] "=&v"(e[1]), [e2] "=&v"(e[2]), [e3] "=&v"(e[3]), [e4] "=&v"(e[4]), [e5] "=&v"(e[5]), [e6] "=&v"(e[6]), [e7] "=&v"(e[7]), [e8] "=&v"(e[8]), [e9] "=&v"(e[9]), [e10] "=&v"(e[10]), [e11] "=&v"(e[11]), [e12] "=&v"(e[12]), [e13] "=&v"(e[13]), [e14] "=&v"(e[14]), [e15] "=&v"(e[15]), [t] "=&v"(tl)
+                   : [a] "v"(a), [q] "v"(q)
+                   : "memory");
+    } else {
+      asm volatile("ds_read_b64 %[e0], %[a] offset:0\n"
+                   "ds_read_b64 %[e1], %[a] offset:8\n"
+                   "ds_read_b64 %[e2], %[a] offset:16\n"
+                   "ds_read_b64 %[e3], %[a] offset:24\n"
+                   "ds_read_b64 %[e4], %[a] offset:32\n"
+                   "ds_read_b64 %[e5], %[a] offset:40\n"
+                   "ds_read_b64 %[e6], %[a] offset:48\n"
+                   "ds_read_b64 %[e7], %[a] offset:56\n"
+                   "ds_read_b64 %[e8], %[a] offset:64\n"
+                   "ds_read_b64 %[e9], %[a] offset:72\n"
+                   "ds_read_b64 %[e10], %[a] offset:80\n"
+                   "ds_read_b64 %[e11], %[a] offset:88\n"
+                   "ds_read_b64 %[e12], %[a] offset:96\n"
+                   "ds_read_b64 %[e13], %[a] offset:104\n"
+                   "ds_read_b64 %[e14], %[a] offset:112\n"
+                   "ds_read_b64 %[e15], %[a] offset:120\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : [e0] "=&v"(e[0]), [e1] "=&v"(e[1]), [e2] "=&v"(e[2]), [e3] "=&v"(e[3]), [e4] "=&v"(e[4]), [e5] "=&v"(e[5]), [e6] "=&v"(e[6]), [e7] "=&v"(e[7]), [e8] "=&v"(e[8]), [e9] "=&v"(e[9]), [e10] "=&v"(e[10]), [e11] "=&v"(e[11]), [e12] "=&v"(e[12]), [e13] "=&v"(e[13]), [e14] "=&v"(e[14]), [e15] "=&v"(e[15])
+                   : [a] "v"(a)
+                   : "memory");
+    }
+  }
+};
 
 struct BlockLayout {
   int nt, rw, pipe, rec;  // threads, row waves, overlapped draws, doubles per sample record
@@ -841,14 +968,11 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
           // own outstanding stores) before each; the barriers order them.  One
           // row address + immediate offsets (d >= D reads the next row or the
           // ring's slack, discarded by the select below)
-          lds_row(base + 8u * (unsigned)(n * D), e, std::make_integer_sequence<int, DMAX>{});
           double tl = 0.0;
-          if (need_lq && pre_lq)
-            asm volatile("ds_read_b64 %0, %1" : "=v"(tl) : "v"(base + 8u * (unsigned)(L.pf_lq + n)));
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(tl) :: "memory");
+          LdsRowWait<DMAX>::run(base + 8u * (unsigned)(n * D), base + 8u * (unsigned)(L.pf_lq + n),
+                                need_lq && pre_lq, e, tl);
 #pragma unroll
           for (int d = 0; d < DMAX; ++d) {
-            asm volatile("" : "+v"(e[d]));
             e[d] = d < D ? e[d] : 0.0;
             if (need_lq && !pre_lq && d < D) {
               if constexpr (TFAM)

@@ -1,0 +1,171 @@
+// vb_probe.hip — peak-rate microbenchmarks (measurement support for bench.py's
+// roofline fractions; BASELINE.md §2: "both peaks must be confirmed with
+// microbenchmarks on the box").  No reference counterpart.
+//
+//   kind 0  HBM copy     16-byte loads + stores over two buffers far past the
+//                        256 MB Infinity Cache; GB/s of read + written bytes
+//   kind 1  HBM read     16-byte loads folded into one XOR per thread; GB/s read
+//   kind 2  fp64 MFMA    v_mfma_f64_16x16x4_f64, 4 independent accumulators per
+//                        wave, 4 waves per SIMD; TFLOP/s
+//   kind 3  fp64 VALU    v_fma_f64, 8 independent chains per lane, 4 waves per
+//                        SIMD; G wave-instructions/s (the VALU issue peak the
+//                        fp64 kernels are priced against)
+//   kind 4  u64 multiply v_mad_u64_u32 chains (Philox's multiply), as kind 3
+#include "../../include/viabel_amd.h"
+#include "vb_internal.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace vbk {
+namespace {
+
+using u4 = unsigned __attribute__((ext_vector_type(4)));
+using d4 = double __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void probe_copy_kernel(const u4* __restrict__ src,
+                                                         u4* __restrict__ dst, long long n) {
+  const long long stride = (long long)gridDim.x * 256;
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const u4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void probe_read_kernel(const u4* __restrict__ src, long long n,
+                                                         unsigned* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * 256;
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  u4 acc = {0u, 0u, 0u, 0u};
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const u4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    acc ^= a ^ b ^ c ^ d;
+  }
+  for (; i < n; i += stride) acc ^= src[i];
+  out[(long long)blockIdx.x * 256 + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
+}
+
+__global__ __launch_bounds__(256) void probe_mfma_kernel(double* out, int iters) {
+  d4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = d4{0, 0, 0, 0};
+  const double a = threadIdx.x * 1e-3, b = 1.0 + blockIdx.x * 1e-6;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
+  }
+  double s = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void probe_fma_kernel(double* out, int iters) {
+  double x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = threadIdx.x * 1e-3 + j;
+  const double m = 0.999999, c = 1e-7 * blockIdx.x;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = fma(x[j], m, c);
+  }
+  double s = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += x[j];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void probe_mad64_kernel(double* out, int iters) {
+  unsigned long long x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = threadIdx.x + 977u * j;
+  const unsigned m = 0xD2511F53u + blockIdx.x;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = (unsigned long long)m * (unsigned)x[j] + (x[j] >> 32);
+  }
+  unsigned long long s = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s ^= x[j];
+  out[blockIdx.x * 256 + threadIdx.x] = (double)(s & 0xFFFF);
+}
+
+}  // namespace
+
+// rate of one probe (see the file header), best of `reps` timed launches after
+// one untimed launch; buffers are allocated and freed here
+int probe_rate(int kind, long long n, int reps, hipStream_t st, double* out) {
+  if (kind < 0 || kind > 4) return vb_set_error(-1, "vb_peak_probe: kind in [0, 4]");
+  if (reps < 1 || n < 1) return vb_set_error(-1, "vb_peak_probe: n >= 1, reps >= 1");
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  void *a = nullptr, *b = nullptr;
+  const long long nv = kind <= 1 ? n / 16 : 0;        // 16-byte vectors
+  const unsigned blocks = kind <= 1 ? (unsigned)ncu * 8 : (unsigned)ncu * 4;
+  const size_t abytes = kind <= 1 ? (size_t)nv * 16 : 0;
+  const size_t bbytes = kind == 0 ? abytes : sizeof(double) * blocks * 256;
+  if (abytes && hipMalloc(&a, abytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return vb_set_error(-3, "vb_peak_probe: hipMalloc(%zu) failed", abytes);
+  }
+  if (hipMalloc(&b, bbytes) != hipSuccess) {
+    (void)hipGetLastError();
+    if (a) (void)hipFree(a);
+    return vb_set_error(-3, "vb_peak_probe: hipMalloc(%zu) failed", bbytes);
+  }
+  if (a) (void)hipMemsetAsync(a, 1, abytes, st);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  const int iters = (int)std::min<long long>(n, 1 << 30);
+  auto launch = [&]() {
+    switch (kind) {
+      case 0:
+        hipLaunchKernelGGL(probe_copy_kernel, dim3(blocks), dim3(256), 0, st, (const u4*)a, (u4*)b, nv);
+        break;
+      case 1:
+        hipLaunchKernelGGL(probe_read_kernel, dim3(blocks), dim3(256), 0, st, (const u4*)a, nv,
+                           (unsigned*)b);
+        break;
+      case 2: hipLaunchKernelGGL(probe_mfma_kernel, dim3(blocks), dim3(256), 0, st, (double*)b, iters); break;
+      case 3: hipLaunchKernelGGL(probe_fma_kernel, dim3(blocks), dim3(256), 0, st, (double*)b, iters); break;
+      default: hipLaunchKernelGGL(probe_mad64_kernel, dim3(blocks), dim3(256), 0, st, (double*)b, iters); break;
+    }
+  };
+  launch();
+  float best = 0.f;
+  int rc = 0;
+  for (int r = 0; r < reps && !rc; ++r) {
+    (void)hipEventRecord(e0, st);
+    launch();
+    (void)hipEventRecord(e1, st);
+    if (hipEventSynchronize(e1) != hipSuccess) {
+      rc = vb_set_error(-2, "vb_peak_probe: kernel failed: %s", hipGetErrorString(hipGetLastError()));
+      break;
+    }
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (r == 0 || ms < best) best = ms;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (a) (void)hipFree(a);
+  (void)hipFree(b);
+  if (rc) return rc;
+  const double sec = best * 1e-3;
+  const double waves = (double)blocks * 4;          // 256-thread blocks
+  switch (kind) {
+    case 0: *out = 2.0 * (double)nv * 16 / sec / 1e9; break;
+    case 1: *out = (double)nv * 16 / sec / 1e9; break;
+    case 2: *out = 2.0 * 16 * 16 * 4 * 4.0 * iters * waves / sec / 1e12; break;
+    default: *out = 8.0 * iters * waves / sec / 1e9; break;   // wave-instructions
+  }
+  return 0;
+}
+
+}  // namespace vbk

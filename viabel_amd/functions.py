@@ -4,6 +4,10 @@
   compute_R_hat_adaptive_numpy   functions.py:44-52
   compute_R_hat_halfway          functions.py:54-65
   stochastic_iterate_averaging   functions.py:68-77
+  safe_root, flat_to_triang, triang_to_flat, compute_posterior_moments
+                                 functions.py:80-150 (host helpers of the IA
+                                 notebooks: index reshapes and a d x d
+                                 conjugate-Gaussian posterior; no Monte Carlo)
 
 Chains are [n_chains, n_iters, K] float64 (host or torch device tensors).  Every
 R-hat of a call is one segment of a single batched kernel launch (vb_rhat);
@@ -15,7 +19,8 @@ import numpy as np
 from . import _native as nat
 
 __all__ = ['compute_R_hat', 'compute_R_hat_adaptive_numpy', 'compute_R_hat_halfway',
-           'stochastic_iterate_averaging']
+           'stochastic_iterate_averaging', 'safe_root', 'flat_to_triang', 'triang_to_flat',
+           'compute_posterior_moments']
 
 
 def _chains(chains):
@@ -101,3 +106,41 @@ def stochastic_iterate_averaging(estimate, start):
     nat.check(nat.lib().vb_iterate_average(nat.context().handle, nat.dptr(x), N, cols, cols, start,
                                            nat.dptr(out)))
     return out, out[-1]
+
+
+def safe_root(N):
+    """Integer square root of a perfect square (functions.py:80-85)."""
+    r = int(np.sqrt(N))
+    if r * r != N:
+        raise ValueError("N is not square!")
+    return r
+
+
+def flat_to_triang(flat_mat):
+    """Row-major lower triangle [M(M+1)/2] -> [M, M] with zeros above the
+    diagonal (functions.py:106-118: row m holds entries (m, 0..m))."""
+    flat = np.asarray(flat_mat, dtype=float).ravel()
+    M = int(-1 + np.sqrt(8 * flat.size + 1)) // 2
+    out = np.zeros((M, M))
+    out[np.tril_indices(M)] = flat[:M * (M + 1) // 2]
+    return out
+
+
+def triang_to_flat(L):
+    """[B, M, M] stack of lower triangles -> [M(M+1)/2, B] (functions.py:126-136)."""
+    L = np.asarray(L)
+    B, _, M = L.shape
+    rows, cols = np.tril_indices(M)
+    return np.ascontiguousarray(L[:, rows, cols].T).astype(float)
+
+
+def compute_posterior_moments(prior_mean, prior_covariance, noise_variance, x, y):
+    """Posterior mean and covariance of Bayesian linear regression with a Gaussian
+    prior (functions.py:139-150): precision = prior precision + x^T x / noise,
+    both inverses through Cholesky factors as the reference forms them."""
+    inv_L = np.linalg.inv(np.linalg.cholesky(prior_covariance))
+    prior_precision = inv_L.T @ inv_L
+    inv_a = np.linalg.inv(np.linalg.cholesky(prior_precision + x.T @ x * (1. / noise_variance)))
+    post_S = inv_a.T @ inv_a
+    post_mu = post_S @ (prior_precision @ prior_mean + (1. / noise_variance) * x.T @ y)
+    return post_mu, post_S

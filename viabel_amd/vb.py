@@ -43,6 +43,7 @@ __all__ = [
     'make_stan_log_density',
     'mean_field_gaussian_variational_family',
     'mean_field_t_variational_family',
+    'full_rank_gaussian_variational_family',
     't_variational_family',
     'black_box_klvi',
     'black_box_chivi',
@@ -262,6 +263,15 @@ def mean_field_gaussian_variational_family(dim, rng=None):
     return _make_family(nat.FAMILY_MF_GAUSSIAN, dim, None, rng)
 
 
+def full_rank_gaussian_variational_family(dim):
+    """Importable for the reference notebooks' import cells (vb.py:85-137); not
+    built: the reference's own version is broken, and the
+    full-rank path here is t_variational_family (a large df approaches it)."""
+    raise NotImplementedError(
+        'full_rank_gaussian_variational_family is out of scope for viabel_amd; '
+        'use t_variational_family(dim, df) with a large df')
+
+
 def mean_field_t_variational_family(dim, df, rng=None):
     """vb.py:140-182.  var_param = [mean (dim), log_scale (dim)]."""
     if df <= 2:
@@ -464,6 +474,14 @@ class DeviceRun:
         nat.check(nat.lib().vb_run_steps_done(self.handle, ctypes.byref(n)))
         return int(n.value)
 
+    def fr_retries(self):
+        """Full-rank runs: advances run again after a warm Newton-Schulz root
+        launched too few iterations (vb_run_fr_retries)."""
+        import ctypes
+        n = ctypes.c_int64()
+        nat.check(nat.lib().vb_run_fr_retries(self.handle, ctypes.byref(n)))
+        return int(n.value)
+
     def synchronize(self):
         nat.context().synchronize()
 
@@ -502,12 +520,12 @@ def _native_adagrad(n_iters, obj, init_param, window, learning_rate, epsilon,
         chunk = max(1, min(chunk, _HOST_CHUNK_ELEMS // max(per_step, 1)))
     bar = _progress(n_iters)
     done = 0
+    step0 = fam.step if fam.rng == 'philox' else None
     try:
         while done < n_iters:
             cs = min(chunk, n_iters - done)
             if fam.rng == 'philox':
-                run.advance_philox(cs, fam.seed, fam.stream, fam.step)
-                fam.step += cs
+                run.advance_philox(cs, fam.seed, fam.stream, step0 + done)
             else:
                 run.advance_host(np.stack([obj._eps_one_call() for _ in range(cs)])[None])
             done += cs
@@ -524,6 +542,10 @@ def _native_adagrad(n_iters, obj, init_param, window, learning_rate, epsilon,
     # a ctypes call cannot be interrupted, but the interrupt may land between an
     # advance returning and `done` being updated: the run's own count is the truth
     done = run.steps_done()
+    if step0 is not None:
+        # the family's Philox counter follows the steps the run really took, so a
+        # later call never reuses draws whatever point an interrupt landed at
+        fam.step = step0 + done
     _, hist, vals, smooth = run.result()
     if done == n_iters:
         return smooth[0], hist[0], vals[0], np.zeros(n_iters)
