@@ -346,3 +346,31 @@ def test_ill_conditioned_sigma_trajectory():
     _close(vals[0], ovals, 1e-7)
     _close(hist[0], ohist, 1e-7)
     _close(lam[0], ohist[-1], 1e-7)
+
+
+@pytest.mark.parametrize('objective', ['klvi', 'chivi'])
+def test_ill_conditioned_single_call(objective):
+    """A single value-and-gradient call at cond(Sigma) ~1e4 (a cold root, no run):
+    the call runs again with larger Newton-Schulz / PCG counts until the device
+    status is clean (vb_capi.hip, vb_fr.hip fr_info), and matches the oracle on
+    the reference's numpy stream."""
+    vb, targets, fo, _, _ = _mods()
+    D, N = 48, 64
+    rs = np.random.RandomState(5)
+    tri = np.tril_indices(D)
+    free = rs.randn(len(tri[0])) * 0.01
+    free[tri[0] == tri[1]] = np.linspace(-2.3, 2.3, D)[rs.permutation(D)]
+    lam = np.concatenate([rs.randn(D) * 0.3, free])
+    fam = vb.t_variational_family(D, 30.0, rng='numpy')
+    ofam = fo.FullRankT(D, 30.0)
+    otgt = fo.target_fn('corr_gauss', D)
+    if objective == 'klvi':
+        v, g = vb.black_box_klvi(fam, targets.corr_gauss(D), N)(lam)
+        ov, og = fo.klvi_value_grad(ofam, otgt, lam, N)
+    else:
+        np.random.seed(3)
+        v, g = vb.black_box_chivi(2.0, fam, targets.corr_gauss(D), N)(lam)
+        np.random.seed(3)
+        ov, og = fo.chivi_value_grad(ofam, otgt, lam, N, 2.0)
+    np.testing.assert_allclose(v, ov, rtol=1e-9)
+    _close(g, og, 1e-7)

@@ -415,13 +415,21 @@ int fr_objective(vb_ctx* c, const FamInfo& fi, const vb_target* tgt, const vb_ob
   key_of(noise->seed, &k0, &k1);
   vbk::FrWork* W;
   VB_TRY(fr_work(c, &W));
-  VB_TRY(vbk::fr_value_grad(W, fr_spec(fi, tgt, obj, tp, tc), dl.d, host ? dn.d : nullptr, k0, k1,
-                            noise->stream, (uint32_t)noise->step, c->slot[4].d(), dg.d,
-                            c->stream));
+  // a root or gradient solve that needed more iterations than launched (an
+  // ill-conditioned Sigma) runs the call again with larger counts (fr_info)
+  for (int attempt = 0;; ++attempt) {
+    VB_TRY(vbk::fr_value_grad(W, fr_spec(fi, tgt, obj, tp, tc), dl.d, host ? dn.d : nullptr, k0,
+                              k1, noise->stream, (uint32_t)noise->step, c->slot[4].d(), dg.d,
+                              c->stream));
+    VB_TRY(sync(c));
+    bool again = false;
+    if (int rc = vbk::fr_info(W, c->stream, attempt < 16 ? &again : nullptr)) return rc;
+    if (!again) break;
+  }
+  vbk::fr_retry_done(W);
   VB_HIP(hipMemcpyAsync(value, c->slot[4].p, sizeof(double), hipMemcpyDefault, c->stream));
   VB_TRY(dg.finish(c));
   VB_TRY(sync(c));
-  if (int rc = vbk::fr_info(W, c->stream)) return rc;
   return VB_OK;
 }
 
@@ -1032,8 +1040,9 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
         if (rerun) vbk::fr_retry_done(W);
         break;
       }
-      // fr_info raised the count (bounded by kFrNSMax, then it reports an error)
-      ++r->fr_retries;
+      // fr_info raised a count (Newton-Schulz by 3 up to kFrNSMax, PCG x2 up to
+      // kFrPcgMax; past those it reports an error)
+      if (++r->fr_retries > 64) return fail(VB_EDEVICE, "full-rank advance: too many reruns");
       VB_HIP(hipMemcpyAsync(r->lam.d(), r->backup.d(), P * sizeof(double),
                             hipMemcpyDeviceToDevice, c->stream));
       VB_HIP(hipMemcpyAsync(r->ring.d(), r->backup.d() + P, P * r->W * sizeof(double),

@@ -918,7 +918,10 @@ struct FrWork {
   const void* owner = nullptr;    // the run whose root the warm state above holds
   int ns_kmax = 12, pcg_kmax = 14;  // iterations launched (device skips past convergence)
   int last_kmax = 12;             // Newton-Schulz iterations the last root launched
-  int retry_kmax = 0;             // floor for warm roots after an advance ran again (same owner)
+  int retry_kmax = 0;             // Newton-Schulz floor after a call / advance ran again
+  int retry_pcg = 0;              // PCG floor after a call / advance ran again
+  const void* retry_owner = nullptr;  // the run the floors belong to
+  int kpcg_max_seen = 0;          // most PCG iterations launched since the last fr_info
   bool eig_pending = false;       // a dsyevd ran since the last fr_info
   bool sqrt_pending = false;      // a Newton-Schulz / PCG status to read at fr_info
   bool last_hz = false;           // the last root's schedule had a Z power vector (uZ valid)
@@ -1108,7 +1111,7 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
   // to the run that made it: any other caller's root (another run, a cold
   // log-weight or single-call root) invalidates it
   warm = warm && W->warm && owner != nullptr && W->owner == owner;
-  if (W->owner != owner) W->retry_kmax = 0;
+  if (W->owner != owner && W->retry_owner != owner) W->retry_kmax = W->retry_pcg = 0;
   W->owner = owner;
   // a cold root starts a new problem: forget the iteration counts learnt on the
   // previous one (fr_info learns them again from this run's warm steps)
@@ -1118,6 +1121,10 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
     const char* e = std::getenv("VIABEL_AMD_FR_NS_START");
     W->ns_kmax = e ? std::max(1, std::atoi(e)) : 12;
     W->pcg_kmax = 14;
+    // and its first warm step starts the Z power vector afresh (not from a vector
+    // another problem left in the workspace): a run's steps then depend only on
+    // the run, whatever used the workspace before it
+    W->zv_init = false;
   }
   const bool hz = warm && W->have_z && W->Zf;
   const int n_pow = ready ? 0 : warm ? 3 : 8;
@@ -1143,7 +1150,8 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
     return e ? std::max(0, std::atoi(e)) : 0;
   }();
   const int kmax =
-      std::min(warm ? std::max({W->ns_kmax + spare, W->retry_kmax, 3}) : std::max(W->ns_kmax + 1, 12),
+      std::min(warm ? std::max({W->ns_kmax + spare, W->retry_kmax, 3})
+                    : std::max({W->ns_kmax + 1, 12, W->retry_kmax}),
                kFrNSMax);
   W->last_warm = warm;
   W->last_kmax = kmax;
@@ -1260,8 +1268,12 @@ int fr_pcg(FrWork* W, int D, hipStream_t st, int N = 0, const double* rw = nullp
   FR_HIP(gemm(zr(-1), st));
   hipLaunchKernelGGL(pcg_p_kernel, tg, dim3(256), 0, st, D, -1, W->C2.d(), W->rz_part.d(),
                      4 * nblk, W->ee_part.d(), nblk, sc, W->P.d());
-  // warm roots launch the learnt count (fr_info), others at least 16
-  const int kpcg = W->last_warm ? std::max(W->pcg_kmax, 3) : std::max(W->pcg_kmax, 16);
+  // warm roots launch the learnt count (fr_info), others at least 16; a rerun
+  // after a residual above the status bar launches at least its floor
+  const int kpcg = std::min(kFrPcgMax, std::max(W->last_warm ? std::max(W->pcg_kmax, 3)
+                                                             : std::max(W->pcg_kmax, 16),
+                                                W->retry_pcg));
+  W->kpcg_max_seen = std::max(W->kpcg_max_seen, kpcg);
   for (int it = 0; it < kpcg; ++it) {
     GemmOp g = mm(D, D, D, W->Yf, false, W->P.d(), false, W->C1.d());
     g.dot_with = W->P.d();
@@ -1864,7 +1876,10 @@ int fr_warm_save(FrWork* W, hipStream_t st) {
   return 0;
 }
 
-void fr_retry_done(FrWork* W) { W->retry_kmax = 0; }
+void fr_retry_done(FrWork* W) {
+  W->retry_kmax = W->retry_pcg = 0;
+  W->retry_owner = nullptr;
+}
 
 int fr_warm_restore(FrWork* W, hipStream_t st) {
   const FrWork::WarmHost h = W->wsnap_h;
@@ -1914,22 +1929,36 @@ int fr_info(FrWork* W, hipStream_t st, bool* retry) {
   const FrSched& h = *W->host_sched;
   FrSched* d = static_cast<FrSched*>(W->sched.p);
   FR_HIP(hipMemsetAsync(&d->status, 0, 5 * sizeof(int), st));   // status and the hints
+  const int kpcg_seen = W->kpcg_max_seen;
+  W->kpcg_max_seen = 0;
   if ((h.status & 1) || (!h.ns_conv && !h.ns_fin)) {
     // warm roots launch exactly the learnt count: a step that needed more asks
-    // the caller to run its advance again with a larger count
-    if (retry && W->last_warm && W->last_kmax < kFrNSMax) {
+    // the caller to run its call / advance again with a larger count
+    if (retry && W->last_kmax < kFrNSMax) {
       *retry = true;
       W->ns_kmax = std::min(kFrNSMax, W->last_kmax + 3);
       W->retry_kmax = W->ns_kmax;   // kept through the cold first step of the rerun
+      W->retry_owner = W->owner;
       W->prep_owner = nullptr;
       return 0;
     }
     return vb_set_error(-2, "Newton-Schulz square root of Sigma did not converge in %d iterations "
                             "(Sigma too ill-conditioned)", W->last_kmax);
   }
-  if (h.status & 2)
+  if (h.status & 2) {
+    // the PCG's iteration count grows with the preconditioned condition number
+    // (2 + k + 1/k) / 4, k = cond(S): an ill-conditioned Sigma needs far more
+    // than the learnt / default count -- run again with twice as many
+    if (retry && kpcg_seen < kFrPcgMax) {
+      *retry = true;
+      W->retry_pcg = std::min(kFrPcgMax, 2 * kpcg_seen);
+      W->retry_owner = W->owner;
+      W->prep_owner = nullptr;
+      return 0;
+    }
     return vb_set_error(-2, "conjugate gradients for the sqrtm gradient did not converge in %d "
-                            "iterations", W->pcg_kmax);
+                            "iterations", kpcg_seen);
+  }
   // Newton-Schulz: launch exactly the iterations the hardest warm step needed --
   // up to its final update when the finish rule ended it (the root is then in
   // the output buffer already: no detection T and no copying launch), or up to
@@ -1941,7 +1970,7 @@ int fr_info(FrWork* W, hipStream_t st, bool* retry) {
   // step needing one more stops one iteration short: ~10x the 1e-9 target
   // residual, far inside the 1e-7 status bar; the next advance learns it)
   if (W->last_warm && h.hint_pcg >= 0)
-    W->pcg_kmax = std::min(40, std::max(h.hint_pcg, h.pcg_iter) + 1);
+    W->pcg_kmax = std::min(kFrPcgMax, std::max(h.hint_pcg, h.pcg_iter) + 1);
   return 0;
 }
 

@@ -213,6 +213,7 @@ int fr_prepare(FrWork* W, int D, const double* lam, hipStream_t st);  // eigh of
 int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm = false,
             const void* owner = nullptr, bool ready = false);
 constexpr int kFrNSMax = 40;  // Newton-Schulz iterations launched at most per root
+constexpr int kFrPcgMax = 192; // PCG iterations launched at most per gradient
 int fr_draw(FrWork* W, int D, long long n, double df, const double* host_eps, uint32_t k0,
             uint32_t k1, uint32_t stream, uint32_t step, const double** s_out,
             const double** z_out, hipStream_t st);
