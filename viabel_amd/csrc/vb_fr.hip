@@ -431,7 +431,10 @@ __global__ __launch_bounds__(256) void fr_norm2_kernel(int n, const double* x, d
 // l_default without one.  A low l_0 costs iterations, never accuracy: the
 // iteration is declared converged from the residual ||I - Z_k Y_k||_F alone.
 struct FrSched {
-  double c, sqrt_c, inv_sqrt_c, c_prev;
+  double c, sqrt_c, inv_sqrt_c;
+  double cbuf[2];                // c of the last two roots: a schedule reads the previous
+                                 // one at [slot ^ 1] and writes its own at [slot] (the
+                                 // fused iteration-0 GEMM's blocks read while block 0 writes)
   double ns0[4];                 // iteration 0 coefficients (GemmOp::ns0)
   double nalpha2[kFrNSMax + 1];  // -a_k^2 (T_k GEMM alpha)
   double shift[kFrNSMax + 1];    // 3 - a_k^2 (residual shift of T_k)
@@ -479,22 +482,106 @@ __global__ __launch_bounds__(256) void fr_power2_kernel(int D, const double* Sig
   }
 }
 
-__device__ double ns_alpha(double l) { return sqrt(3.0 / (1.0 + l + l * l)); }
+// The schedule's scalar math uses hardware reciprocal / reciprocal-sqrt seeds and
+// Newton steps (a few dependent FMAs each) instead of IEEE division and sqrt
+// (long software sequences): it runs on one thread on the step's critical path,
+// and any deterministic value of these scaling coefficients is a valid schedule
+// (Newton-Schulz converges to the same root; the fused and stand-alone schedule
+// share this code, so they agree bit for bit).
+__device__ __forceinline__ double frcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = r * fma(-x, r, 2.0);
+  return r * fma(-x, r, 2.0);
+}
+__device__ __forceinline__ double frsq(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * fma(-0.5 * x, y * y, 1.5);
+  return y * fma(-0.5 * x, y * y, 1.5);
+}
+__device__ __forceinline__ double ns_alpha(double l) {
+  return 1.7320508075688772 * frsq(1.0 + l + l * l);   // sqrt(3 / (1 + l + l^2))
+}
 
-// One block: c, l_0 and the whole schedule; resets the per-step flags.
-// Also scal[0] = 0.5 log det Sigma = sum_i log L_ii, the free log-diagonal of lam.
-// Power vectors: y = Sigma x (x the previous unit vector), v = Z_prev u.  A
-// fused step instead passes qf_part, the Sigma GEMM's partials of x^T Sigma x for
-// x = y (the previous step's last kernel computed y = Sigma_prev uS): lambda_max
-// is estimated by the Rayleigh quotient x^T Sigma x / x^T x.  Every sched stores
-// the unit vectors uS = y / ||y||, uZ = v / ||v|| for the next power steps.
+// The schedule from the reduced sums (f = ||Sigma||_F^2 partial sum, ly / lv =
+// ||y||^2 / ||v||^2, ld = sum log L_ii, qf = y^T Sigma y): one thread computes
+// c, l_0 and the iteration-0 coefficients ns0[4]; with `a` non-null also the
+// per-iteration a_k (k <= kmax) into a[] and the scalar fields of FrSched
+// (write), for fr_schedule_store to spread over threads.
+__device__ void fr_schedule(int kmax, double f, double ly, double lv, double ld, double qf,
+                            bool has_qf, int has_z, double l_default, FrSched* sc, int slot,
+                            double* scal, bool write, double* ns0, double* a_out) {
+  const double lmax = has_qf ? (ly > 0.0 ? qf * frcp(ly) : 0.0) : ly * frsq(ly);
+  const double c = fmin(1.25 * lmax, f * frsq(f));   // ||Sigma||_F >= lambda_max
+  const double ic = frcp(c);
+  double l = l_default;
+  double ee_scale = 1.0;
+  if (has_z && lv > 0.0) {
+    const double lmin = sc->cbuf[slot ^ 1] * frcp(lv);   // lambda_min(Sigma_prev)
+    const double q = lmin * ic;
+    l = 0.8 * q * frsq(q);
+    // the PCG's X carries up to kappa x its relative residual, kappa = (2 + k +
+    // 1/k) / 4 the preconditioned condition number, k = cond(S) = sqrt(lmax /
+    // lmin): past kappa = 2 the stopping test tightens by kappa / 2, so X's
+    // relative error stays <= 2 x the tolerance however ill-conditioned Sigma is
+    // (config 4: kappa ~1.2, unchanged)
+    if (write && lmin > 0.0 && lmax > lmin) {
+      const double r = lmax * frcp(lmin), k = r * frsq(r), kap = 0.25 * (2.0 + k + frcp(k));
+      if (kap > 2.0) ee_scale = 4.0 * frcp(kap * kap);
+    }
+  }
+  l = fmin(fmax(l, 1e-4), 1.0);
+  {
+    const double a = ns_alpha(l), a2 = a * a;
+    // Y_1 = (3/2) a A - (1/2) a^3 A^2, Z_1 = (a / 2) (3 I - a^2 A), A = Sigma / c
+    ns0[0] = -0.5 * a * a2 * (ic * ic);
+    ns0[1] = 1.5 * a * ic;
+    ns0[2] = 0.5 * a;
+    ns0[3] = a2 * ic;
+  }
+  if (!write) return;
+  scal[0] = ld;
+  sc->ee_scale = ee_scale;
+  sc->l0 = l;
+  sc->lmax_est = lmax;
+  sc->c = c;
+  const double rc = frsq(c);
+  sc->sqrt_c = c * rc;
+  sc->inv_sqrt_c = rc;
+  sc->cbuf[slot] = c;
+  for (int k = 0; k < 4; ++k) sc->ns0[k] = ns0[k];
+  const int kn = kmax < kFrNSMax ? kmax : kFrNSMax;
+  for (int k = 0; k <= kn; ++k) {
+    const double a = ns_alpha(l), a2 = a * a;
+    a_out[k] = a;
+    l = fmin(0.5 * a * l * (3.0 - a2 * l * l), 1.0);
+  }
+  sc->ns_conv = 0;
+  sc->ns_fin = 0;
+  sc->ns_iter = -1;
+  sc->warm_step = has_z;
+  sc->pcg_done = 0;
+  sc->pcg_iter = -1;
+}
+
+// per-iteration coefficients from a_k, one k per thread (after fr_schedule)
+__device__ __forceinline__ void fr_schedule_store(int kmax, const double* a_k, FrSched* sc) {
+  const int k = threadIdx.x;
+  if (k <= kmax && k <= kFrNSMax) {
+    const double a = a_k[k], a2 = a * a;
+    sc->nalpha2[k] = -a2;
+    sc->shift[k] = 3.0 - a2;
+    sc->halpha[k] = 0.5 * a;
+    sc->inv_a4[k] = frcp(a2 * a2);
+  }
+}
+
 __global__ __launch_bounds__(1024) void fr_sched_kernel(int D, int kmax, const double* fro_part,
                                                        int n_part, const double* y,
                                                        const double* v, int has_z,
                                                        double l_default, FrSched* sc,
                                                        const double* lam, double* scal,
                                                        const double* qf_part, double* uS,
-                                                       double* uZ) {
+                                                       double* uZ, int slot) {
   __shared__ double red[16];
   const int T = blockDim.x;
   double f = 0.0, ly = 0.0, lv = 0.0, ld = 0.0, qf = 0.0;
@@ -519,61 +606,230 @@ __global__ __launch_bounds__(1024) void fr_sched_kernel(int D, int kmax, const d
     qf = block_sum(qf, red);
   }
   {
-    const double iy = ly > 0.0 ? 1.0 / sqrt(ly) : 0.0, iv = lv > 0.0 ? 1.0 / sqrt(lv) : 0.0;
+    const double iy = ly > 0.0 ? frsq(ly) : 0.0, iv = lv > 0.0 ? frsq(lv) : 0.0;
     for (int i = threadIdx.x; i < D; i += T) {
       uS[i] = y[i] * iy;
       if (has_z && lv > 0.0) uZ[i] = v[i] * iv;
     }
   }
-  if (threadIdx.x != 0) return;
-  scal[0] = ld;
-  // ||Sigma x|| for unit x, or the Rayleigh quotient: both <= lambda_max
-  const double lmax = qf_part ? (ly > 0.0 ? qf / ly : 0.0) : sqrt(ly);
-  const double c = fmin(1.25 * lmax, sqrt(f));   // ||Sigma||_F >= lambda_max
-  double l = l_default;
-  double ee_scale = 1.0;
-  if (has_z && lv > 0.0) {
-    const double lmin = sc->c_prev / lv;        // lambda_min(Sigma_prev)
-    l = 0.8 * sqrt(lmin / c);
-    // the PCG's X carries up to kappa x its relative residual, kappa = (2 + k +
-    // 1/k) / 4 the preconditioned condition number, k = cond(S) = sqrt(lmax /
-    // lmin): past kappa = 2 the stopping test tightens by kappa / 2, so X's
-    // relative error stays <= 2 x the tolerance however ill-conditioned Sigma is
-    // (config 4: kappa ~1.2, unchanged)
-    if (lmin > 0.0 && lmax > lmin) {
-      const double k = sqrt(lmax / lmin), kap = 0.25 * (2.0 + k + 1.0 / k);
-      if (kap > 2.0) ee_scale = 4.0 / (kap * kap);
+  __shared__ double a_k[kFrNSMax + 1];
+  if (threadIdx.x == 0) {
+    double ns0[4];
+    fr_schedule(kmax, f, ly, lv, ld, qf, qf_part != nullptr, has_z, l_default, sc, slot, scal,
+                true, ns0, a_k);
+  }
+  __syncthreads();
+  fr_schedule_store(kmax, a_k, sc);
+}
+
+// fr_sched_kernel's work inside the Newton-Schulz iteration-0 GEMM (whose
+// coefficients are the only use of the schedule in that launch): every block
+// loads its share of the partial sums before the main loop, reduces them after
+// it (the loads' latency hides under the product) and computes the schedule;
+// block 0 stores it (FrSched, uS / uZ, scal) for the launches that follow.  For
+// D <= kSchedHookMaxD (the per-thread load counts below).
+constexpr int kSchedP = 4, kSchedV = 2;   // partials / vector entries per thread
+constexpr int kSchedHookMaxD = kSchedV * 512;
+struct SchedArgs {
+  int D, kmax, n_part, has_z, slot;
+  double l_default;
+  const double *fro_part, *qf_part, *y, *v, *lam;
+  FrSched* sc;
+  double *scal, *uS, *uZ;
+};
+struct SchedHook {
+  using Args = SchedArgs;
+  static constexpr bool kKScale = false;
+  static constexpr int kLds = 128;
+  const SchedArgs& a;
+  const int blk;
+  double* const lds;
+  double fp[kSchedP], qp[kSchedP], yv[kSchedV], vv[kSchedV], dv[kSchedV];
+  __device__ __forceinline__ SchedHook(const SchedArgs& args, int b, double* l)
+      : a(args), blk(b), lds(l) {}
+  __device__ __forceinline__ const double* kscale() const { return nullptr; }
+  __device__ __forceinline__ void pre() {
+    const int D = a.D, n_part = a.n_part, has_z = a.has_z;
+    const double *fro_part = a.fro_part, *qf_part = a.qf_part, *y = a.y, *v = a.v, *lam = a.lam;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < kSchedP; ++e) {
+      const int i = t + 512 * e;
+      fp[e] = i < n_part ? fro_part[i] : 0.0;
+      qp[e] = (qf_part && i < n_part) ? qf_part[i] : 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < kSchedV; ++e) {
+      const int i = t + 512 * e;
+      yv[e] = i < D ? y[i] : 0.0;
+      vv[e] = (has_z && i < D) ? v[i] : 0.0;
+      dv[e] = i < D ? lam[D + (long long)i * (i + 1) / 2 + i] : 0.0;
     }
   }
-  sc->ee_scale = ee_scale;
-  l = fmin(fmax(l, 1e-4), 1.0);
-  sc->l0 = l;
-  sc->lmax_est = lmax;
-  sc->c = c;
-  sc->sqrt_c = sqrt(c);
-  sc->inv_sqrt_c = 1.0 / sqrt(c);
-  sc->c_prev = c;
-  for (int k = 0; k <= kmax && k <= kFrNSMax; ++k) {
-    const double a = ns_alpha(l), a2 = a * a;
-    if (k == 0) {
-      // Y_1 = (3/2) a A - (1/2) a^3 A^2, Z_1 = (a / 2) (3 I - a^2 A), A = Sigma / c
-      sc->ns0[0] = -0.5 * a * a2 / (c * c);
-      sc->ns0[1] = 1.5 * a / c;
-      sc->ns0[2] = 0.5 * a;
-      sc->ns0[3] = a2 / c;
+  __device__ __forceinline__ const double* post() {
+    const int D = a.D, has_z = a.has_z;
+    double* uS = a.uS;
+    double* uZ = a.uZ;
+    double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int e = 0; e < kSchedP; ++e) {
+      s5[0] += fp[e];
+      s5[4] += qp[e];
     }
-    sc->nalpha2[k] = -a2;
-    sc->shift[k] = 3.0 - a2;
-    sc->halpha[k] = 0.5 * a;
-    sc->inv_a4[k] = 1.0 / (a2 * a2);
-    l = fmin(0.5 * a * l * (3.0 - a2 * l * l), 1.0);
+#pragma unroll
+    for (int e = 0; e < kSchedV; ++e) {
+      s5[1] += yv[e] * yv[e];
+      s5[2] += vv[e] * vv[e];
+      s5[3] += dv[e];
+    }
+    const int t = threadIdx.x, w = t >> 6;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      s5[k] = wave_sum(s5[k]);
+      if ((t & 63) == 0) lds[8 + 5 * w + k] = s5[k];
+    }
+    __syncthreads();
+    if (t == 0) {
+      double r[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+      for (int ww = 0; ww < 8; ++ww)
+        for (int k = 0; k < 5; ++k) r[k] += lds[8 + 5 * ww + k];
+      fr_schedule(a.kmax, r[0], r[1], r[2], r[3], r[4], a.qf_part != nullptr, has_z, a.l_default,
+                  a.sc, a.slot, a.scal, blk == 0, lds, lds + 64);
+      lds[4] = r[1] > 0.0 ? frsq(r[1]) : 0.0;
+      lds[5] = r[2] > 0.0 ? frsq(r[2]) : 0.0;
+    }
+    __syncthreads();
+    if (blk == 0) {   // the per-iteration coefficients and the next step's unit power vectors
+      fr_schedule_store(a.kmax, lds + 64, a.sc);
+      const double iy = lds[4], iv = lds[5];
+#pragma unroll
+      for (int e = 0; e < kSchedV; ++e) {
+        const int i = t + 512 * e;
+        if (i < D) {
+          uS[i] = yv[e] * iy;
+          if (has_z && iv > 0.0) uZ[i] = vv[e] * iv;
+        }
+      }
+    }
+    return lds;
   }
-  sc->ns_conv = 0;
-  sc->ns_fin = 0;
-  sc->ns_iter = -1;
-  sc->warm_step = has_z;
-  sc->pcg_done = 0;
-  sc->pcg_iter = -1;
+};
+
+// fr_weights_kernel's work inside the G_S = Z^T diag(rk) G GEMM, whose only use of
+// the weights is the K scale rk: every block forms the N log weights (log p from
+// the target GEMM's row partials, log q from zz and s) and the KLVI / CHIVI
+// weights itself, in one fixed order, while the first operand stage is in
+// flight, and keeps rk in LDS for the K-scaled LDS-DMA loop; block 0 stores
+// logp, r, rk, the objective value and scal[1] for the launches that follow.
+// N <= 512, N a multiple of the loop's 64-deep stages.
+struct WeightsArgs {
+  int N, D, chivi, pd;
+  double alpha, df, t_const;
+  double* logp;
+  const double *zz, *s;
+  double *scal, *r, *rk, *value;
+  const double* lp_part;
+  int n_lp;
+  double lp_const;
+};
+struct WeightsHook {
+  using Args = WeightsArgs;
+  static constexpr bool kKScale = true;
+  static constexpr int kLds = 512 + 64;
+  const WeightsArgs& a;
+  const int blk;
+  double* const lds;
+  __device__ __forceinline__ WeightsHook(const WeightsArgs& args, int b, double* l)
+      : a(args), blk(b), lds(l) {}
+  __device__ __forceinline__ const double* kscale() const { return lds; }
+  __device__ __forceinline__ const double* post() { return nullptr; }
+  // fixed-order block reduction over 512 threads (8 waves): op 0 sum, 1 max
+  __device__ __forceinline__ double reduce(double v, bool mx) {
+    double* red = lds + 512;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double o = __shfl_xor(v, off, 64);
+      v = mx ? fmax(v, o) : v + o;
+    }
+    if ((t & 63) == 0) red[t >> 6] = v;
+    __syncthreads();
+    double r = red[0];
+    for (int w = 1; w < 8; ++w) r = mx ? fmax(r, red[w]) : r + red[w];
+    __syncthreads();
+    return r;
+  }
+  __device__ __forceinline__ void pre() {
+    const int N = a.N, t = threadIdx.x;
+    const int tpr = N <= 64 ? 8 : N <= 128 ? 4 : N <= 256 ? 2 : 1;   // threads per row
+    const int k = t / tpr, sub = t % tpr;
+    const bool own = k < N && sub == 0;
+    double lp = 0.0;
+    if (a.lp_part) {
+      double acc = 0.0;
+      if (k < N) {
+#pragma unroll 4
+        for (int j = sub; j < a.n_lp; j += tpr) acc += a.lp_part[(long long)j * N + k];
+      }
+      for (int off = 1; off < tpr; off <<= 1) acc += __shfl_xor(acc, off, 64);
+      lp = 0.5 * acc + a.lp_const;
+    } else if (own) {
+      lp = a.logp[k];
+    }
+    const double hld = a.scal[0];
+    const double e = 0.5 * (a.df + a.D);
+    double sk = 1.0, lw = 0.0;
+    if (own) {
+      sk = a.s[k];
+      if (a.chivi || a.pd) {
+        const double maha = a.zz[k] / (sk * sk);
+        lw = lp - ((a.t_const - hld) - e * log(1.0 + maha / a.df));
+      }
+    }
+    if (blk == 0 && own && a.lp_part) a.logp[k] = lp;
+    if (!a.chivi) {
+      const double tot = reduce(own ? (a.pd ? lw : lp) : 0.0, false);
+      if (own) {
+        lds[k] = (-1.0 / N) / sk;
+        if (blk == 0) {
+          a.r[k] = -1.0 / N;
+          a.rk[k] = lds[k];
+        }
+      }
+      if (blk == 0 && t == 0) {
+        *a.value = a.pd ? -(tot / N) : -(hld + tot / N);
+        a.scal[1] = -0.5;
+      }
+    } else {
+      const double mx = reduce(own ? lw : -INFINITY, true);
+      const double w = own ? pow(exp(lw - mx), a.alpha) : 0.0;
+      const double sw = reduce(w, false);
+      if (own) {
+        const double rr = a.alpha * w / N;
+        lds[k] = rr / sk;
+        if (blk == 0) {
+          a.r[k] = rr;
+          a.rk[k] = lds[k];
+        }
+      }
+      if (blk == 0 && t == 0) {
+        *a.value = log(sw / N) / a.alpha + mx;
+        a.scal[1] = 0.5 * a.alpha * sw / N;
+      }
+    }
+    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+};
+
+// VIABEL_AMD_FR_WEIGHTS_FUSE=1: the weights inside the G_S GEMM (WeightsHook);
+// otherwise the weights kernel runs on its own
+bool weights_fused() {
+  static const bool on = [] {
+    const char* e = std::getenv("VIABEL_AMD_FR_WEIGHTS_FUSE");
+    return e && e[0] == '1';
+  }();
+  return on;
 }
 
 // The fused step's last kernel (adagrad runs, Philox draws): the packed gradient
@@ -925,6 +1181,7 @@ struct FrWork {
   bool eig_pending = false;       // a dsyevd ran since the last fr_info
   bool sqrt_pending = false;      // a Newton-Schulz / PCG status to read at fr_info
   bool last_hz = false;           // the last root's schedule had a Z power vector (uZ valid)
+  int c_slot = 0;                 // FrSched::cbuf slot the last schedule wrote
   // fused steps (fr_value_grad with an adagrad update and Philox draws): the last
   // step's final kernel prepared the next one -- L of the updated parameters, the
   // draws (Z, s, zz) of rng step prep_step on (prep_k0, prep_k1, prep_stream) and
@@ -940,7 +1197,7 @@ struct FrWork {
   Buf wsnap;
   struct WarmHost {
     bool warm, have_z, zv_init, last_hz, valid;
-    int pv_cur, zf_slot;
+    int pv_cur, zf_slot, c_slot;
     const void* owner;
   } wsnap_h{};
   // N x D / N
@@ -960,6 +1217,15 @@ FrWork* fr_work_create() { return new (std::nothrow) FrWork(); }
 void fr_work_destroy(FrWork* w) { delete w; }
 
 namespace {
+
+// VIABEL_AMD_FR_SCHED_FUSE=0: the schedule kernel runs on its own (A/B switch)
+bool sched_fused() {
+  static const bool on = [] {
+    const char* e = std::getenv("VIABEL_AMD_FR_SCHED_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 #define FR_HIP(expr)                                                                       \
   do {                                                                                     \
@@ -1155,22 +1421,38 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
                kFrNSMax);
   W->last_warm = warm;
   W->last_kmax = kmax;
-  if (ready)
-    hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(1024), 0, st, D, kmax, W->fro_part.d(),
-                       nparts, W->pS.d(), W->pz.d(), 1, 0.05, sc, lam, W->scal.d(),
-                       W->ypart.d(), W->uS.d(), W->uZ.d());
-  else
-    hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(1024), 0, st, D, kmax, W->fro_part.d(),
-                       nparts, W->pv[W->pv_cur].d(), W->pv[2 + W->pv_cur].d(), hz ? 1 : 0, 0.05,
-                       sc, lam, W->scal.d(), nullptr, W->uS.d(), W->uZ.d());
+  W->c_slot ^= 1;
+  SchedArgs sh{};
+  sh.D = D;
+  sh.kmax = kmax;
+  sh.n_part = nparts;
+  sh.has_z = ready || hz ? 1 : 0;
+  sh.slot = W->c_slot;
+  sh.l_default = 0.05;
+  sh.fro_part = W->fro_part.d();
+  sh.qf_part = ready ? W->ypart.d() : nullptr;
+  sh.y = ready ? W->pS.d() : W->pv[W->pv_cur].d();
+  sh.v = ready ? W->pz.d() : W->pv[2 + W->pv_cur].d();
+  sh.lam = lam;
+  sh.sc = sc;
+  sh.scal = W->scal.d();
+  sh.uS = W->uS.d();
+  sh.uZ = W->uZ.d();
   W->last_hz = ready || hz;
-  // iteration 0: Y_1 -> Yb[1], Z_1 -> Zb[1]
-  {
-    GemmOp g = mm(D, D, D, W->Sig.d(), false, W->Sig.d(), false, W->Yb[1].d());
-    g.sym = 1;
-    g.ns0 = sc->ns0;
-    g.ns0_z = W->Zb[1].d();
-    FR_HIP(gemm(g, st));
+  // iteration 0: Y_1 -> Yb[1], Z_1 -> Zb[1]; the schedule is computed inside it
+  // (SchedHook) when the shapes allow, else by its own kernel first
+  GemmOp g0 = mm(D, D, D, W->Sig.d(), false, W->Sig.d(), false, W->Yb[1].d());
+  g0.sym = 1;
+  g0.ns0_z = W->Zb[1].d();
+  if (sched_fused() && D <= kSchedHookMaxD && nparts <= kSchedP * 512 && gemm_detail::glds_ok_shape(g0)) {
+    g0.ns0 = sc->ns0;   // (marks the iteration-0 epilogue; the hook's block-local copy is used)
+    FR_HIP(gemm_hook<SchedHook>(g0, sh, st));
+  } else {
+    hipLaunchKernelGGL(fr_sched_kernel, dim3(1), dim3(1024), 0, st, D, kmax, sh.fro_part, nparts,
+                       sh.y, sh.v, sh.has_z, sh.l_default, sc, lam, sh.scal, sh.qf_part, sh.uS,
+                       sh.uZ, sh.slot);
+    g0.ns0 = sc->ns0;
+    FR_HIP(gemm(g0, st));
   }
   for (int k = 1; k <= kmax; ++k) {
     const double *Yk = W->Yb[k & 1].d(), *Zk = W->Zb[k & 1].d();
@@ -1393,13 +1675,21 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
       hipLaunchKernelGGL(fr_rows_kernel, dim3(blocks(N, 4)), dim3(256), 0, st, D, (long long)N,
                          z, nullptr, nullptr, 0.0, 0, W->zz.d(), nullptr);
   }
-  hipLaunchKernelGGL(fr_weights_kernel, dim3(1), dim3(1024), 0, st, N, D, f.chivi, f.pd, f.alpha, f.df,
-                     f.t_const, W->logp.d(), W->zz.d(), s, W->scal.d(), W->r.d(), W->rk.d(),
-                     value, lp_parts ? W->lp_part.d() : nullptr, lp_parts ? nlp : 0, f.tconst);
-  // cotangent of S: G_S = Z^T diag(r / s) G
+  // cotangent of S: G_S = Z^T diag(r / s) G, r the objective's weights
   GemmOp g = mm(D, D, N, z, true, W->G.d(), false, W->GS.d());
-  g.kscale = W->rk.d();
-  FR_HIP(gemm(g, st));
+  if (weights_fused() && N <= 512 && gemm_detail::glds_ok_shape(g)) {
+    WeightsArgs wa{N, D, f.chivi, f.pd, f.alpha, f.df, f.t_const, W->logp.d(), W->zz.d(), s,
+                   W->scal.d(), W->r.d(), W->rk.d(), value,
+                   lp_parts ? W->lp_part.d() : nullptr, lp_parts ? nlp : 0, f.tconst};
+    FR_HIP(gemm_hook<WeightsHook>(g, wa, st));
+  } else {
+    hipLaunchKernelGGL(fr_weights_kernel, dim3(1), dim3(1024), 0, st, N, D, f.chivi, f.pd, f.alpha,
+                       f.df, f.t_const, W->logp.d(), W->zz.d(), s, W->scal.d(), W->r.d(),
+                       W->rk.d(), value, lp_parts ? W->lp_part.d() : nullptr, lp_parts ? nlp : 0,
+                       f.tconst);
+    g.kscale = W->rk.d();
+    FR_HIP(gemm(g, st));
+  }
   if (!fused)
     hipLaunchKernelGGL(fr_colsum_kernel, dim3(blocks(D, 64)), dim3(1024), 0, st, N, D, W->r.d(),
                        W->G.d(), grad);
@@ -1858,7 +2148,7 @@ int fr_moments(FrWork* W, int D, const double* lam, double* sigma, double* eig, 
 // failed pass did, not from where that pass ended.
 int fr_warm_save(FrWork* W, hipStream_t st) {
   W->wsnap_h = FrWork::WarmHost{W->warm, W->have_z, W->zv_init, W->last_hz, false, W->pv_cur, -1,
-                                W->owner};
+                                W->c_slot, W->owner};
   if (W->D == 0 || !W->sched.p) return 0;   // nothing warm yet: the first step is cold
   const size_t D = (size_t)W->D, vec = sizeof(double) * D;
   FR_HIP(W->wsnap.reserve(6 * vec + vec * D + sizeof(FrSched)));
@@ -1888,6 +2178,7 @@ int fr_warm_restore(FrWork* W, hipStream_t st) {
   W->zv_init = h.zv_init;
   W->last_hz = h.last_hz;
   W->pv_cur = h.pv_cur;
+  W->c_slot = h.c_slot;
   W->owner = h.owner;
   W->prep_owner = nullptr;
   if (!h.valid) {

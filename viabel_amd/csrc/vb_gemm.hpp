@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace vbk {
 
@@ -350,9 +351,11 @@ __device__ __forceinline__ void vm_wait_tiles(int pending) {
 #ifdef VB_GEMM_PROF
 // phase timestamps (s_memrealtime, 100 MHz) of thread 0 of every block of the
 // last launch: [0] entry, [1] after the skip test, [2] main loop start,
-// [3..10] after each of the first 8 k stages' barriers, [14] main loop end, [11]
-// k parts reduced, [12] tile stored, [13] partial sums stored, [15] epilogue end
-__device__ unsigned long long g_gemm_ts[1024][16];
+// [3..10] after each of the first 8 k stages' barriers, [14] main loop end, [16]
+// accumulators summed (MFMA results in registers), [11] k parts reduced, [17]
+// epilogue operands read (alpha, partners' sums), [12] tile stored, [13] partial
+// sums stored, [15] epilogue end
+__device__ unsigned long long g_gemm_ts[1024][24];
 #define VB_GEMM_TS(k)                                                                \
   do {                                                                               \
     if (threadIdx.x == 0 && blockIdx.x + blockIdx.y * gridDim.x < 1024)              \
@@ -362,9 +365,13 @@ __device__ unsigned long long g_gemm_ts[1024][16];
 #define VB_GEMM_TS(k) do {} while (0)
 #endif
 
-template <bool TA, bool TB>
+// KSC: the A fragments are scaled by a per-k factor read from LDS (ks, K
+// doubles), after the fragment reads: the same product a * ks that the
+// register-staged loop forms at its LDS store, so the bits are the same.  mid()
+// runs after the first stages are issued (a hook's loads then overlap them).
+template <bool TA, bool TB, bool KSC, class Mid>
 __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, double* lds,
-                                              d4 (&acc)[4]) {
+                                              d4 (&acc)[4], const double* ks, Mid&& mid) {
   // A rows: m when not transposed (k contiguous), k when transposed.
   // B rows: n when transposed (k contiguous), k otherwise.
   constexpr bool AK = !TA, BK = TB;
@@ -399,18 +406,21 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
 #pragma unroll
   for (int s = 0; s < GS - 1; ++s)
     if (s < nt) issue(s);
+  mid();
   // fragment offsets within a stage for this wave's 4 NSUB k4-steps (sub-tile u,
   // step s: k = 32 u + 16 h + 4 s + kq)
   const int ra = wm * 16 + (lane & 15), cb = wn * 16 + (lane & 15), kq = lane >> 4;
   constexpr int NST = 4 * NSUB;
   typedef __attribute__((address_space(3))) double lds_f64;
   const unsigned la = (unsigned)(uintptr_t)((lds_f64*)sA), lb = (unsigned)(uintptr_t)((lds_f64*)sB);
-  unsigned xa[NST], xb[NST];
+  unsigned xa[NST], xb[NST], xk[KSC ? NST : 1];
+  const unsigned lk = KSC ? (unsigned)(uintptr_t)((const lds_f64*)ks) : 0u;
 #pragma unroll
   for (int f = 0; f < NST; ++f) {
     const int kk = 32 * (f >> 2) + 16 * h + 4 * (f & 3) + kq;
     xa[f] = la + 8u * (unsigned)(AK ? glds_at<true>(ra, kk) : glds_at<false>(kk, ra));
     xb[f] = lb + 8u * (unsigned)(BK ? glds_at<true>(cb, kk) : glds_at<false>(kk, cb));
+    if constexpr (KSC) xk[f] = lk + 8u * (unsigned)kk;
   }
   VB_GEMM_TS(2);
   for (int it = 0; it < nt; ++it) {
@@ -427,19 +437,29 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
     // Four steps' reads (8) stay in flight: step f + 4 is issued after step f's
     // MFMA, into its own registers (lgkmcnt counts LDS reads in order)
     const unsigned so = (unsigned)((it % GS) * TD * 8);
-    double fa[NST], fb[NST];
+    const unsigned ko = (unsigned)(it * KTG * 8);
+    double fa[NST], fb[NST], fk[KSC ? NST : 1];
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
       asm volatile("ds_read_b64 %0, %1" : "=v"(fa[f]) : "v"(xa[f] + so));
       asm volatile("ds_read_b64 %0, %1" : "=v"(fb[f]) : "v"(xb[f] + so));
+      if constexpr (KSC) asm volatile("ds_read_b64 %0, %1" : "=v"(fk[f]) : "v"(xk[f] + ko));
     }
 #pragma unroll
     for (int f = 0; f < NST; ++f) {
       const int ahead = (NST - 1 - f) < 3 ? (NST - 1 - f) : 3;   // steps issued after f
-      if (ahead == 3) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(fa[f]), "+v"(fb[f]));
-      else if (ahead == 2) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(fa[f]), "+v"(fb[f]));
-      else if (ahead == 1) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(fa[f]), "+v"(fb[f]));
-      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[f]), "+v"(fb[f]));
+      if constexpr (KSC) {   // three reads per step
+        if (ahead == 3) asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(fa[f]), "+v"(fb[f]), "+v"(fk[f]));
+        else if (ahead == 2) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(fa[f]), "+v"(fb[f]), "+v"(fk[f]));
+        else if (ahead == 1) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(fa[f]), "+v"(fb[f]), "+v"(fk[f]));
+        else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[f]), "+v"(fb[f]), "+v"(fk[f]));
+        fa[f] *= fk[f];
+      } else {
+        if (ahead == 3) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(fa[f]), "+v"(fb[f]));
+        else if (ahead == 2) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(fa[f]), "+v"(fb[f]));
+        else if (ahead == 1) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(fa[f]), "+v"(fb[f]));
+        else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[f]), "+v"(fb[f]));
+      }
 #ifdef VB_GEMM_NOMFMA
       acc[f & 3][0] += fa[f] * fb[f];
 #else
@@ -448,6 +468,8 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
       if (f + 4 < NST) {
         asm volatile("ds_read_b64 %0, %1" : "=v"(fa[f + 4]) : "v"(xa[f + 4] + so));
         asm volatile("ds_read_b64 %0, %1" : "=v"(fb[f + 4]) : "v"(xb[f + 4] + so));
+        if constexpr (KSC)
+          asm volatile("ds_read_b64 %0, %1" : "=v"(fk[f + 4]) : "v"(xk[f + 4] + ko));
       }
     }
   }
@@ -469,9 +491,24 @@ __device__ __forceinline__ void tri_tile(int b, int nt, int& bi, int& bj) {
   bj = i + b;
 }
 
-template <bool TA, bool TB, bool KS, bool DUAL>
+// A GEMM kernel may carry a hook (gemm_f64_hook_kernel): pre() runs before the
+// main loop (e.g. issues loads whose latency then hides under it), post(lds)
+// after it; a non-null return of post is a block-local Newton-Schulz iteration-0
+// coefficient set used in place of GemmOp::ns0 (a schedule the block computed).
+struct NoHook {
+  static constexpr bool kKScale = false;   // pre() leaves K scales of A in LDS (kscale())
+  static constexpr int kLds = 1;           // doubles of LDS scratch the hook uses
+  __device__ __forceinline__ void pre() {}
+  __device__ __forceinline__ const double* post() { return nullptr; }
+  __device__ __forceinline__ const double* kscale() const { return nullptr; }
+};
+
+template <bool TA, bool TB, bool KS, bool DUAL, class Hook = NoHook>
 __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int slot,
-                                          double (*sA)[BUF], double (*sB)[BUF], double* lds) {
+                                          double (*sA)[BUF], double (*sB)[BUF], double* lds,
+                                          Hook&& hook = Hook{}) {
+  using H = std::decay_t<Hook>;
+  constexpr bool kHook = !std::is_same_v<H, NoHook>;
   // A is k-contiguous when not transposed; B is k-contiguous when transposed.
   constexpr bool AK = !TA, BK = TB;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -489,9 +526,15 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
   bool done = false;
   if constexpr (!KS && !DUAL) {
     if (g.glds) {   // aligned shapes: LDS-DMA main loop (same k order, same bits)
-      mainloop_glds<TA, TB>(g, i0, j0, lds, acc);
+      mainloop_glds<TA, TB, H::kKScale>(g, i0, j0, lds, acc, hook.kscale(), [&]() {
+        if constexpr (kHook) hook.pre();
+      });
       done = true;
     }
+  }
+  // (a hook that scales K runs on the LDS-DMA loop only: gemm_hook checks)
+  if constexpr (kHook && !H::kKScale) {
+    if (!done) hook.pre();
   }
   if (!done) {
   const int nt1 = (g.K + KT - 1) / KT;
@@ -560,10 +603,20 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
   }
   }
   d4 r4 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+#ifdef VB_GEMM_PROF
+  asm volatile("" : "+v"(r4));
+#endif
+  VB_GEMM_TS(16);
   if constexpr (DUAL) {
     const d4 r2 = (acc2[0] + acc2[1]) + (acc2[2] + acc2[3]);
     // combine here so the epilogue's alpha applies to both: alpha r + alpha2 r2
     r4 = r4 + (g.alpha2 / g.alpha) * r2;
+  }
+  // hook: after the main loop
+  const double* ns0 = g.ns0;
+  if constexpr (kHook) {
+    const double* h = hook.post();
+    if (h) ns0 = h;
   }
   // k parts 1.. hand their partial tiles to part 0 through LDS (fixed order)
   double* red = sA[0];
@@ -588,6 +641,13 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
     const double qfx = (g.qf_x && col < g.N) ? g.qf_x[col] : 0.0;
     const double alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
     const double shift = g.sq_shift_dev ? *g.sq_shift_dev : g.sq_shift;
+#ifdef VB_GEMM_PROF
+    {
+      double a_ = alpha, s_ = shift;
+      asm volatile("" : "+v"(a_), "+v"(s_), "+v"(r4));
+    }
+#endif
+    VB_GEMM_TS(17);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = i0 + wm * 16 + kq + 4 * r;
@@ -596,10 +656,10 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
         if (g.row_div) v = v / g.row_div[row];
         if (g.col_bias) v = g.col_bias[col] + v;
         if (row == col) v += g.diag;
-        if (g.ns0) {
+        if (ns0) {
           const double a = g.A[(long long)row * g.lda + col];
-          v = fma(g.ns0[1], a, g.ns0[0] * r4[r]);
-          g.ns0_z[(long long)row * g.ldc + col] = g.ns0[2] * ((row == col ? 3.0 : 0.0) - g.ns0[3] * a);
+          v = fma(ns0[1], a, ns0[0] * r4[r]);
+          g.ns0_z[(long long)row * g.ldc + col] = ns0[2] * ((row == col ? 3.0 : 0.0) - ns0[3] * a);
         }
         double* c = g.C + (long long)row * g.ldc + col;
         if (g.dot_with) dt = fma(g.dot_with[(long long)row * g.ldc + col], v, dt);
@@ -610,7 +670,7 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
         *c = v;
         if (mirror) {
           g.C[(long long)col * g.ldc + row] = v;
-          if (g.ns0) g.ns0_z[(long long)col * g.ldc + row] = g.ns0_z[(long long)row * g.ldc + col];
+          if (ns0) g.ns0_z[(long long)col * g.ldc + row] = g.ns0_z[(long long)row * g.ldc + col];
         }
         const double e = row == col ? v - shift : v;
         sq += e * e;
@@ -701,6 +761,32 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   VB_GEMM_TS(15);
 }
 
+// The same kernel with a hook (see NoHook) built in registers from its
+// arguments (Hook(args)); one GemmOp, no skip / copy control (the hook's
+// kernels are plain products).
+template <bool TA, bool TB, class Hook>
+__global__ __launch_bounds__(NTH) void gemm_f64_hook_kernel(GemmGroup gg, typename Hook::Args ha) {
+  const GemmOp& g = gg.op[0];
+  kernarg_warm(g);
+  __shared__ __attribute__((aligned(16))) double smem[SMEM];
+  __shared__ __attribute__((aligned(16))) double hlds[Hook::kLds];
+  double(*sA)[BUF] = reinterpret_cast<double(*)[BUF]>(smem);
+  double(*sB)[BUF] = reinterpret_cast<double(*)[BUF]>(smem + 2 * BUF);
+  int bx = blockIdx.x, by = blockIdx.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
+  if (g.sym) {
+    tri_tile(blockIdx.x, (g.N + BT - 1) / BT, by, bx);
+    slot = blockIdx.x;
+  }
+  gemm_tile<TA, TB, false, false>(g, bx, by, slot, sA, sB, smem, Hook(ha, slot, hlds));
+}
+
+// shape / alignment conditions of the LDS-DMA loop (glds_ok without the A/B switch)
+inline bool glds_ok_shape(const GemmOp& o) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return o.M % 32 == 0 && o.N % 32 == 0 && o.K % KTG == 0 && !o.kscale && !o.A2 &&
+         o.lda % 2 == 0 && o.ldb % 2 == 0 && al(o.A) && al(o.B);
+}
+
 }  // namespace gemm_detail
 
 // The LDS-DMA main loop needs whole 32 x 32 x KTG tiles and 16-byte aligned pairs.
@@ -776,5 +862,27 @@ inline hipError_t gemm_group(const GemmOp* ops, int n, hipStream_t s) {
 }
 
 inline hipError_t gemm(const GemmOp& g, hipStream_t s) { return gemm_group(&g, 1, s); }
+
+// One product (no kscale / dual) with a hook object (gemm_f64_hook_kernel).
+template <class Hook>
+inline hipError_t gemm_hook(const GemmOp& g0, const typename Hook::Args& hook, hipStream_t s) {
+  using namespace gemm_detail;
+  if (g0.M <= 0 || g0.N <= 0 || g0.kscale || g0.A2 || g0.skip_flag) return hipErrorInvalidValue;
+  if (Hook::kKScale && !glds_ok_shape(g0)) return hipErrorInvalidValue;
+  GemmGroup gg{};
+  gg.op[0] = g0;
+  gg.op[0].glds = (glds_ok(g0) || (Hook::kKScale && glds_ok_shape(g0))) ? 1 : 0;
+  if (!gemm_sym_enabled()) gg.op[0].sym = 0;
+  if (gg.op[0].sym && (g0.M != g0.N || g0.rp_part)) return hipErrorInvalidValue;
+  const unsigned ntn = (unsigned)((g0.N + BT - 1) / BT);
+  const dim3 grid = gg.op[0].sym ? dim3(ntn * (ntn + 1) / 2) : dim3(ntn, (unsigned)((g0.M + BT - 1) / BT));
+  if (!g0.ta && !g0.tb)
+    hipLaunchKernelGGL((gemm_f64_hook_kernel<false, false, Hook>), grid, dim3(NTH), 0, s, gg, hook);
+  else if (g0.ta && !g0.tb)
+    hipLaunchKernelGGL((gemm_f64_hook_kernel<true, false, Hook>), grid, dim3(NTH), 0, s, gg, hook);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
 
 }  // namespace vbk
