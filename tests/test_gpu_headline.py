@@ -48,6 +48,41 @@ def test_config3_klvi_call_numpy_stream(N):
         _close(g, og, 1e-10)
 
 
+def test_config3_short_launches_values_in_kernel():
+    """The driver's shape (a 5-step warm-up launch, then 20-step launches): launches
+    of <= 24 steps reduce their per-step values inside sep_kernel (the last block
+    to finish sums the blocks' write-through partials; vb_capi.hip
+    sep_values_fused), longer ones in a second launch.  Launches of 5, 20 x 5, 1,
+    24 and 25 steps against the oracle on the C-oracle Philox draws: values,
+    history rows and lambda to 1e-7."""
+    from viabel_amd import vb, targets
+    from oracle import vb_oracle as vo, rng_oracle as ro
+    N, W, LR, EPS = 128, 10, 0.01, 0.1
+    chunks = [5, 20, 20, 20, 20, 20, 1, 24, 25]
+    n_iters = sum(chunks)
+    fam = vb.mean_field_gaussian_variational_family(D, rng='philox')
+    obj = vb.black_box_klvi(fam, targets.isogauss(D), N)
+    init = np.concatenate([np.zeros(D), np.ones(D)])
+    run = vb.DeviceRun(obj, n_iters, init[None, :], window=W, learning_rate=LR, epsilon=EPS)
+    done = 0
+    for cs in chunks:
+        run.advance_philox(cs, 0, 3, done)
+        done += cs
+    lam, hist, vals, smooth = run.result()
+    ofam = vo.Family('gauss', D)
+    step = [0]
+
+    def f(l):
+        eps = ro.noise(0, 3, step[0], N, D, 'gauss')
+        step[0] += 1
+        return vo.klvi_value_grad(ofam, 'isogauss', l, N, eps=eps)
+    osm, ohist, ovals, _ = vo.adagrad_optimize(n_iters, f, init, window=W, learning_rate=LR,
+                                               epsilon=EPS)
+    np.testing.assert_allclose(vals[0], ovals, rtol=1e-7, atol=1e-7)
+    _close(hist[0], ohist, 1e-7)
+    _close(lam[0], ohist[-1], 1e-7)
+
+
 @pytest.mark.parametrize('N,n_iters', [(128, 300), (256, 130)])
 def test_config3_bench_run_philox_trajectory(N, n_iters):
     from viabel_amd import vb, targets

@@ -250,6 +250,17 @@ int block_pf_enabled() {
   return on;
 }
 
+// VIABEL_AMD_SEP_FUSE_VALUES=0: short column-pair chunks reduce their per-step
+// values in a second launch (sep_values_kernel) instead of the kernel's last block
+// (A/B switch)
+bool sep_values_fused() {
+  static const bool on = [] {
+    const char* e = std::getenv("VIABEL_AMD_SEP_FUSE_VALUES");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int check_ctx(vb_ctx* c) {
   if (!c) return fail(VB_EINVAL, "null vb_ctx");
   VB_HIP(hipSetDevice(c->device));
@@ -767,6 +778,7 @@ struct vb_run {
   int n_waves = 0;
   int max_chunk = 256;
   DevBuf lam, ring, hist, values, vpart, noise, smooth;
+  DevBuf ticket;  // column-pair path: the in-kernel value combine's block counter
   DevBuf noise_lq;  // pre-drawn log q partials (block kernel, predraw)
   // full-rank family / wide mean-field: one value_grad + update per step
   bool fr = false, wide = false;
@@ -901,11 +913,13 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
   if ((rc = r->smooth.reserve(sizeof(double) * P * n_problems)) != VB_OK) return bail(rc);
   if (sep && (rc = r->vpart.reserve(sizeof(double) * r->n_waves * r->max_chunk)) != VB_OK)
     return bail(rc);
+  if (sep && (rc = r->ticket.reserve(sizeof(unsigned))) != VB_OK) return bail(rc);
   In di;
   if ((rc = di.stage(c, 0, init, P * n_problems)) != VB_OK) return bail(rc);
   hipError_t e = hipMemcpyAsync(r->lam.p, di.d, sizeof(double) * P * n_problems,
                                 hipMemcpyDeviceToDevice, c->stream);
   if (e == hipSuccess) e = hipMemsetAsync(r->ring.p, 0, sizeof(double) * P * r->W * n_problems, c->stream);
+  if (e == hipSuccess && sep) e = hipMemsetAsync(r->ticket.p, 0, sizeof(unsigned), c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) return bail(fail(VB_EDEVICE, "run init failed: %s", hipGetErrorString(e)));
   *out = r;
@@ -1080,6 +1094,11 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
       a.k0 = k0;
       a.k1 = k1;
       a.stream = noise->stream;
+      // short chunks: the per-step values inside the kernel (one launch per chunk)
+      a.fuse_values = (cs <= vbk::kSepFuseSteps && sep_values_fused()) ? 1 : 0;
+      a.ticket = static_cast<unsigned*>(r->ticket.p);
+      a.values = r->values.d();
+      a.c0 = sep_c0(r->fi, a.pd != 0);
       std::pair<hipEvent_t, hipEvent_t>* ev;
       HostTrace ht;
       VB_TRY(r->next_event(cs, &ev));
@@ -1088,8 +1107,9 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
       ht.mark();
       VB_HIP(vbk::launch_sep(r->fi.kind, r->tgt, host, a, c->stream));
       ht.mark();
-      VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, sep_c0(r->fi, a.pd != 0), r->values.d() + a.step0,
-                                    c->stream));
+      if (!a.fuse_values)
+        VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, sep_c0(r->fi, a.pd != 0),
+                                      r->values.d() + a.step0, c->stream));
       ht.mark();
       if (ev) VB_HIP(hipEventRecord(ev->second, c->stream));
       ht.mark();

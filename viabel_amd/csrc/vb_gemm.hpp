@@ -523,6 +523,16 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
   for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int c = 0; c < (DUAL ? 4 : 1); ++c) acc2[c] = d4{0.0, 0.0, 0.0, 0.0};
+  // the epilogue's device scalars (written by earlier launches), loaded now so
+  // their latency hides under the main loop
+  double alpha = g.alpha, shift = g.sq_shift;
+  if (g.alpha_dev) alpha = g.alpha * *g.alpha_dev;
+  if (g.sq_shift_dev) shift = *g.sq_shift_dev;
+  double ns0v[4] = {0.0, 0.0, 0.0, 0.0};
+  if (g.ns0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ns0v[k] = g.ns0[k];
+  }
   bool done = false;
   if constexpr (!KS && !DUAL) {
     if (g.glds) {   // aligned shapes: LDS-DMA main loop (same k order, same bits)
@@ -613,10 +623,12 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
     r4 = r4 + (g.alpha2 / g.alpha) * r2;
   }
   // hook: after the main loop
-  const double* ns0 = g.ns0;
   if constexpr (kHook) {
     const double* h = hook.post();
-    if (h) ns0 = h;
+    if (h) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ns0v[k] = h[k];
+    }
   }
   // k parts 1.. hand their partial tiles to part 0 through LDS (fixed order)
   double* red = sA[0];
@@ -637,10 +649,9 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
     const int col = j0 + wn * 16 + (lane & 15);
     double sq = 0.0, dt = 0.0, qf = 0.0, rp[4] = {0.0, 0.0, 0.0, 0.0};
     const bool mirror = g.sym && bx != by;   // also store the tile transposed
+    const bool is_ns0 = g.ns0 != nullptr;
     const double rpx = (g.rp_x && col < g.N) ? g.rp_x[col] : 0.0;
     const double qfx = (g.qf_x && col < g.N) ? g.qf_x[col] : 0.0;
-    const double alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
-    const double shift = g.sq_shift_dev ? *g.sq_shift_dev : g.sq_shift;
 #ifdef VB_GEMM_PROF
     {
       double a_ = alpha, s_ = shift;
@@ -648,32 +659,44 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
     }
 #endif
     VB_GEMM_TS(17);
+    // two passes: every load (per-element operands) first, then every store, so no
+    // wait for a load ever waits for an earlier row's stores as well (vmcnt counts
+    // both); the arithmetic and its order are unchanged
+    double vv[4], zv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = i0 + wm * 16 + kq + 4 * r;
+      vv[r] = zv[r] = 0.0;
       if (row < g.M && col < g.N) {
         double v = alpha * r4[r];
         if (g.row_div) v = v / g.row_div[row];
         if (g.col_bias) v = g.col_bias[col] + v;
         if (row == col) v += g.diag;
-        if (ns0) {
+        if (is_ns0) {
           const double a = g.A[(long long)row * g.lda + col];
-          v = fma(ns0[1], a, ns0[0] * r4[r]);
-          g.ns0_z[(long long)row * g.ldc + col] = ns0[2] * ((row == col ? 3.0 : 0.0) - ns0[3] * a);
+          v = fma(ns0v[1], a, ns0v[0] * r4[r]);
+          zv[r] = ns0v[2] * ((row == col ? 3.0 : 0.0) - ns0v[3] * a);
         }
-        double* c = g.C + (long long)row * g.ldc + col;
         if (g.dot_with) dt = fma(g.dot_with[(long long)row * g.ldc + col], v, dt);
         if (g.rp_x) rp[r] = v * rpx;
         if (g.qf_x) qf = fma(g.qf_x[row] * v, qfx, qf);
         if (g.rp_w) rp[r] = v * g.rp_w[(long long)row * g.ldc + col];
-        if (g.beta != 0.0) v += g.beta * *c;
-        *c = v;
-        if (mirror) {
-          g.C[(long long)col * g.ldc + row] = v;
-          if (ns0) g.ns0_z[(long long)col * g.ldc + row] = g.ns0_z[(long long)row * g.ldc + col];
-        }
+        if (g.beta != 0.0) v += g.beta * g.C[(long long)row * g.ldc + col];
+        vv[r] = v;
         const double e = row == col ? v - shift : v;
         sq += e * e;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = i0 + wm * 16 + kq + 4 * r;
+      if (row < g.M && col < g.N) {
+        g.C[(long long)row * g.ldc + col] = vv[r];
+        if (is_ns0) g.ns0_z[(long long)row * g.ldc + col] = zv[r];
+        if (mirror) {
+          g.C[(long long)col * g.ldc + row] = vv[r];
+          if (is_ns0) g.ns0_z[(long long)col * g.ldc + row] = zv[r];
+        }
       }
     }
     VB_GEMM_TS(12);

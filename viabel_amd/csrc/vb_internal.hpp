@@ -42,7 +42,17 @@ struct SepArgs {
   const double* noise;    // host noise [n_steps][N][D] or null
   uint32_t k0, k1, stream;
   int pairs2, blocks2, blocks1;  // filled by the launcher (2-pair / 1-pair split)
+  // in-kernel per-step values (n_steps <= kSepFuseSteps): blocks sum their pairs'
+  // partials in LDS, store one partial per (step, block) into vpart with
+  // write-through stores, and the last block to finish (ticket) sums them in a
+  // fixed order into values[step0 .. step0 + n_steps) = -(c0 + sum); else
+  // launch_sep_values does it (a second launch)
+  int fuse_values;
+  unsigned* ticket;       // zero between launches (the last block resets it)
+  double* values;
+  double c0;
 };
+constexpr int kSepFuseSteps = 24;
 
 // Arguments of the block-per-problem kernel (any target, D <= kBlockDMax).
 struct BlockArgs {

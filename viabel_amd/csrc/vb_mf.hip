@@ -165,7 +165,7 @@ __device__ unsigned long long g_sep_clk[kTsWaves][16];  // s_memtime (core clock
 template <class TGT, bool TFAM, bool HOST, int PPW, bool REGRING>
 __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, int wave,
                                          const double2* sct, const double2* ltab,
-                                         unsigned long long t_entry = 0) {
+                                         unsigned long long t_entry = 0, double* s_vp = nullptr) {
   constexpr int LPP = 64 / PPW;       // lanes per column pair
   constexpr int SL = LPP / 4;         // slot lanes per parameter
 #ifdef VB_SEP_PROF
@@ -298,7 +298,10 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
     if ((s & 3) == 3 || s + 1 == a.n_steps) {
       const double tot = reduce4<PPW>(lane, v3, v2, v1, v0);  // owner q: step s - 3 + q
       const int st = s - 3 + own;
-      if (rep && live && st >= (s & ~3)) a.vpart[(long long)st * a.n_waves + w] = tot;
+      if (rep && live && st >= (s & ~3)) {
+        if (s_vp) s_vp[st * 16 + (threadIdx.x >> 6) * PPW + grp] = tot;   // block-local pair
+        else a.vpart[(long long)st * a.n_waves + w] = tot;
+      }
     }
 
     if (a.emit_grad) {
@@ -412,15 +415,75 @@ void sep_kernel(SepArgs a) {
   }
   const int wid = threadIdx.x >> 6;
   double* ring = REGRING ? nullptr : &s_ring[REGRING ? 0 : wid][0];
+  // per-step value partials of the block's (up to 16) column pairs (fuse_values)
+  __shared__ double s_vp[kSepFuseSteps * 16];
+  __shared__ int s_last;
+  const bool fuse = a.fuse_values != 0;
+  if (fuse) {
+    for (int i = threadIdx.x; i < kSepFuseSteps * 16; i += blockDim.x) s_vp[i] = 0.0;
+    __syncthreads();
+  }
   if ((int)blockIdx.x < a.blocks2) {
     const int wave = blockIdx.x * 4 + wid;
-    if (wave * PPW_BIG >= a.pairs2) return;
-    sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave, s_sct, s_lt, t_entry);
+    if (wave * PPW_BIG < a.pairs2)
+      sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave, s_sct, s_lt, t_entry,
+                                                  fuse ? s_vp : nullptr);
   } else {
     const int pair = a.pairs2 + (blockIdx.x - a.blocks2) * 4 + wid;
-    if (pair >= a.n_pairs) return;
-    sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair, s_sct, s_lt, t_entry);
+    if (pair < a.n_pairs)
+      sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair, s_sct, s_lt, t_entry,
+                                            fuse ? s_vp : nullptr);
   }
+  if (!fuse) return;
+  // the block's partial of every step (its pairs in order), write-through so the
+  // last block sees it from any XCD; then one ticket per block
+  __syncthreads();
+  const int t = threadIdx.x, ns = a.n_steps, nb = (int)gridDim.x;
+  if (t < ns) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += s_vp[t * 16 + k];
+    __hip_atomic_store(a.vpart + (long long)t * nb + blockIdx.x, v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const unsigned old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == (unsigned)(nb - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // last block: values[step] = -(c0 + sum over blocks in order); thread t reads
+  // blocks t, t + 256, ... of every step (write-through loads, all of a round
+  // in flight at once), a fixed-order tree over the lanes, then over the waves
+  __shared__ double s_red[kSepFuseSteps * 4];
+  double acc[kSepFuseSteps];
+#pragma unroll
+  for (int st = 0; st < kSepFuseSteps; ++st) acc[st] = 0.0;
+  for (int b = t; b < nb; b += 256) {
+    double v[kSepFuseSteps];
+#pragma unroll
+    for (int st = 0; st < kSepFuseSteps; ++st)
+      v[st] = st < ns ? __hip_atomic_load(a.vpart + (long long)st * nb + b, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT)
+                      : 0.0;
+#pragma unroll
+    for (int st = 0; st < kSepFuseSteps; ++st) acc[st] += v[st];
+  }
+#pragma unroll
+  for (int st = 0; st < kSepFuseSteps; ++st) {
+    if (st < ns) {
+      const double v = wave_sum_dpp(acc[st]);
+      if ((t & 63) == 0) s_red[st * 4 + (t >> 6)] = v;
+    }
+  }
+  __syncthreads();
+  if (t < ns) {
+    const double v = (s_red[t * 4] + s_red[t * 4 + 1]) + (s_red[t * 4 + 2] + s_red[t * 4 + 3]);
+    a.values[a.step0 + t] = -(a.c0 + v);
+  }
+  if (t == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // values[i] = -(c0 + sum_w vpart[s][w]), fixed-order tree reduction.  One
@@ -1705,6 +1768,79 @@ __global__ __launch_bounds__(256) void logw_sep_kernel(int D, long long m, const
   if (lane == 0) lw[r] = lp - lq;
 }
 
+// VB_LOGW_PAIR_LOOPS: the per-pair gamma loops of draw_pair instead (A/B build)
+__device__ __forceinline__ constexpr bool logw_gamma_row() {
+#ifdef VB_LOGW_PAIR_LOOPS
+  return false;
+#else
+  return true;
+#endif
+}
+
+// The gamma variates of a row's t draws, every pair's Marsaglia-Tsang attempts in
+// ONE loop per thread (draw_pair runs one loop per pair; a wave repeats a pair's
+// loop while any lane still rejects, ~1.4 passes per pair at shape 20): the
+// thread walks its pairs in order, attempt k of pair j from Philox purpose 1 + k
+// as in gamma_pair, so the accepted values are bit for bit gamma_pair's.  The
+// loop ends when every lane has finished all its pairs.  g[2 j + c] -> sg (LDS,
+// [DMAX][256] per block).
+template <int DMAX>
+__device__ __forceinline__ void gamma_row(const Rng& rng, long long r, int npairs, uint32_t step,
+                                          double shape, double* sg, const double2* sct,
+                                          const double2* ltab) {
+  const double d = shape - 1.0 / 3.0;
+  const double c = 1.0 / sqrt(9.0 * d);
+  const int t = threadIdx.x;
+  int j = 0;
+  uint32_t k = 0;
+  bool da = false, db = false;
+  double ga = d, gb = d;
+  while (j < npairs) {
+    const u4 w = rng.draw((uint32_t)j, (uint32_t)r, step, 1u + k);
+    const double u1 = ((double)w.x + 0.5) * 0x1p-32;
+    const double u2 = (double)w.y * 0x1p-32;
+    double sn, cs;
+    const double rr = sqrt_pos(-2.0 * log_u01_tab(u1, ltab));
+    sincospi_tab(2.0 * u2, sn, cs, sct);
+    const double za = rr * cs, zb = rr * sn;
+    const double ua = ((double)w.z + 0.5) * 0x1p-32;
+    const double ub = ((double)w.w + 0.5) * 0x1p-32;
+    if (!da) {
+      double v = 1.0 + c * za;
+      if (v > 0.0) {
+        v = v * v * v;
+        const double lu = log_u01_tab(ua, ltab);
+        const double lv = (v >= 0x1p-1022 && v < 0x1p+1023) ? log_unit_tab(v, ltab) : log(v);
+        if (lu < 0.5 * za * za + d - d * v + d * lv) {
+          ga = d * v;
+          da = true;
+        }
+      }
+    }
+    if (!db) {
+      double v = 1.0 + c * zb;
+      if (v > 0.0) {
+        v = v * v * v;
+        const double lu = log_u01_tab(ub, ltab);
+        const double lv = (v >= 0x1p-1022 && v < 0x1p+1023) ? log_unit_tab(v, ltab) : log(v);
+        if (lu < 0.5 * zb * zb + d - d * v + d * lv) {
+          gb = d * v;
+          db = true;
+        }
+      }
+    }
+    ++k;
+    if ((da && db) || k >= 64u) {
+      sg[(2 * j) * 256 + t] = ga;
+      sg[(2 * j + 1) * 256 + t] = gb;
+      ++j;
+      k = 0;
+      da = db = false;
+      ga = gb = d;
+    }
+  }
+}
+
 // any target with D <= DMAX: one thread per draw
 template <class TGT, bool TFAM, bool HOST, int DMAX>
 __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const double* lam,
@@ -1715,6 +1851,8 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
   __shared__ double s_mu[DMAX], s_ls[DMAX], s_sg[DMAX];
+  // t family, Philox: the row's gamma variates (gamma_row), [DMAX][256]
+  __shared__ double s_gam[(TFAM && !HOST) ? DMAX * 256 : 1];
   // row q of a batched launch (vb_log_weights_rows): its own lambda, output
   // row, noise rows and Philox stream (stream + q * stride)
   const int q = blockIdx.y;
@@ -1737,11 +1875,26 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
   if (r >= m) return;
   double x[DMAX], g[DMAX];
   double lq = 0.0;
+  if constexpr (TFAM && !HOST) {
+    if (logw_gamma_row())
+      gamma_row<DMAX>(rng, r, (D + 1) / 2, step, shape, s_gam, s_sct, s_lt);
+  }
 #pragma unroll
   for (int j = 0; j < (DMAX + 1) / 2; ++j) {
     double e0 = 0.0, e1 = 0.0;
-    if (2 * j < D)
-      draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e0, e1, s_sct, s_lt);
+    if (2 * j < D) {
+      if constexpr (TFAM && !HOST) {
+        if (logw_gamma_row()) {   // the numerators here, the gammas from gamma_row
+          normal_pair_tab(rng.draw((uint32_t)j, (uint32_t)r, step, 0u), e0, e1, s_sct, s_lt);
+          e0 = t_scale * e0 / sqrt(s_gam[(2 * j) * 256 + threadIdx.x]);
+          e1 = t_scale * e1 / sqrt(s_gam[(2 * j + 1) * 256 + threadIdx.x]);
+        } else {
+          draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e0, e1, s_sct, s_lt);
+        }
+      } else {
+        draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e0, e1, s_sct, s_lt);
+      }
+    }
     const double e[2] = {e0, e1};
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
