@@ -66,10 +66,10 @@ int main(int argc, char** argv) {
     for (int k = 1; k < 24; ++k) ph[k] += ((double)ts[b * 24 + k] - (double)ts[b * 24]) * 0.01;
   }
   printf("entry after first block: mean %.2f us\n", ent / nb);
-  const char* nm[18] = {"entry", "skip done", "loop start", "k0", "k1", "k2", "k3", "k4", "k5", "k6", "k7",
+  const char* nm[20] = {"entry", "skip done", "loop start", "k0", "k1", "k2", "k3", "k4", "k5", "k6", "k7",
                         "k-part reduced", "tile stored", "partials done", "loop end", "epilogue end",
-                        "acc summed", "epi operands"};
-  const int order[17] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 14, 16, 11, 17, 12, 13, 15};
+                        "acc summed", "epi operands", "store pass 2 start", "store pass 2 end"};
+  const int order[19] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 14, 16, 11, 17, 12, 13, 15, 18, 19};
   for (int k : order) printf("  %-14s %7.2f us after entry (mean over blocks)\n", nm[k], ph[k] / nb);
   return 0;
 }

@@ -250,13 +250,16 @@ int block_pf_enabled() {
   return on;
 }
 
-// VIABEL_AMD_SEP_FUSE_VALUES=0: short column-pair chunks reduce their per-step
-// values in a second launch (sep_values_kernel) instead of the kernel's last block
-// (A/B switch)
+// VIABEL_AMD_SEP_FUSE_VALUES=1: short column-pair chunks reduce their per-step
+// values in the kernel's last block instead of a second launch
+// (sep_values_kernel).  Measured slower, so off: the 20-step headline launch's
+// device span 81.3 -> 84 us, 5.34 -> 5.58 us/step (the blocks' write-through
+// partial stores and the last block's round trips outlast the 4.3 us launch;
+// profiles/r04/headline_fuse_values_rejected.log)
 bool sep_values_fused() {
   static const bool on = [] {
     const char* e = std::getenv("VIABEL_AMD_SEP_FUSE_VALUES");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }

@@ -523,16 +523,16 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
   for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int c = 0; c < (DUAL ? 4 : 1); ++c) acc2[c] = d4{0.0, 0.0, 0.0, 0.0};
-  // the epilogue's device scalars (written by earlier launches), loaded now so
-  // their latency hides under the main loop
-  double alpha = g.alpha, shift = g.sq_shift;
-  if (g.alpha_dev) alpha = g.alpha * *g.alpha_dev;
-  if (g.sq_shift_dev) shift = *g.sq_shift_dev;
-  double ns0v[4] = {0.0, 0.0, 0.0, 0.0};
-  if (g.ns0) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ns0v[k] = g.ns0[k];
+#ifdef VB_GEMM_EXP_CTOUCH
+  {   // experiment: touch this thread's output rows before the main loop (TLB / L2)
+    const int col_ = j0 + wn * 16 + (lane & 15), row_ = i0 + wm * 16 + kq;
+    if (h == 0 && row_ < g.M && col_ < g.N) {
+      double t_;
+      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(t_) : "v"(g.C + (long long)row_ * g.ldc + col_));
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(t_));
+    }
   }
+#endif
   bool done = false;
   if constexpr (!KS && !DUAL) {
     if (g.glds) {   // aligned shapes: LDS-DMA main loop (same k order, same bits)
@@ -623,12 +623,14 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
     r4 = r4 + (g.alpha2 / g.alpha) * r2;
   }
   // hook: after the main loop
+  // (the epilogue's device scalars are read after the main loop: loaded before
+  // it, they stay live across it and push the kernel past the 128 VGPRs that two
+  // 512-thread blocks per CU allow -- the grouped Y|Z launch then runs in two
+  // rounds, 15.8 -> 19.0 us)
+  const double* ns0 = g.ns0;
   if constexpr (kHook) {
     const double* h = hook.post();
-    if (h) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ns0v[k] = h[k];
-    }
+    if (h) ns0 = h;
   }
   // k parts 1.. hand their partial tiles to part 0 through LDS (fixed order)
   double* red = sA[0];
@@ -649,7 +651,10 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
     const int col = j0 + wn * 16 + (lane & 15);
     double sq = 0.0, dt = 0.0, qf = 0.0, rp[4] = {0.0, 0.0, 0.0, 0.0};
     const bool mirror = g.sym && bx != by;   // also store the tile transposed
-    const bool is_ns0 = g.ns0 != nullptr;
+    const bool is_ns0 = ns0 != nullptr;
+    const double alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
+    double shift = g.sq_shift;
+    if (g.sq_shift_dev) shift = *g.sq_shift_dev;
     const double rpx = (g.rp_x && col < g.N) ? g.rp_x[col] : 0.0;
     const double qfx = (g.qf_x && col < g.N) ? g.qf_x[col] : 0.0;
 #ifdef VB_GEMM_PROF
@@ -674,8 +679,8 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
         if (row == col) v += g.diag;
         if (is_ns0) {
           const double a = g.A[(long long)row * g.lda + col];
-          v = fma(ns0v[1], a, ns0v[0] * r4[r]);
-          zv[r] = ns0v[2] * ((row == col ? 3.0 : 0.0) - ns0v[3] * a);
+          v = fma(ns0[1], a, ns0[0] * r4[r]);
+          zv[r] = ns0[2] * ((row == col ? 3.0 : 0.0) - ns0[3] * a);
         }
         if (g.dot_with) dt = fma(g.dot_with[(long long)row * g.ldc + col], v, dt);
         if (g.rp_x) rp[r] = v * rpx;
@@ -687,6 +692,11 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
         sq += e * e;
       }
     }
+#ifdef VB_GEMM_EXP_EPI2
+    // experiment: the store pass twice (the second one timed at [18])
+    for (int rep_ = 0; rep_ < 2; ++rep_) {
+      if (rep_ == 1) VB_GEMM_TS(18);
+#endif
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = i0 + wm * 16 + kq + 4 * r;
@@ -699,6 +709,10 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
         }
       }
     }
+#ifdef VB_GEMM_EXP_EPI2
+    }
+    VB_GEMM_TS(19);
+#endif
     VB_GEMM_TS(12);
     const double pw = mirror ? 2.0 : 1.0;   // the transposed tile's share of a sum
     if (g.sq_part) {
