@@ -286,6 +286,25 @@ def load_traffic():
         return None
 
 
+def load_valu_busy():
+    """The headline launch's VALU busy fraction measured with rocprofv3 PMC
+    (SQ_ACTIVE_INST_VALU x 4 / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs): the
+    fraction of SIMD cycles issuing a VALU instruction, at the clock the launch ran
+    at), from the committed record scripts/gpu_valu_busy.sh wrote.  A measured
+    counterpart to the instruction-count model's frac, which prices every VALU
+    instruction at 4 cycles."""
+    p = os.path.join(ROOT, 'profiles', 'r04', 'valu_busy_headline.json')
+    try:
+        with open(p) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    disp = d.get('dispatches') or []
+    return {'busy': d.get('timed_dispatch_valu_busy'),
+            'clock_ghz': disp[-1].get('clock_ghz') if disp else None,
+            'formula': d.get('formula'), 'source': 'profiles/r04/valu_busy_headline.json'}
+
+
 def roofline_cfg3(launches, n, traffic):
     """Dominant kernel: sep_kernel (+ its per-step value reduction, one launch
     pair per advance call).  Bytes and VALU instructions are priced for the
@@ -812,6 +831,10 @@ def main():
     if valu and measured and measured.get('valu_fma_f64'):
         valu['measured_fma_f64_peak'] = measured['valu_fma_f64']
         valu['frac_of_measured_fma_f64_peak'] = valu['achieved'] / measured['valu_fma_f64']
+    if valu:
+        busy = load_valu_busy()
+        if busy:
+            valu['pmc_busy'] = busy
     for leg, key in (('cfg3_256', 'hbm_copy'), ('cfg4', 'mfma_f64'), ('cfg5', 'hbm_copy')):
         if isinstance(configs.get(leg), dict):
             add_measured(configs[leg].get('roofline'), measured, key)

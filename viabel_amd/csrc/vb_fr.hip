@@ -641,6 +641,7 @@ struct SchedHook {
   using Args = SchedArgs;
   static constexpr bool kKScale = false;
   static constexpr int kLds = 128;
+  static constexpr int kEpi = kEpiSym | kEpiNs0;   // the iteration-0 product's epilogue
   const SchedArgs& a;
   const int blk;
   double* const lds;
@@ -736,6 +737,7 @@ struct WeightsHook {
   using Args = WeightsArgs;
   static constexpr bool kKScale = true;
   static constexpr int kLds = 512 + 64;
+  static constexpr int kEpi = 0;
   const WeightsArgs& a;
   const int blk;
   double* const lds;

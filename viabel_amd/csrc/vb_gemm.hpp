@@ -137,6 +137,18 @@ struct GemmGroup {
   GemmOp op[2];
 };
 
+// Epilogue / control features of a GemmOp as compile-time bits.  A kernel
+// instantiated for an exact feature set (gemm_group picks one of the sets the
+// full-rank step uses) carries only that code: each launch runs its entry and
+// epilogue from a cold instruction cache (the store phase takes ~1 us the first
+// time and 0.3 us when run again, profiles/r04), so the once-per-launch code is
+// kept short and straight.  kEpiAll: every feature tested at run time.
+enum : int {
+  kEpiRowDiv = 1, kEpiColBias = 2, kEpiDiag = 4, kEpiNs0 = 8, kEpiDot = 16, kEpiRpX = 32,
+  kEpiQf = 64, kEpiRpW = 128, kEpiBeta = 256, kEpiSq = 512, kEpiAlphaDev = 1024,
+  kEpiShiftDev = 2048, kEpiSym = 4096, kEpiSkip = 8192, kEpiAll = 16383
+};
+
 namespace gemm_detail {
 
 using d4 = double __attribute__((ext_vector_type(4)));
@@ -228,7 +240,9 @@ __device__ __forceinline__ double frag(const double* s, int r, int k) {
 // 1 = skipped (converged in an earlier launch); 2 = skipped (this launch's own
 // convergence test).  Every block sums the partials in the same order, so all
 // blocks decide alike.
+template <int EPI = kEpiAll>
 __device__ __forceinline__ int gemm_skip(const GemmOp& g, double* red) {
+  if constexpr (!(EPI & kEpiSkip)) return 0;
   if (!g.skip_flag) return 0;
   __shared__ int s_skip;
   const int t = threadIdx.x;
@@ -498,15 +512,22 @@ __device__ __forceinline__ void tri_tile(int b, int nt, int& bi, int& bj) {
 struct NoHook {
   static constexpr bool kKScale = false;   // pre() leaves K scales of A in LDS (kscale())
   static constexpr int kLds = 1;           // doubles of LDS scratch the hook uses
+  static constexpr int kEpi = kEpiAll;     // epilogue feature set of the hooked product
   __device__ __forceinline__ void pre() {}
   __device__ __forceinline__ const double* post() { return nullptr; }
   __device__ __forceinline__ const double* kscale() const { return nullptr; }
 };
 
-template <bool TA, bool TB, bool KS, bool DUAL, class Hook = NoHook>
+template <bool TA, bool TB, bool KS, bool DUAL, int EPI = kEpiAll, class Hook = NoHook>
 __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int slot,
                                           double (*sA)[BUF], double (*sB)[BUF], double* lds,
                                           Hook&& hook = Hook{}) {
+  // feature f is compiled in when its bit is set; an exact set also drops the
+  // run-time null test of its fields
+  constexpr bool kExact = EPI != kEpiAll;
+  auto has = [&](int f, bool rt) __attribute__((always_inline)) {
+    return (EPI & f) && (kExact || rt);
+  };
   using H = std::decay_t<Hook>;
   constexpr bool kHook = !std::is_same_v<H, NoHook>;
   // A is k-contiguous when not transposed; B is k-contiguous when transposed.
@@ -650,13 +671,13 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
     }
     const int col = j0 + wn * 16 + (lane & 15);
     double sq = 0.0, dt = 0.0, qf = 0.0, rp[4] = {0.0, 0.0, 0.0, 0.0};
-    const bool mirror = g.sym && bx != by;   // also store the tile transposed
-    const bool is_ns0 = ns0 != nullptr;
-    const double alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
+    const bool mirror = has(kEpiSym, g.sym) && bx != by;   // also store the tile transposed
+    const bool is_ns0 = has(kEpiNs0, ns0 != nullptr);
+    const double alpha = has(kEpiAlphaDev, g.alpha_dev) ? g.alpha * *g.alpha_dev : g.alpha;
     double shift = g.sq_shift;
-    if (g.sq_shift_dev) shift = *g.sq_shift_dev;
-    const double rpx = (g.rp_x && col < g.N) ? g.rp_x[col] : 0.0;
-    const double qfx = (g.qf_x && col < g.N) ? g.qf_x[col] : 0.0;
+    if (has(kEpiShiftDev, g.sq_shift_dev)) shift = *g.sq_shift_dev;
+    const double rpx = (has(kEpiRpX, g.rp_x) && col < g.N) ? g.rp_x[col] : 0.0;
+    const double qfx = (has(kEpiQf, g.qf_x) && col < g.N) ? g.qf_x[col] : 0.0;
 #ifdef VB_GEMM_PROF
     {
       double a_ = alpha, s_ = shift;
@@ -664,73 +685,59 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
     }
 #endif
     VB_GEMM_TS(17);
-    // two passes: every load (per-element operands) first, then every store, so no
-    // wait for a load ever waits for an earlier row's stores as well (vmcnt counts
-    // both); the arithmetic and its order are unchanged
-    double vv[4], zv[4];
+    // (a two-pass form -- every load first, then every store -- measured no faster:
+    // the store phase's ~1 us is the cold instruction cache of this once-per-launch
+    // code, 0.3 us when the same stores run a second time; profiles/r04)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = i0 + wm * 16 + kq + 4 * r;
-      vv[r] = zv[r] = 0.0;
       if (row < g.M && col < g.N) {
         double v = alpha * r4[r];
-        if (g.row_div) v = v / g.row_div[row];
-        if (g.col_bias) v = g.col_bias[col] + v;
-        if (row == col) v += g.diag;
+        if (has(kEpiRowDiv, g.row_div)) v = v / g.row_div[row];
+        if (has(kEpiColBias, g.col_bias)) v = g.col_bias[col] + v;
+        if ((EPI & kEpiDiag) && row == col) v += g.diag;
+        double z = 0.0;
         if (is_ns0) {
           const double a = g.A[(long long)row * g.lda + col];
           v = fma(ns0[1], a, ns0[0] * r4[r]);
-          zv[r] = ns0[2] * ((row == col ? 3.0 : 0.0) - ns0[3] * a);
+          z = ns0[2] * ((row == col ? 3.0 : 0.0) - ns0[3] * a);
+          g.ns0_z[(long long)row * g.ldc + col] = z;
         }
-        if (g.dot_with) dt = fma(g.dot_with[(long long)row * g.ldc + col], v, dt);
-        if (g.rp_x) rp[r] = v * rpx;
-        if (g.qf_x) qf = fma(g.qf_x[row] * v, qfx, qf);
-        if (g.rp_w) rp[r] = v * g.rp_w[(long long)row * g.ldc + col];
-        if (g.beta != 0.0) v += g.beta * g.C[(long long)row * g.ldc + col];
-        vv[r] = v;
-        const double e = row == col ? v - shift : v;
-        sq += e * e;
-      }
-    }
-#ifdef VB_GEMM_EXP_EPI2
-    // experiment: the store pass twice (the second one timed at [18])
-    for (int rep_ = 0; rep_ < 2; ++rep_) {
-      if (rep_ == 1) VB_GEMM_TS(18);
-#endif
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = i0 + wm * 16 + kq + 4 * r;
-      if (row < g.M && col < g.N) {
-        g.C[(long long)row * g.ldc + col] = vv[r];
-        if (is_ns0) g.ns0_z[(long long)row * g.ldc + col] = zv[r];
+        double* c = g.C + (long long)row * g.ldc + col;
+        if (has(kEpiDot, g.dot_with)) dt = fma(g.dot_with[(long long)row * g.ldc + col], v, dt);
+        if (has(kEpiRpX, g.rp_x)) rp[r] = v * rpx;
+        if (has(kEpiQf, g.qf_x)) qf = fma(g.qf_x[row] * v, qfx, qf);
+        if (has(kEpiRpW, g.rp_w)) rp[r] = v * g.rp_w[(long long)row * g.ldc + col];
+        if (has(kEpiBeta, g.beta != 0.0)) v += g.beta * *c;
+        *c = v;
         if (mirror) {
-          g.C[(long long)col * g.ldc + row] = vv[r];
-          if (is_ns0) g.ns0_z[(long long)col * g.ldc + row] = zv[r];
+          g.C[(long long)col * g.ldc + row] = v;
+          if (is_ns0) g.ns0_z[(long long)col * g.ldc + row] = z;
+        }
+        if constexpr ((EPI & kEpiSq) != 0) {
+          const double e = row == col ? v - shift : v;
+          sq += e * e;
         }
       }
     }
-#ifdef VB_GEMM_EXP_EPI2
-    }
-    VB_GEMM_TS(19);
-#endif
     VB_GEMM_TS(12);
     const double pw = mirror ? 2.0 : 1.0;   // the transposed tile's share of a sum
-    if (g.sq_part) {
+    if (has(kEpiSq, g.sq_part)) {
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off, 64);
       if (lane == 0) g.sq_part[4 * slot + q] = pw * sq;
     }
-    if (g.dot_part) {
+    if (has(kEpiDot, g.dot_part)) {
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) dt += __shfl_xor(dt, off, 64);
       if (lane == 0) g.dot_part[4 * slot + q] = pw * dt;
     }
-    if (g.qf_part) {
+    if (has(kEpiQf, g.qf_part)) {
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) qf += __shfl_xor(qf, off, 64);
       if (lane == 0) g.qf_part[4 * slot + q] = pw * qf;
     }
-    if (g.rp_part) {
+    if ((EPI & (kEpiRpX | kEpiRpW)) && (kExact || g.rp_part)) {
       // sum over the 16 lanes of a row (lanes 16 kq .. 16 kq + 15 hold row kq + 4 r)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -745,7 +752,7 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
   __syncthreads();
 }
 
-template <bool TA, bool TB, bool KS, bool DUAL>
+template <bool TA, bool TB, bool KS, bool DUAL, int EPI = kEpiAll>
 __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   const GemmOp& g = gg.op[blockIdx.z];
 #ifndef VB_NO_KWARM
@@ -756,7 +763,7 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   double(*sB)[BUF] = reinterpret_cast<double(*)[BUF]>(smem + 2 * BUF);
   VB_GEMM_TS(0);
   int bx = blockIdx.x, by = blockIdx.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
-  if (g.sym) {
+  if ((EPI & kEpiSym) && g.sym) {
     tri_tile(blockIdx.x, (g.N + BT - 1) / BT, by, bx);
     slot = blockIdx.x;
   }
@@ -771,7 +778,7 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
     slot = by * 16 + bx;
   }
 #endif
-  if (const int sk = gemm_skip(g, sB[1])) {
+  if (const int sk = gemm_skip<EPI>(g, sB[1])) {
     // the copy decision uses this block's own test (sk == 2) or state written
     // by earlier launches (sk == 1), never a peer block's stores in this launch
     // (launches without copy_src or conv_iter_out never look at the counter)
@@ -786,7 +793,7 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
         const int row = by * BT + e / BT, col = bx * BT + e % BT;
         if (row < g.M && col < g.N) {
           g.C[(long long)row * g.ldc + col] = g.copy_src[(long long)row * g.ldc + col];
-          if (g.sym && bx != by)
+          if ((EPI & kEpiSym) && g.sym && bx != by)
             g.C[(long long)col * g.ldc + row] = g.copy_src[(long long)col * g.ldc + row];
         }
       }
@@ -794,14 +801,14 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
     return;
   }
   VB_GEMM_TS(1);
-  gemm_tile<TA, TB, KS, DUAL>(g, bx, by, slot, sA, sB, smem);
+  gemm_tile<TA, TB, KS, DUAL, EPI>(g, bx, by, slot, sA, sB, smem);
   VB_GEMM_TS(15);
 }
 
 // The same kernel with a hook (see NoHook) built in registers from its
 // arguments (Hook(args)); one GemmOp, no skip / copy control (the hook's
 // kernels are plain products).
-template <bool TA, bool TB, class Hook>
+template <bool TA, bool TB, class Hook, int EPI = kEpiAll>
 __global__ __launch_bounds__(NTH) void gemm_f64_hook_kernel(GemmGroup gg, typename Hook::Args ha) {
   const GemmOp& g = gg.op[0];
   kernarg_warm(g);
@@ -814,7 +821,7 @@ __global__ __launch_bounds__(NTH) void gemm_f64_hook_kernel(GemmGroup gg, typena
     tri_tile(blockIdx.x, (g.N + BT - 1) / BT, by, bx);
     slot = blockIdx.x;
   }
-  gemm_tile<TA, TB, false, false>(g, bx, by, slot, sA, sB, smem, Hook(ha, slot, hlds));
+  gemm_tile<TA, TB, false, false, EPI>(g, bx, by, slot, sA, sB, smem, Hook(ha, slot, hlds));
 }
 
 // shape / alignment conditions of the LDS-DMA loop (glds_ok without the A/B switch)
@@ -850,6 +857,50 @@ inline bool gemm_sym_enabled() {
   }();
   return on;
 }
+// VIABEL_AMD_GEMM_EPI_EXACT=0: every launch uses the kEpiAll kernel (A/B switch)
+inline bool gemm_epi_exact_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("VIABEL_AMD_GEMM_EPI_EXACT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+namespace gemm_detail {
+// The feature set of one op (after gemm_group's sym override), or kEpiAll when a
+// feature is half-specified (an exact kernel reads every field of its features).
+inline int epi_mask(const GemmOp& o) {
+  int m = 0;
+  if (o.row_div) m |= kEpiRowDiv;
+  if (o.col_bias) m |= kEpiColBias;
+  if (o.diag != 0.0) m |= kEpiDiag;
+  if (o.ns0) { if (!o.ns0_z) return kEpiAll; m |= kEpiNs0; }
+  if (o.dot_with || o.dot_part) { if (!(o.dot_with && o.dot_part)) return kEpiAll; m |= kEpiDot; }
+  if (o.rp_x && o.rp_w) return kEpiAll;
+  if (o.rp_x || o.rp_w) { if (!o.rp_part) return kEpiAll; m |= o.rp_x ? kEpiRpX : kEpiRpW; }
+  else if (o.rp_part) return kEpiAll;
+  if (o.qf_x || o.qf_part) { if (!(o.qf_x && o.qf_part)) return kEpiAll; m |= kEpiQf; }
+  if (o.beta != 0.0) m |= kEpiBeta;
+  if (o.sq_part) m |= kEpiSq;
+  if (o.alpha_dev) m |= kEpiAlphaDev;
+  if (o.sq_shift_dev) m |= kEpiShiftDev;
+  if (o.sym) m |= kEpiSym;
+  if (o.skip_flag) m |= kEpiSkip;
+  return m;
+}
+// The feature sets of the full-rank step (vb_fr.hip) that get an exact kernel.
+#define VB_GEMM_EPI_SETS(X)                                                        \
+  X(0)                                               /* plain products */          \
+  X(kEpiSym | kEpiSq)                                /* Sigma = L L^T */           \
+  X(kEpiSym | kEpiSq | kEpiQf)                       /* Sigma, with z^T Sigma z */ \
+  X(kEpiSym | kEpiNs0)                               /* Newton-Schulz iter 0 */    \
+  X(kEpiSym | kEpiAlphaDev | kEpiDiag | kEpiSq | kEpiShiftDev | kEpiSkip) /* T */  \
+  X(kEpiSym | kEpiAlphaDev | kEpiSkip)               /* Y | Z */                   \
+  X(kEpiDot | kEpiSkip)                              /* PCG Y P, Z R */            \
+  X(kEpiAlphaDev | kEpiRowDiv | kEpiColBias)         /* x = mu + c z Y / s */      \
+  X(kEpiRpW)                                         /* corr_gauss target */
+}  // namespace gemm_detail
+
 // number of 4-per-block partial sums of an n x n result (sym: upper triangle)
 inline int gemm_parts(int n, bool sym) {
   const int t = (n + gemm_detail::BT - 1) / gemm_detail::BT;
@@ -881,6 +932,24 @@ inline hipError_t gemm_group(const GemmOp* ops, int n, hipStream_t s) {
                           : dim3(ntn, (unsigned)((g.M + BT - 1) / BT), (unsigned)n);
   const bool ks = g.kscale != nullptr, dual = g.A2 != nullptr;
   if (ks && dual) return hipErrorInvalidValue;
+  // exact epilogue kernels: plain NN products whose ops share one listed set
+  int epi = kEpiAll;
+  if (!g.ta && !g.tb && !ks && !dual && gemm_epi_exact_enabled()) {
+    epi = epi_mask(gg.op[0]);
+    for (int i = 1; i < n; ++i)
+      if (epi_mask(gg.op[i]) != epi) epi = kEpiAll;
+  }
+  switch (epi) {
+#define VB_EPI_CASE(M)                                                                      \
+  case (M):                                                                                 \
+    hipLaunchKernelGGL((gemm_f64_kernel<false, false, false, false, (M)>), grid, dim3(NTH), 0, \
+                       s, gg);                                                              \
+    return hipGetLastError();
+    VB_GEMM_EPI_SETS(VB_EPI_CASE)
+#undef VB_EPI_CASE
+    default:
+      break;
+  }
 #define VB_GEMM(TA, TB)                                                                 \
   do {                                                                                  \
     if (dual)                                                                           \
@@ -913,8 +982,16 @@ inline hipError_t gemm_hook(const GemmOp& g0, const typename Hook::Args& hook, h
   if (gg.op[0].sym && (g0.M != g0.N || g0.rp_part)) return hipErrorInvalidValue;
   const unsigned ntn = (unsigned)((g0.N + BT - 1) / BT);
   const dim3 grid = gg.op[0].sym ? dim3(ntn * (ntn + 1) / 2) : dim3(ntn, (unsigned)((g0.M + BT - 1) / BT));
-  if (!g0.ta && !g0.tb)
+  // the hook's own feature set (Hook::kEpi) when the op matches it exactly
+  const bool exact = gemm_epi_exact_enabled() && epi_mask(gg.op[0]) == Hook::kEpi;
+  if (!g0.ta && !g0.tb && exact)
+    hipLaunchKernelGGL((gemm_f64_hook_kernel<false, false, Hook, Hook::kEpi>), grid, dim3(NTH), 0,
+                       s, gg, hook);
+  else if (!g0.ta && !g0.tb)
     hipLaunchKernelGGL((gemm_f64_hook_kernel<false, false, Hook>), grid, dim3(NTH), 0, s, gg, hook);
+  else if (g0.ta && !g0.tb && exact)
+    hipLaunchKernelGGL((gemm_f64_hook_kernel<true, false, Hook, Hook::kEpi>), grid, dim3(NTH), 0,
+                       s, gg, hook);
   else if (g0.ta && !g0.tb)
     hipLaunchKernelGGL((gemm_f64_hook_kernel<true, false, Hook>), grid, dim3(NTH), 0, s, gg, hook);
   else

@@ -934,6 +934,17 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
 #else
 #define VB_PH(k) do {} while (0)
 #endif
+#ifdef VB_BLOCK_TS
+  // barrier-exit timestamps (no waits): thread 0 of problem 0 -- a row thread and
+  // the update thread of parameter 0 -- accumulates the clock64 cycles between
+  // marks A step start, B rows done, C CHIVI max barrier left, D reduce-scatter
+  // issued, E reduction barrier left, F own update done, G end barrier left
+  unsigned long long bt[6] = {0, 0, 0, 0, 0, 0}, tb = clock64();
+  const unsigned long long tb0 = tb;
+#define VB_BT(k) do { const unsigned long long t_ = clock64(); bt[k] += t_ - tb; tb = t_; } while (0)
+#else
+#define VB_BT(k) do {} while (0)
+#endif
 
   int slot = W > 0 ? (int)(a.step0 % W) : 0;  // window ring slot of step i (i % W)
   // One step.  RO = 0: every wave runs the whole step (host noise, chunked
@@ -1112,6 +1123,7 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
       }
     }
 
+    VB_BT(0);
     double M = 0.0;
     if (a.chivi) {
       if (rows) {
@@ -1128,8 +1140,11 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
       }
     }
     VB_PH(3);
+    VB_BT(1);
     if (rows) wave_reduce_scatter<K>(acc, s_red[wid]);
+    VB_BT(2);
     __syncthreads();
+    VB_BT(3);
     // block total of column k: the row waves' rows summed in order by each reader
     // (the update threads and the value thread read their own columns, so no
     // separate column pass and barrier)
@@ -1216,9 +1231,11 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
                   s_e + ((s + 1) & 1) * (kBlockDrawLds / 2));
     }
     VB_PH(5);
+    VB_BT(4);
     slot = slot + 1 == W ? 0 : slot + 1;
     __syncthreads();
     VB_PH(6);
+    VB_BT(5);
   };
   // (the t family runs only with pre-drawn noise: one loop of row waves)
   bool split = false;
@@ -1257,6 +1274,14 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
   }
 #endif
 #undef VB_PH
+#ifdef VB_BLOCK_TS
+  if (prob == 0 && tid == 0 && a.n_steps > 0)
+    printf("BLOCKTS D=%d N=%d NT=%d RW=%d chivi=%d steps=%d cyc/step=%.0f | rows %.0f max+bar %.0f rs %.0f bar %.0f upd %.0f bar %.0f\n",
+           D, N, NT, RW, a.chivi ? 1 : 0, a.n_steps, (double)(clock64() - tb0) / a.n_steps,
+           (double)bt[0] / a.n_steps, (double)bt[1] / a.n_steps, (double)bt[2] / a.n_steps,
+           (double)bt[3] / a.n_steps, (double)bt[4] / a.n_steps, (double)bt[5] / a.n_steps);
+#endif
+#undef VB_BT
 
   if (!a.emit_grad) {
     for (int p = tid; p < P; p += NT) lam_g[p] = s_lam[p];
@@ -1850,7 +1875,7 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
                                                        double* xs) {
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
-  __shared__ double s_mu[DMAX], s_ls[DMAX], s_sg[DMAX];
+  __shared__ double s_mu[DMAX], s_ls[DMAX], s_sg[DMAX], s_isg[DMAX];
   // t family, Philox: the row's gamma variates (gamma_row), [DMAX][256]
   __shared__ double s_gam[(TFAM && !HOST) ? DMAX * 256 : 1];
   // row q of a batched launch (vb_log_weights_rows): its own lambda, output
@@ -1868,6 +1893,7 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
     s_mu[threadIdx.x] = lam[threadIdx.x];
     s_ls[threadIdx.x] = ls;
     s_sg[threadIdx.x] = exp(ls);
+    s_isg[threadIdx.x] = exp(-ls);
   }
   if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
   __syncthreads();
@@ -1875,6 +1901,7 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
   if (r >= m) return;
   double x[DMAX], g[DMAX];
   double lq = 0.0;
+  const double inv_df = 1.0 / df;
   if constexpr (TFAM && !HOST) {
     if (logw_gamma_row())
       gamma_row<DMAX>(rng, r, (D + 1) / 2, step, shape, s_gam, s_sct, s_lt);
@@ -1886,8 +1913,10 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
       if constexpr (TFAM && !HOST) {
         if (logw_gamma_row()) {   // the numerators here, the gammas from gamma_row
           normal_pair_tab(rng.draw((uint32_t)j, (uint32_t)r, step, 0u), e0, e1, s_sct, s_lt);
-          e0 = t_scale * e0 / sqrt(s_gam[(2 * j) * 256 + threadIdx.x]);
-          e1 = t_scale * e1 / sqrt(s_gam[(2 * j + 1) * 256 + threadIdx.x]);
+          // t = sqrt(df / 2) z / sqrt(G) with a refined rsqrt (as the block kernel's
+          // draw items), not sqrt + divide
+          e0 = t_scale * e0 * rsqrt_pos(s_gam[(2 * j) * 256 + threadIdx.x]);
+          e1 = t_scale * e1 * rsqrt_pos(s_gam[(2 * j + 1) * 256 + threadIdx.x]);
         } else {
           draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e0, e1, s_sct, s_lt);
         }
@@ -1905,7 +1934,14 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
       if (d < D) {
         const double mu = s_mu[d], sg = s_sg[d];
         x[d] = e[c] * sg + mu;
-        lq += logq1s<TFAM, HOST>(x[d], mu, s_ls[d], sg, df, t_const, s_lt);
+        if constexpr (TFAM && !HOST) {
+          // log q with 1 / sigma and 1 / df multiplications (the Philox t path, whose
+          // draws are already ~1 ulp from the C oracle's)
+          const double z = (x[d] - mu) * s_isg[d];
+          lq += t_const - log1p_pos_tab(z * z * inv_df, s_lt) * (0.5 * (df + 1.0)) - s_ls[d];
+        } else {
+          lq += logq1s<TFAM, HOST>(x[d], mu, s_ls[d], sg, df, t_const, s_lt);
+        }
         if (xs) xs[r * D + d] = x[d];
       }
     }

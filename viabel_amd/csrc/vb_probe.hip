@@ -3,8 +3,10 @@
 // microbenchmarks on the box").  No reference counterpart.
 //
 //   kind 0  HBM copy     16-byte loads + stores over two buffers far past the
-//                        256 MB Infinity Cache; GB/s of read + written bytes
-//   kind 1  HBM read     16-byte loads folded into one XOR per thread; GB/s read
+//                        256 MB Infinity Cache, one slab per block; GB/s of read +
+//                        written bytes
+//   kind 1  HBM read     nontemporal 16-byte loads folded into one XOR per thread;
+//                        GB/s read
 //   kind 2  fp64 MFMA    v_mfma_f64_16x16x4_f64, 4 independent accumulators per
 //                        wave, 4 waves per SIMD; TFLOP/s
 //   kind 3  fp64 VALU    v_fma_f64, 8 independent chains per lane, 4 waves per
@@ -22,28 +24,35 @@ namespace {
 using u4 = unsigned __attribute__((ext_vector_type(4)));
 using d4 = double __attribute__((ext_vector_type(4)));
 
+// copy: each block streams one contiguous slab (4 vectors in flight per thread);
+// of the forms tried (grid-stride, 8-deep, nontemporal, 4-32 blocks per CU,
+// scripts/ubench/hbm_probe.hip, profiles/r04/hbm_probe_variants.log) the slab
+// form reaches the highest copy rate, 5.37-5.41 TB/s against 4.4-4.6 grid-stride
 __global__ __launch_bounds__(256) void probe_copy_kernel(const u4* __restrict__ src,
                                                          u4* __restrict__ dst, long long n) {
-  const long long stride = (long long)gridDim.x * 256;
-  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    const u4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+  const long long per = (n + gridDim.x - 1) / gridDim.x;
+  const long long b0 = (long long)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
+  long long i = b0 + threadIdx.x;
+  for (; i + 3 * 256 < b1; i += 4 * 256) {
+    const u4 a = src[i], b = src[i + 256], c = src[i + 512], d = src[i + 768];
     dst[i] = a;
-    dst[i + stride] = b;
-    dst[i + 2 * stride] = c;
-    dst[i + 3 * stride] = d;
+    dst[i + 256] = b;
+    dst[i + 512] = c;
+    dst[i + 768] = d;
   }
-  for (; i < n; i += stride) dst[i] = src[i];
+  for (; i < b1; i += 256) dst[i] = src[i];
 }
 
+// read: nontemporal 16-byte loads, 8 in flight per thread (the fastest read form,
+// 5.5-6.0 TB/s in the same sweep)
 __global__ __launch_bounds__(256) void probe_read_kernel(const u4* __restrict__ src, long long n,
                                                          unsigned* __restrict__ out) {
   const long long stride = (long long)gridDim.x * 256;
   long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   u4 acc = {0u, 0u, 0u, 0u};
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    const u4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    acc ^= a ^ b ^ c ^ d;
+  for (; i + 7 * stride < n; i += 8 * stride) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc ^= __builtin_nontemporal_load(src + i + u * stride);
   }
   for (; i < n; i += stride) acc ^= src[i];
   out[(long long)blockIdx.x * 256 + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
@@ -106,7 +115,7 @@ int probe_rate(int kind, long long n, int reps, hipStream_t st, double* out) {
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   void *a = nullptr, *b = nullptr;
   const long long nv = kind <= 1 ? n / 16 : 0;        // 16-byte vectors
-  const unsigned blocks = kind <= 1 ? (unsigned)ncu * 8 : (unsigned)ncu * 4;
+  const unsigned blocks = kind == 0 ? (unsigned)ncu * 16 : kind == 1 ? (unsigned)ncu * 32 : (unsigned)ncu * 4;
   const size_t abytes = kind <= 1 ? (size_t)nv * 16 : 0;
   const size_t bbytes = kind == 0 ? abytes : sizeof(double) * blocks * 256;
   if (abytes && hipMalloc(&a, abytes) != hipSuccess) {
