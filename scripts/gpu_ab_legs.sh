@@ -19,8 +19,10 @@ LIBS_REV=$(echo $LIBS_FWD | awk '{for (i = NF; i > 0; i--) printf "%s ", $i}')
 for i in $(seq 1 ${ROUNDS:-3}); do
   if [ $((i % 2)) -eq 1 ]; then ORDER=$LIBS_FWD; else ORDER=$LIBS_REV; fi
   for L in $ORDER; do
-    lib=$PWD/viabel_amd/libviabel_amd_$L.so; [ "$L" = new ] && lib=$PWD/viabel_amd/libviabel_amd.so
-    VIABEL_AMD_LIB=$lib timeout -k 10 200 python bench.py --legs ${LEGS:-cfg1,cfg2,cfg5} --no-cpu-baseline \
+    # "name+VAR=value": the library plus an environment switch
+    name=${L%%+*}; envv=""; [ "$name" != "$L" ] && envv=${L#*+}
+    lib=$PWD/viabel_amd/libviabel_amd_$name.so; [ "$name" = new ] && lib=$PWD/viabel_amd/libviabel_amd.so
+    env $envv VIABEL_AMD_LIB=$lib timeout -k 10 200 python bench.py --legs ${LEGS:-cfg1,cfg2,cfg5} --no-cpu-baseline \
       --steps 20 --warmup 5 > gpurun_out/ab_legs.json 2> gpurun_out/ab_legs.err || exit $?
     python - "$L" <<'PY'
 import json, sys

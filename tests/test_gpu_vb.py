@@ -3,6 +3,8 @@ noise.  Tolerances (written per test): single estimator calls 1e-10 relative
 (SURVEY §8c asks <= 1e-12 for identical noise; reduction-order and FMA
 differences stay around 1e-14..1e-12); adagrad trajectories <= 1e-7 relative
 over >= 100 steps (the bar is 1e-5)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -410,8 +412,61 @@ def test_predraw_equals_in_kernel_draws(objective, target, D, N, nprob, monkeypa
         run.advance_philox(3, 7, 5, 0)
         run.advance_philox(697, 7, 5, 3)        # > one 512-step predraw chunk
         out[mode] = run.result()
-    for a, b in zip(out['0'], out['all']):
-        np.testing.assert_array_equal(a, b)
+    if _split_rows(D, N):
+        # the pre-drawn rows run as split rows (two lanes per sample):
+        # the same draws and arithmetic summed in another order -- equal to
+        # rounding; the bitwise identity of the unsplit layout is
+        # test_predraw_equals_in_kernel_draws_unsplit
+        for a, b in zip(out['0'], out['all']):
+            np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-12)
+    else:
+        for a, b in zip(out['0'], out['all']):
+            np.testing.assert_array_equal(a, b)
+
+
+def _split_rows(D, N):
+    """block_layout's split-row condition (copy-wave layout, VIABEL_AMD_BLOCK_SPLIT
+    not 0)."""
+    return os.environ.get('VIABEL_AMD_BLOCK_SPLIT', '1') != '0' and 2 <= D <= 10 and N <= 128
+
+
+_UNSPLIT = '''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import viabel_amd.vb as vb
+from viabel_amd import targets
+D, N, nprob = 10, int(sys.argv[3]), int(sys.argv[4])
+fam = vb.mean_field_gaussian_variational_family(D, rng='philox')
+tgt = targets.eight_schools_ncp() if sys.argv[2] == 'eight_schools_ncp' else getattr(targets, sys.argv[2])(D)
+obj = vb.black_box_chivi(2.0, fam, tgt, N) if sys.argv[5] == 'chivi' else vb.black_box_klvi(fam, tgt, N)
+rs = np.random.RandomState(40)
+init = np.stack([np.concatenate([rs.randn(D) * 0.3, rs.randn(D) * 0.2 - 0.5]) for _ in range(nprob)])
+out = {}
+import os
+for mode in ('0', 'all'):
+    os.environ['VIABEL_AMD_PREDRAW'] = mode
+    run = vb.DeviceRun(obj, 700, init, learning_rate=0.01)
+    run.advance_philox(3, 7, 5, 0)
+    run.advance_philox(697, 7, 5, 3)
+    out[mode] = run.result()
+for a, b in zip(out['0'], out['all']):
+    np.testing.assert_array_equal(a, b)
+print('bitwise-equal')
+'''
+
+
+@pytest.mark.parametrize('target,N,nprob,objective', [('funnel', 128, 1, 'chivi'),
+                                                      ('eight_schools_ncp', 100, 3, 'klvi')])
+def test_predraw_equals_in_kernel_draws_unsplit(target, N, nprob, objective):
+    """With split rows off (VIABEL_AMD_BLOCK_SPLIT=0, read once per process, so in
+    a child process) the copy-wave layout gives the in-kernel draws' bits."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, VIABEL_AMD_BLOCK_SPLIT='0')
+    r = subprocess.run([sys.executable, '-c', _UNSPLIT, root, target, str(N), str(nprob), objective],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and 'bitwise-equal' in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
 @pytest.mark.parametrize('objective', ['klvi', 'chivi'])

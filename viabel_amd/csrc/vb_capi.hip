@@ -228,7 +228,7 @@ bool predraw_enabled(int fam_kind, bool run = false, int N = 0, int D = 0, bool 
   if (fam_kind == VB_FAMILY_MF_T) return true;
   if (e && e[0] == 'a') return true;
   if (e && e[0] == 't') return false;
-  return run && block_pf_enabled() && vbk::block_pf_layout(N, D, need_lq);
+  return run && block_pf_enabled() && vbk::block_pf_layout(N, D, need_lq, block_pf_enabled());
 }
 
 // VIABEL_AMD_FR_FUSE=0: the full-rank step keeps its separate unpack / power /
@@ -242,10 +242,16 @@ bool fr_fuse_enabled() {
 // VIABEL_AMD_BLOCK_PF=0: the block kernel's device-noise rows are read straight
 // from HBM by the row threads instead of staged into LDS by a copy wave (A/B
 // switch; same bits)
+// VIABEL_AMD_BLOCK_SPLIT=0: the copy-wave layout keeps one row thread per sample
+// instead of two (each lane of a pair takes half of the sample's coordinates,
+// block_layout); the value is the BlockArgs::pf mode: 0 off, 1 copy wave, 2 copy
+// wave with split rows where the layout allows them
 int block_pf_enabled() {
   static const int on = [] {
     const char* e = std::getenv("VIABEL_AMD_BLOCK_PF");
-    return (e && e[0] == '0') ? 0 : 1;
+    if (e && e[0] == '0') return 0;
+    const char* sp = std::getenv("VIABEL_AMD_BLOCK_SPLIT");
+    return (sp && sp[0] == '0') ? 1 : 2;
   }();
   return on;
 }
@@ -1234,7 +1240,7 @@ int vb_block_floor(vb_ctx* c, int32_t D, int32_t N, int32_t chivi, int32_t host_
   VB_HIP(hipEventCreate(&e1));
   VB_HIP(hipEventRecord(e0, c->stream));
   VB_HIP(vbk::launch_block_floor(D, N, host_layout != 0, chivi != 0, (int)n_steps,
-                                 (int)n_problems, out.d(), c->stream, block_pf_enabled() != 0));
+                                 (int)n_problems, out.d(), c->stream, block_pf_enabled()));
   VB_HIP(hipEventRecord(e1, c->stream));
   VB_HIP(hipEventSynchronize(e1));
   float ms = 0.f;

@@ -484,6 +484,34 @@ struct Funnel {
     g[1] = gv;
     return lp;
   }
+  // Split rows (block_kernel, lanes 2j / 2j + 1 of a pair): this lane's log p part
+  // and the gradients of its coordinates [h DH, h DH + DH) (xh / gh); x1 = log sigma
+  // is computed by both lanes.  The pair's gv parts are summed with one DPP swap
+  // (both lanes active) and land on coordinate 1's owner.
+  template <int DMAX, int DH>
+  __device__ __forceinline__ static double row_half(const double* xh, double* gh, int h, int D,
+                                                    double /*x0*/, double x1) {
+    constexpr double s0 = 1.35;
+    const double v = x1;
+    const double zv = v / s0;
+    double lp = h == 0 ? -0.5 * zv * zv - log(s0) - 0.5 * kLog2Pi : 0.0;
+    double gv = h == 0 ? -zv / s0 : 0.0;
+    const double inv_s = exp(-v);
+    const double inv_s2 = inv_s * inv_s;
+#pragma unroll
+    for (int k = 0; k < DH; ++k) {
+      const int d = h * DH + k;
+      const bool on = d < D && d != 1;
+      const double z = xh[k] * inv_s;
+      lp += on ? -0.5 * z * z - v - 0.5 * kLog2Pi : 0.0;
+      gh[k] = on ? -xh[k] * inv_s2 : 0.0;
+      gv += on ? z * z - 1.0 : 0.0;
+    }
+    gv += dpp_f64<0xB1>(gv);   // quad_perm [1,0,3,2]: the pair's other lane
+    constexpr int h1 = DH >= 2 ? 0 : 1, k1 = DH >= 2 ? 1 : 0;
+    if (h == h1) gh[k1] = gv;
+    return lp;
+  }
 };
 
 // eight_schools_ncp.stan:1-23 log_prob (constants of the ~ statements dropped,
@@ -516,6 +544,46 @@ struct EightSchools {
     g[1] = gu;
     return lp;
   }
+  // Split rows (see Funnel::row_half): lane 0 owns mu, log tau and theta_tilde
+  // 0-2, lane 1 theta_tilde 3-7 (DH = 5); both compute tau.  The pair's mu and
+  // log tau gradient parts are summed with one DPP swap each.
+  template <int DMAX, int DH>
+  __device__ __forceinline__ static double row_half(const double* xh, double* gh, int h, int /*D*/,
+                                                    double x0, double x1) {
+    static_assert(DH >= 2, "eight schools: coordinates 0 and 1 on lane 0");
+    constexpr double y[8] = {28., 8., -3., 7., -1., 1., 18., 12.};
+    constexpr double is[8] = {1. / 15., 1. / 10., 1. / 16., 1. / 11.,
+                              1. / 9.,  1. / 11., 1. / 10., 1. / 18.};
+    const double mu = x0, u = x1, tau = exp(u);
+    const double t5 = tau * 0.2, m5 = mu * 0.2;
+    double lp = 0.0, gmu = 0.0, gu = 0.0;
+    if (h == 0) {
+      lp = -0.5 * m5 * m5 - log1p(t5 * t5) + u;
+      gmu = -m5 * 0.2;
+      gu = -2.0 * t5 * t5 / (1.0 + t5 * t5) + 1.0;
+    }
+#pragma unroll
+    for (int k = 0; k < DH; ++k) {
+      // theta_tilde j = h DH + k - 2: lane 0's k >= 2, every k of lane 1
+      const bool th_on = h == 1 || k >= 2;
+      const int j0 = k >= 2 ? k - 2 : 0, j1 = DH + k - 2 < 8 ? DH + k - 2 : 7;
+      const double yj = h ? y[j1] : y[j0], isj = h ? is[j1] : is[j0];
+      const double th = xh[k];
+      const double r = (yj - mu - tau * th) * isj;
+      const double rs = r * isj;
+      lp += th_on ? -0.5 * th * th - 0.5 * r * r : 0.0;
+      gmu += th_on ? rs : 0.0;
+      gu += th_on ? rs * (tau * th) : 0.0;
+      gh[k] = th_on ? -th + rs * tau : 0.0;
+    }
+    gmu += dpp_f64<0xB1>(gmu);
+    gu += dpp_f64<0xB1>(gu);
+    if (h == 0) {
+      gh[0] = gmu;
+      gh[1] = gu;
+    }
+    return lp;
+  }
 };
 
 // Row evaluation for separable targets.
@@ -531,6 +599,21 @@ struct SepRow {
       const bool on = d < D;
       lp += on ? l : 0.0;
       g[d] = on ? gd : 0.0;
+    }
+    return lp;
+  }
+  // Split rows: this lane's coordinates [h DH, h DH + DH) only (no cross terms)
+  template <int DMAX, int DH>
+  __device__ __forceinline__ static double row_half(const double* xh, double* gh, int h, int D,
+                                                    double /*x0*/, double /*x1*/) {
+    double lp = 0.0;
+#pragma unroll
+    for (int k = 0; k < DH; ++k) {
+      double gd;
+      const double l = T::lp1(xh[k], gd);
+      const bool on = h * DH + k < D;
+      lp += on ? l : 0.0;
+      gh[k] = on ? gd : 0.0;
     }
     return lp;
   }

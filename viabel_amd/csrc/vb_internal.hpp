@@ -75,18 +75,19 @@ struct BlockArgs {
   // column pairs, without -sum log sigma) from launch_block_predraw, or null
   const double* noise_lq;
   uint32_t k0, k1, stream, stream_stride;
-  int pf;   // device-noise rows staged into LDS by a copy wave (VIABEL_AMD_BLOCK_PF, default on)
+  int pf;   // device-noise rows staged into LDS by a copy wave (VIABEL_AMD_BLOCK_PF, default on);
+            // 2: also split rows (two lanes per sample) where block_layout allows them
 };
 
 // family kind 0 = mf gaussian, 1 = mf t; target kind per vb_target_kind.
 hipError_t launch_sep(int fam, int tgt, bool host_noise, const SepArgs& a, hipStream_t s);
 // block step skeleton without draws / target (vb_block_floor)
 hipError_t launch_block_floor(int D, int N, bool host_layout, bool chivi, int n_steps, int nprob,
-                              double* out, hipStream_t s, bool pf = false);
+                              double* out, hipStream_t s, int pf = 0);
 hipError_t launch_block(int fam, int tgt, bool host_noise, const BlockArgs& a, int n_problems,
                         hipStream_t s);
 // whether device-noise blocks of this shape get the copy wave (its LDS ring fits)
-bool block_pf_layout(int N, int D, bool need_lq);
+bool block_pf_layout(int N, int D, bool need_lq, int pf_mode);
 bool target_separable(int tgt);
 // Pre-drawn block-kernel noise: the standardized draws of n_steps steps of
 // n_problems problems, [q][s][N][D], bit-identical to the block kernel's own

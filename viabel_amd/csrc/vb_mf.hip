@@ -599,6 +599,41 @@ __device__ __forceinline__ void wave_reduce_scatter(const double (&v)[K], double
   }
 }
 
+// Split rows: the same reduce-scatter over the lanes of one parity (lane h of
+// every pair holds register j for output index map(j, h)): the in-row steps are
+// lane ^ 2, row_ror 4 and row_ror 8 (parity preserving), and lanes 0 / 1 of each
+// row write the even / odd totals.  Register j < DH is coordinate h DH + j's
+// gradient sum, DH <= j < 2 DH the (g e) sum of coordinate h DH + j - DH, j = 2 DH
+// the log p / weight sum (even lanes only; odd lanes hold zero).
+template <int KH, int DH, int DMAX>
+__device__ __forceinline__ void wave_reduce_scatter_pair(const double (&v)[KH], double* out) {
+  constexpr int H1 = (KH + 1) / 2, H2 = (H1 + 1) / 2;
+  double r1[H1], r2[H2];
+#pragma unroll
+  for (int i = 0; i < H1; ++i) r1[i] = swap32_pair(v[i], i + H1 < KH ? v[i + H1] : 0.0);
+#pragma unroll
+  for (int j = 0; j < H2; ++j) {
+    double t = swap16_pair(r1[j], j + H2 < H1 ? r1[j + H2] : 0.0);
+    t += dpp_f64<0x4E>(t);   // quad_perm [2,3,0,1]: lane ^ 2
+    t += dpp_f64<0x124>(t);  // row_ror:4
+    t += dpp_f64<0x128>(t);  // row_ror:8
+    r2[j] = t;
+  }
+  const int lane = threadIdx.x & 63, q = lane >> 4, pos = lane & 15;
+  if (pos < 2) {
+    const int h = pos;
+#pragma unroll
+    for (int j = 0; j < H2; ++j) {
+      const int i = j + (q & 1) * H2;
+      const int k = i + (q >> 1) * H1;
+      if (i < H1 && k < KH) {
+        const int idx = k < DH ? h * DH + k : k < 2 * DH ? DMAX + h * DH + (k - DH) : (h == 0 ? 2 * DMAX : -1);
+        if (idx >= 0) out[idx] = r2[j];
+      }
+    }
+  }
+}
+
 // Philox mode runs the block as row waves (reparameterise, target, accumulate:
 // one thread per sample) and draw waves (normal pair [+ gamma pair] and the
 // pair's log q partial per (sample, pair) item, into LDS).  When one step's
@@ -760,12 +795,23 @@ struct BlockLayout {
   int nt, rw, pipe, rec;  // threads, row waves, overlapped draws, doubles per sample record
   int pf;                 // device noise prefetched by a copy wave (the last wave)
   int pf_lq, pf_slot;     // doubles offset of the lq part in a slot, doubles per slot
+  int split;              // two row lanes per sample, each with half of the coordinates
 };
+
+// Split rows (copy-wave layout, 2 <= D <= 10, N <= 128): lanes 2j and 2j + 1 of a
+// row wave share sample j; lane h takes coordinates [h DH, h DH + DH), DH =
+// ceil(DMAX / 2), and the pair exchanges its cross-coordinate sums (log p, the
+// shared-coordinate gradients) with one DPP swap.  A step is a dependent chain of
+// one wave's instructions (one wave per SIMD), so halving each lane's
+// per-coordinate work and spreading the samples over up to 4 row waves (all four
+// SIMDs) shortens it; the copy wave shares a SIMD.
+constexpr int kBlockSplitMaxD = 10;
+constexpr int kBlockQpreMaxW = 16;   // windows the copy wave pre-sums (block_kernel)
 
 __host__ __device__ inline int pf_round(int n) { return (n + kPfUnit - 1) / kPfUnit * kPfUnit; }
 
 __host__ __device__ inline BlockLayout block_layout(int N, int D, bool host, bool need_lq,
-                                                   bool pf_ok = false) {
+                                                   int pf_ok = 0) {
   const int NP = (D + 1) / 2;
   const int rw = std::min(kBlockMaxRowWaves, std::max(1, (N + 63) / 64));
   BlockLayout L{};
@@ -779,6 +825,13 @@ __host__ __device__ inline BlockLayout block_layout(int N, int D, bool host, boo
     // at most 3 row waves + the copy wave: the PF instances launch with <= 256
     // threads (one wave per SIMD), so their registers may reach the whole file
     L.pf = pf_ok && rw <= 3 && 3 * L.pf_slot <= kBlockPfLds;
+    if (pf_ok == 2 && D >= 2 && D <= kBlockSplitMaxD && 2 * N <= 64 * kBlockMaxRowWaves &&
+        3 * L.pf_slot <= kBlockPfLds) {
+      L.split = 1;
+      L.pf = 1;
+      L.rw = (2 * N + 63) / 64;
+      L.nt = 64 * L.rw;
+    }
     if (L.pf) L.nt += 64;
     return L;
   }
@@ -794,12 +847,15 @@ __host__ __device__ inline BlockLayout block_layout(int N, int D, bool host, boo
   return L;
 }
 
-template <class TGT, bool TFAM, bool HOST, int DMAX, bool PF = false>
+template <class TGT, bool TFAM, bool HOST, int DMAX, bool PF = false, bool SPLIT = false>
 // device-noise (HOST) instances launch <= 256 threads (<= 4 row waves, or <= 3 and the
 // copy wave): one wave per SIMD, so their registers may use the whole file instead of
-// spilling at the 256-VGPR cap a 512-thread bound implies (the DMAX = 16 instances)
-__global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(BlockArgs a) {
+// spilling at the 256-VGPR cap a 512-thread bound implies (the DMAX = 16 instances).
+// Split-row instances (DMAX <= 10) launch up to 4 row waves + the copy wave.
+__global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void block_kernel(BlockArgs a) {
+  static_assert(!SPLIT || (HOST && PF && DMAX <= kBlockSplitMaxD), "split rows: copy-wave layout");
   constexpr int K = 2 * DMAX + 2;   // G[DMAX], H[DMAX], V/S, spare
+  constexpr int DH = (DMAX + 1) / 2, KH = 2 * DH + 1;   // split rows: per-lane half
   constexpr int WMAX = 64;
   __shared__ double s_lam[2 * DMAX];
   __shared__ double s_sg[DMAX];     // exp(log sigma) of the current lam
@@ -810,6 +866,7 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
   __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
   __shared__ double s_e[HOST ? 1 : kBlockDrawLds + DMAX];  // + slack for the row loads
   __shared__ __attribute__((aligned(16))) double s_pf[HOST && PF ? kBlockPfLds + kBlockDMax : 1];
+  __shared__ double s_qold[HOST && PF ? 2 * DMAX : 1];   // window sums without the newest slot
   if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
 
   using Row = RowOf<TGT>;
@@ -818,7 +875,7 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
   const int prob = blockIdx.x;
   const int D = a.D, N = a.N, W = a.W, P = a.P;
   const bool need_lq = a.chivi || a.pd;
-  const BlockLayout L = block_layout(N, D, HOST, need_lq, HOST && PF);
+  const BlockLayout L = block_layout(N, D, HOST, need_lq, (HOST && PF) ? a.pf : 0);
   const int RW = L.rw, RT = 64 * RW, R = L.rec;
   const bool row_wave = wid < RW;
   // PF instances are launched exactly when the layout has the copy wave (block_dispatch_dm)
@@ -856,6 +913,10 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
     }
   };
   const double dN = (double)N;
+  // adagrad window sums: the copy wave adds up the older W - 1 slots of every
+  // parameter while the rows run (same order, oldest first), so the update adds
+  // only the newest square (the same bits as the whole loop)
+  const bool qpre = kPF && a.opt == 0 && !a.emit_grad && W >= 1 && W <= kBlockQpreMaxW;
   double* lam_g = a.lam + (long long)prob * P;
   double* ring_g = a.ring ? a.ring + (long long)prob * W * P : nullptr;
 
@@ -962,9 +1023,12 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
       const double l = s_lam[D + d];
       sl += d < D ? l : 0.0;
     }
-    double acc[K];
+    double acc[K];   // (unused by split rows: the compiler drops it)
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    double acch[KH];   // split rows: this lane's half (wave_reduce_scatter_pair; else unused)
+#pragma unroll
+    for (int k = 0; k < KH; ++k) acch[k] = 0.0;
     double mloc = -INFINITY;  // CHIVI: running max of this thread's log weights
     // overlapped draws: items [0, cut_a) of step s + 1 are drawn while the rows
     // consume step s, the rest during the update (see below)
@@ -1029,7 +1093,91 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
       }
     };
 
-    if constexpr (kPF) {
+    // split rows: lane h of the pair (eh = its half of the noise, e = the whole
+    // row for the shared coordinates 0 and 1); log p summed over the pair
+    auto row_half_of = [&](const double* eh, const double* e, double lqs, int h) {
+      double xh[DH], gh[DH];
+#pragma unroll
+      for (int k = 0; k < DH; ++k) {
+        const int d = h * DH + k;
+        const double m = s_lam[d], sgd = s_sg[d];
+        xh[k] = d < D ? eh[k] * sgd + m : 0.0;
+        gh[k] = 0.0;
+      }
+      const double x0 = e[0] * s_sg[0] + s_lam[0], x1 = e[1] * s_sg[1] + s_lam[1];
+      double lp = Row::template row_half<DMAX, DH>(xh, gh, h, D, x0, x1);
+      lp += dpp_f64<0xB1>(lp);   // the pair's total (the same sum in both lanes)
+      const double lq = lqs - sl;
+      if (a.pd) lp -= lq;
+      const double own = h == 0 ? 1.0 : 0.0;   // the log p / weight slot: lane 0 only
+      if (!a.chivi) {
+#pragma unroll
+        for (int k = 0; k < DH; ++k) {
+          acch[k] += gh[k];
+          acch[DH + k] += gh[k] * eh[k];
+        }
+        acch[2 * DH] += own * lp;
+      } else {
+        const double lw = lp - lq;
+        if (mloc == -INFINITY && lw > -INFINITY && lw < INFINITY) {
+          mloc = lw;
+#pragma unroll
+          for (int k = 0; k < DH; ++k) {
+            acch[k] += gh[k];
+            acch[DH + k] += gh[k] * eh[k];
+          }
+          acch[2 * DH] += own;
+          return;
+        }
+        if (lw > mloc) {
+          const double f = (mloc == -INFINITY) ? 0.0 : exp(a.alpha * (mloc - lw));
+#pragma unroll
+          for (int k = 0; k < KH; ++k) acch[k] *= f;
+          mloc = lw;
+        }
+        const double wgt = exp(a.alpha * (lw - mloc));
+#pragma unroll
+        for (int k = 0; k < DH; ++k) {
+          acch[k] += wgt * gh[k];
+          acch[DH + k] += wgt * (gh[k] * eh[k]);
+        }
+        acch[2 * DH] += own * wgt;
+      }
+    };
+
+    if constexpr (SPLIT) {
+      if (rows) {
+        typedef __attribute__((address_space(3))) double lds_f64;
+        const double* buf = s_pf + (s % 3) * L.pf_slot;
+        const unsigned base = (unsigned)(uintptr_t)((const lds_f64*)buf);
+        const int h = tid & 1;
+        // pairs are active together (n is the same for both lanes): the DPP swaps
+        // inside row_half_of see their partner
+        for (int n = tid >> 1; n < N; n += RT >> 1) {
+          double e[DMAX];
+          double tl = 0.0;
+          LdsRowWait<DMAX>::run(base + 8u * (unsigned)(n * D), base + 8u * (unsigned)(L.pf_lq + n),
+                                need_lq && pre_lq, e, tl);
+          double eh[DH];
+          double lqs = 0.0;
+#pragma unroll
+          for (int k = 0; k < DH; ++k) {
+            const double hi = DH + k < DMAX ? e[DH + k] : 0.0;
+            const double v = h ? hi : e[k];
+            eh[k] = h * DH + k < D ? v : 0.0;
+            if (need_lq && !pre_lq && h * DH + k < D) {
+              if constexpr (TFAM)
+                lqs += a.t_const - log1p(eh[k] * eh[k] / a.df) * lq_half;
+              else
+                lqs += -0.5 * eh[k] * eh[k] - 0.5 * kLog2Pi;
+            }
+          }
+          if (need_lq && !pre_lq) lqs += dpp_f64<0xB1>(lqs);
+          if (need_lq && pre_lq) lqs = tl;
+          row_half_of(eh, e, lqs, h);
+        }
+      }
+    } else if constexpr (kPF) {
       if (rows) {
         typedef __attribute__((address_space(3))) double lds_f64;
         const double* buf = s_pf + (s % 3) * L.pf_slot;
@@ -1131,27 +1279,49 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
         if (lane == 0) s_max[wid] = wm;
       }
       __syncthreads();
-      M = s_max[0];
-      for (int q = 1; q < RW; ++q) M = fmax(M, s_max[q]);
+      {
+        double mq[kBlockMaxRowWaves];
+#pragma unroll
+        for (int q = 0; q < kBlockMaxRowWaves; ++q) mq[q] = s_max[q];
+        M = mq[0];
+#pragma unroll
+        for (int q = 1; q < kBlockMaxRowWaves; ++q) M = q < RW ? fmax(M, mq[q]) : M;
+      }
       if (rows) {
         const double f = (mloc == -INFINITY) ? 0.0 : exp(a.alpha * (mloc - M));
+        if constexpr (SPLIT) {
 #pragma unroll
-        for (int k = 0; k <= 2 * DMAX; ++k) acc[k] *= f;
+          for (int k = 0; k < KH; ++k) acch[k] *= f;
+        } else {
+#pragma unroll
+          for (int k = 0; k <= 2 * DMAX; ++k) acc[k] *= f;
+        }
       }
     }
     VB_PH(3);
     VB_BT(1);
-    if (rows) wave_reduce_scatter<K>(acc, s_red[wid]);
+    if constexpr (SPLIT) {
+      if (rows) wave_reduce_scatter_pair<KH, DH, DMAX>(acch, s_red[wid]);
+    } else {
+      if (rows) wave_reduce_scatter<K>(acc, s_red[wid]);
+    }
     VB_BT(2);
     __syncthreads();
     VB_BT(3);
     // block total of column k: the row waves' rows summed in order by each reader
     // (the update threads and the value thread read their own columns, so no
     // separate column pass and barrier)
+    // (every row's value is read at once, then summed in row order: a loop over
+    // RW issued one dependent LDS read per row, ~0.25 us of the update's chain at
+    // RW = 4)
     auto colsum = [&](int k) {
-      double t = s_red[0][k];
-      for (int q = 1; q < RW; ++q) t += s_red[q][k];
-      return t;
+      double t[kBlockMaxRowWaves];
+#pragma unroll
+      for (int q = 0; q < kBlockMaxRowWaves; ++q) t[q] = s_red[q][k];
+      double u = t[0];
+#pragma unroll
+      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = q < RW ? u + t[q] : u;
+      return u;
     };
     VB_PH(4);
 
@@ -1195,14 +1365,18 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
           }
         } else {
           s_ring[slot * P + p] = gp;
-          const int cnt = (i + 1 < W) ? (int)(i + 1) : W;
-          const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;  // (i + 1) % W
           double q = 0.0;
-          for (int k = 0; k < cnt; ++k) {
-            int Lk = oldest + k;
-            if (Lk >= W) Lk -= W;
-            const double t = s_ring[Lk * P + p];
-            q = __dadd_rn(q, __dmul_rn(t, t));
+          if (qpre) {
+            q = __dadd_rn(s_qold[p], __dmul_rn(gp, gp));
+          } else {
+            const int cnt = (i + 1 < W) ? (int)(i + 1) : W;
+            const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;  // (i + 1) % W
+            for (int k = 0; k < cnt; ++k) {
+              int Lk = oldest + k;
+              if (Lk >= W) Lk -= W;
+              const double t = s_ring[Lk * P + p];
+              q = __dadd_rn(q, __dmul_rn(t, t));
+            }
           }
           nl = __dsub_rn(s_lam[p], __dmul_rn(a.lr.at(i), gp) / sqrt(__dadd_rn(a.eps, q)));
           if (i >= a.hist_start) a.hist[((long long)prob * a.n_hist + (i - a.hist_start)) * P + p] = nl;
@@ -1249,10 +1423,30 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
     // and hold every wave at the step's first barrier.  The count matches the
     // row waves' step: the CHIVI max barrier, the reduction barrier and the
     // end-of-step barrier.
+    // It also writes the window sums of step s (s_qold) before the step's first
+    // barrier: the slots it reads were written by earlier steps' updates (before
+    // their end barriers), and the update of step s reads s_qold after the
+    // reduction barrier.
     const int nbar = a.chivi ? 3 : 2;
+    int cslot = slot;
     for (int s = 0; s < a.n_steps; ++s) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (s + 2 < a.n_steps) pf_issue(s + 2);
+      if (qpre && lane < P) {
+        const long long i = a.step0 + s;
+        const int cnt = (i + 1 < W) ? (int)(i + 1) : W;
+        const int oldest = (cnt < W || cslot + 1 == W) ? 0 : cslot + 1;
+        double q = 0.0;
+        for (int k = 0; k + 1 < cnt; ++k) {
+          int Lk = oldest + k;
+          if (Lk >= W) Lk -= W;
+          const double t = s_ring[Lk * P + lane];
+          q = __dadd_rn(q, __dmul_rn(t, t));
+        }
+        s_qold[lane] = q;
+      }
+      cslot = cslot + 1 == W ? 0 : cslot + 1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       for (int b = 0; b < nbar; ++b) __builtin_amdgcn_s_barrier();
     }
   } else if (split) {
@@ -1297,7 +1491,7 @@ __global__ __launch_bounds__(HOST ? 256 : kBlockMaxThreads) void block_kernel(Bl
 template <int DMAX>
 __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, int N, int NT_rows,
                                                                      int chivi, int n_steps,
-                                                                     int W, double* out) {
+                                                                     int W, double* out, int n_act) {
   constexpr int K = 2 * DMAX + 2;
   __shared__ double s_lam[2 * DMAX];
   __shared__ double s_sg[DMAX];
@@ -1324,22 +1518,32 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
     double acc[K];
     const double t = (double)(tid + 1) * 1e-3 * s_lam[0];
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = (tid < N) ? t + (double)k : 0.0;
+    for (int k = 0; k < K; ++k) acc[k] = (tid < n_act) ? t + (double)k : 0.0;
     double M = 0.0;
     if (chivi) {
       if (row_wave) {
-        const double wm = wave_max_dpp(tid < N ? t + sl : -INFINITY);
+        const double wm = wave_max_dpp(tid < n_act ? t + sl : -INFINITY);
         if (lane == 0) s_max[wid] = wm;
       }
       __syncthreads();
-      M = s_max[0];
-      for (int q = 1; q < RW; ++q) M = fmax(M, s_max[q]);
+      {
+        double mq[kBlockMaxRowWaves];
+#pragma unroll
+        for (int q = 0; q < kBlockMaxRowWaves; ++q) mq[q] = s_max[q];
+        M = mq[0];
+#pragma unroll
+        for (int q = 1; q < kBlockMaxRowWaves; ++q) M = q < RW ? fmax(M, mq[q]) : M;
+      }
     }
     if (row_wave) wave_reduce_scatter<K>(acc, s_red[wid]);
     __syncthreads();
     auto colsum = [&](int k) {   // as block_kernel: each reader sums its column
-      double u = s_red[0][k];
-      for (int q = 1; q < RW; ++q) u += s_red[q][k];
+      double t[kBlockMaxRowWaves];
+#pragma unroll
+      for (int q = 0; q < kBlockMaxRowWaves; ++q) t[q] = s_red[q][k];
+      double u = t[0];
+#pragma unroll
+      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = q < RW ? u + t[q] : u;
       return u;
     };
     if (tid < P) {
@@ -1368,21 +1572,23 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
 }
 
 hipError_t launch_block_floor(int D, int N, bool host_layout, bool chivi, int n_steps, int nprob,
-                              double* out, hipStream_t s, bool pf) {
+                              double* out, hipStream_t s, int pf) {
   if (D < 1 || D > kBlockDMax || N < 1 || n_steps < 0 || nprob < 1) return hipErrorInvalidValue;
   // the same block shape as block_kernel's (with the device-noise copy wave, which
   // only joins the barriers here)
   const BlockLayout L = block_layout(N, D, host_layout, chivi, pf);
   const dim3 grid(nprob), block(L.nt);
-  const int rows = 64 * L.rw, W = 10;
+  // (split rows: 2N active row lanes, each reducing the full K accumulators -- an
+  // upper bound on the split kernel's KH-wide pair reduction)
+  const int rows = 64 * L.rw, W = 10, n_act = L.split ? 2 * N : N;
   if (D <= 2)
-    hipLaunchKernelGGL((block_floor_kernel<2>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out);
+    hipLaunchKernelGGL((block_floor_kernel<2>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act);
   else if (D <= 4)
-    hipLaunchKernelGGL((block_floor_kernel<4>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out);
+    hipLaunchKernelGGL((block_floor_kernel<4>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act);
   else if (D <= 10)
-    hipLaunchKernelGGL((block_floor_kernel<10>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out);
+    hipLaunchKernelGGL((block_floor_kernel<10>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act);
   else
-    hipLaunchKernelGGL((block_floor_kernel<kBlockDMax>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out);
+    hipLaunchKernelGGL((block_floor_kernel<kBlockDMax>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act);
   return hipGetLastError();
 }
 
@@ -2033,22 +2239,32 @@ hipError_t launch_sep(int fam, int tgt, bool host, const SepArgs& a, hipStream_t
   }
 }
 
-bool block_pf_layout(int N, int D, bool need_lq) {
-  return N >= 1 && D >= 1 && D <= kBlockDMax && block_layout(N, D, true, need_lq, true).pf;
+bool block_pf_layout(int N, int D, bool need_lq, int pf_mode) {
+  return N >= 1 && D >= 1 && D <= kBlockDMax && block_layout(N, D, true, need_lq, pf_mode).pf;
 }
 
 // Threads per problem: the draws of one step spread over ceil(N/64) waves (<= 4).
 // Threads per problem: host noise -> one thread per sample (<= 4 waves); Philox ->
 // enough waves for the (sample, pair) draw items of a step (<= 8 waves).
 inline unsigned block_threads(const BlockArgs& a, bool host) {
-  return (unsigned)block_layout(a.N, a.D, host, a.chivi || a.pd, a.pf != 0).nt;
+  return (unsigned)block_layout(a.N, a.D, host, a.chivi || a.pd, host ? a.pf : 0).nt;
 }
 
 template <class TGT, int DM>
 static hipError_t block_dispatch_dm(int fam, bool host, const BlockArgs& a, int nprob,
                                     hipStream_t s) {
   const dim3 grid(nprob), block(block_threads(a, host));
-  const bool pf = host && block_layout(a.N, a.D, true, a.chivi || a.pd, a.pf != 0).pf;
+  const BlockLayout L = block_layout(a.N, a.D, true, a.chivi || a.pd, a.pf);
+  const bool pf = host && L.pf;
+  if constexpr (DM <= kBlockSplitMaxD) {
+    if (host && L.split) {
+      if (fam == 1)
+        hipLaunchKernelGGL((block_kernel<TGT, true, true, DM, true, true>), grid, block, 0, s, a);
+      else
+        hipLaunchKernelGGL((block_kernel<TGT, false, true, DM, true, true>), grid, block, 0, s, a);
+      return hipGetLastError();
+    }
+  }
   if (host && fam == 1) {
     if (pf)
       hipLaunchKernelGGL((block_kernel<TGT, true, true, DM, true>), grid, block, 0, s, a);
