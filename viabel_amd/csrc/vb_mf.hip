@@ -867,6 +867,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
   __shared__ double s_e[HOST ? 1 : kBlockDrawLds + DMAX];  // + slack for the row loads
   __shared__ __attribute__((aligned(16))) double s_pf[HOST && PF ? kBlockPfLds + kBlockDMax : 1];
   __shared__ double s_qold[HOST && PF ? 2 * DMAX : 1];   // window sums without the newest slot
+  __shared__ double s_sl;   // copy-wave layout: sum_d log sigma_d of the step's lam
   if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
 
   using Row = RowOf<TGT>;
@@ -1017,11 +1018,17 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
     const bool rows = RO == 1 || (RO == 0 && row_wave);
     const long long i = a.step0 + s;
     const long long ri = a.rng_step0 + s;
-    double sl = 0.0;  // sum_d log sigma_d of the pre-update lam
+    // sum_d log sigma_d of the pre-update lam: only the value needs it (log q
+    // enters the rows without it: a per-step constant that cancels in the CHIVI
+    // weights, added back to the value).  The copy wave computes it off the rows'
+    // chain (s_sl); other layouts here, in the same order.
+    double sl = 0.0;
+    if constexpr (!kPF) {
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d) {
-      const double l = s_lam[D + d];
-      sl += d < D ? l : 0.0;
+      for (int d = 0; d < DMAX; ++d) {
+        const double l = s_lam[D + d];
+        sl += d < D ? l : 0.0;
+      }
     }
     double acc[K];   // (unused by split rows: the compiler drops it)
 #pragma unroll
@@ -1051,8 +1058,9 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
         g[d] = 0.0;
       }
       double lp = Row::template row<DMAX>(x, g, D);
-      // log q(x; lam) with all constants (mvn.logpdf / t.logpdf), z = eps
-      const double lq = lqs - sl;
+      // log q(x; lam) + sum_d log sigma_d (mvn.logpdf / t.logpdf with all
+      // constants, z = eps): the sigma term is added back in the value
+      const double lq = lqs;
       if (a.pd) lp -= lq;
       if (!a.chivi) {
 #pragma unroll
@@ -1107,7 +1115,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
       const double x0 = e[0] * s_sg[0] + s_lam[0], x1 = e[1] * s_sg[1] + s_lam[1];
       double lp = Row::template row_half<DMAX, DH>(xh, gh, h, D, x0, x1);
       lp += dpp_f64<0xB1>(lp);   // the pair's total (the same sum in both lanes)
-      const double lq = lqs - sl;
+      const double lq = lqs;   // (+ sum_d log sigma_d, as row_of)
       if (a.pd) lp -= lq;
       const double own = h == 0 ? 1.0 : 0.0;   // the log p / weight slot: lane 0 only
       if (!a.chivi) {
@@ -1328,14 +1336,18 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
     // gradient + update: thread p owns parameter p (wave 0, a row wave)
     if (RO != 2 && tid < P) {
       const int p = tid;
+      // one column read and one division for both parameter kinds (the two
+      // sides of a select, not of a branch: wave 0 holds both kinds)
+      const bool mean = p < D;
+      const double c = colsum(mean ? p : DMAX + (p - D));
+      const double sgp = s_sg[mean ? 0 : p - D];
       double gp;
       if (!a.chivi) {
-        gp = p < D ? -(colsum(p) / dN)
-                   : -(1.0 + s_sg[p - D] * (colsum(DMAX + (p - D)) / dN));
+        const double cd = c / dN;
+        gp = mean ? -cd : -(1.0 + sgp * cd);
       } else {
         const double Ssum = colsum(2 * DMAX);
-        gp = p < D ? a.alpha * colsum(p) / dN
-                   : a.alpha * (s_sg[p - D] * colsum(DMAX + (p - D)) + Ssum) / dN;
+        gp = (mean ? a.alpha * c : a.alpha * (sgp * c + Ssum)) / dN;
       }
       if (a.emit_grad) {
         a.grad[(long long)prob * P + p] = gp;
@@ -1387,12 +1399,14 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
     }
     if (RO != 1 && tid == val_tid) {
       double val;
+      if constexpr (kPF) sl = s_sl;
       if (!a.chivi) {
-        // entropy uses the pre-update lam: sum_d log sigma_d
+        // entropy uses the pre-update lam: sum_d log sigma_d (the sampled log q of
+        // klvi_pd lacks it: -(mean (log p - log q)) = -(st / N + sl))
         const double st = colsum(2 * DMAX);
-        val = a.pd ? -(st / dN) : -(c0 + sl + st / dN);
+        val = a.pd ? -(st / dN + sl) : -(c0 + sl + st / dN);
       } else {
-        val = log(colsum(2 * DMAX) / dN) / a.alpha + M;
+        val = log(colsum(2 * DMAX) / dN) / a.alpha + (M + sl);
       }
       a.values[(long long)prob * a.n_iters + (a.emit_grad ? 0 : i)] = val;
     }
@@ -1446,6 +1460,15 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
         s_qold[lane] = q;
       }
       cslot = cslot + 1 == W ? 0 : cslot + 1;
+      if (lane == 0) {   // sum_d log sigma_d for the value (same order as the rows' loop)
+        double sl = 0.0;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          const double l = s_lam[D + d];
+          sl += d < D ? l : 0.0;
+        }
+        s_sl = sl;
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       for (int b = 0; b < nbar; ++b) __builtin_amdgcn_s_barrier();
     }
@@ -1491,16 +1514,22 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
 template <int DMAX>
 __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, int N, int NT_rows,
                                                                      int chivi, int n_steps,
-                                                                     int W, double* out, int n_act) {
+                                                                     int W, double* out, int n_act,
+                                                                     int has_copy) {
   constexpr int K = 2 * DMAX + 2;
   __shared__ double s_lam[2 * DMAX];
   __shared__ double s_sg[DMAX];
   __shared__ double s_ring[64 * 2 * DMAX];
   __shared__ double s_red[kBlockMaxRowWaves][K];
   __shared__ double s_max[kBlockMaxRowWaves];
+  __shared__ double s_qold[2 * DMAX];
+  __shared__ double s_sl;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int NT = blockDim.x, P = 2 * D, RW = NT_rows / 64;
   const bool row_wave = wid < RW;
+  // the copy-wave layout: that wave pre-sums the window and sum_d log sigma_d, as
+  // block_kernel's copy wave does
+  const bool copy = has_copy && wid == RW, qpre = has_copy && W <= kBlockQpreMaxW;
   const double dN = (double)N;
   for (int p = tid; p < P; p += NT) s_lam[p] = 0.01 * p;
   for (int q = tid; q < W * P; q += NT) s_ring[q] = 0.0;
@@ -1510,8 +1539,25 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
   double val = 0.0;
   for (int s = 0; s < n_steps; ++s) {
     double sl = 0.0;
+    if (copy || !has_copy) {
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d) sl += d < D ? s_lam[D + d] : 0.0;
+      for (int d = 0; d < DMAX; ++d) sl += d < D ? s_lam[D + d] : 0.0;
+    }
+    if (copy) {
+      if (lane == 0) s_sl = sl;
+      if (qpre && lane < P) {
+        const int cnt = (s + 1 < W) ? s + 1 : W;
+        const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;
+        double q = 0.0;
+        for (int k = 0; k + 1 < cnt; ++k) {
+          int Lk = oldest + k;
+          if (Lk >= W) Lk -= W;
+          const double v = s_ring[Lk * P + lane];
+          q = __dadd_rn(q, __dmul_rn(v, v));
+        }
+        s_qold[lane] = q;
+      }
+    }
     // accumulators: a cheap function of the last update (one LDS read and K adds; a
     // per-k read of s_lam[k % P] spent an integer division per accumulator and made
     // the floor grow with K by ~0.06 us per accumulator)
@@ -1522,49 +1568,55 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
     double M = 0.0;
     if (chivi) {
       if (row_wave) {
-        const double wm = wave_max_dpp(tid < n_act ? t + sl : -INFINITY);
+        const double wm = wave_max_dpp(tid < n_act ? t : -INFINITY);
         if (lane == 0) s_max[wid] = wm;
       }
       __syncthreads();
-      {
-        double mq[kBlockMaxRowWaves];
+      double mq[kBlockMaxRowWaves];
 #pragma unroll
-        for (int q = 0; q < kBlockMaxRowWaves; ++q) mq[q] = s_max[q];
-        M = mq[0];
+      for (int q = 0; q < kBlockMaxRowWaves; ++q) mq[q] = s_max[q];
+      M = mq[0];
 #pragma unroll
-        for (int q = 1; q < kBlockMaxRowWaves; ++q) M = q < RW ? fmax(M, mq[q]) : M;
-      }
+      for (int q = 1; q < kBlockMaxRowWaves; ++q) M = q < RW ? fmax(M, mq[q]) : M;
     }
     if (row_wave) wave_reduce_scatter<K>(acc, s_red[wid]);
     __syncthreads();
     auto colsum = [&](int k) {   // as block_kernel: each reader sums its column
-      double t[kBlockMaxRowWaves];
+      double tq[kBlockMaxRowWaves];
 #pragma unroll
-      for (int q = 0; q < kBlockMaxRowWaves; ++q) t[q] = s_red[q][k];
-      double u = t[0];
+      for (int q = 0; q < kBlockMaxRowWaves; ++q) tq[q] = s_red[q][k];
+      double u = tq[0];
 #pragma unroll
-      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = q < RW ? u + t[q] : u;
+      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = q < RW ? u + tq[q] : u;
       return u;
     };
     if (tid < P) {
       const int p = tid;
-      const double gp = p < D ? -(colsum(p) / dN)
-                              : -(1.0 + s_sg[p - D] * (colsum(DMAX + (p - D)) / dN));
+      const bool mean = p < D;
+      const double cd = colsum(mean ? p : DMAX + (p - D)) / dN;
+      const double gp = mean ? -cd : -(1.0 + s_sg[mean ? 0 : p - D] * cd);
       s_ring[slot * P + p] = gp;
-      const int cnt = (s + 1 < W) ? s + 1 : W;
-      const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;
       double q = 0.0;
-      for (int k = 0; k < cnt; ++k) {
-        int Lk = oldest + k;
-        if (Lk >= W) Lk -= W;
-        const double v = s_ring[Lk * P + p];
-        q = __dadd_rn(q, __dmul_rn(v, v));
+      if (qpre) {
+        q = __dadd_rn(s_qold[p], __dmul_rn(gp, gp));
+      } else {
+        const int cnt = (s + 1 < W) ? s + 1 : W;
+        const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;
+        for (int k = 0; k < cnt; ++k) {
+          int Lk = oldest + k;
+          if (Lk >= W) Lk -= W;
+          const double v = s_ring[Lk * P + p];
+          q = __dadd_rn(q, __dmul_rn(v, v));
+        }
       }
       const double nl = __dsub_rn(s_lam[p], __dmul_rn(1e-6, gp) / sqrt(__dadd_rn(0.1, q)));
       s_lam[p] = nl;
       if (p >= D) s_sg[p - D] = exp(nl);
     }
-    if (tid == (NT > 64 ? NT - 64 : 0)) val += chivi ? log(colsum(2 * DMAX) / dN) + M : colsum(2 * DMAX);
+    if (tid == (NT > 64 ? NT - 64 : 0)) {
+      if (has_copy) sl = s_sl;
+      val += chivi ? log(colsum(2 * DMAX) / dN) + M + sl : colsum(2 * DMAX) + sl;
+    }
     slot = slot + 1 == W ? 0 : slot + 1;
     __syncthreads();
   }
@@ -1582,13 +1634,13 @@ hipError_t launch_block_floor(int D, int N, bool host_layout, bool chivi, int n_
   // upper bound on the split kernel's KH-wide pair reduction)
   const int rows = 64 * L.rw, W = 10, n_act = L.split ? 2 * N : N;
   if (D <= 2)
-    hipLaunchKernelGGL((block_floor_kernel<2>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act);
+    hipLaunchKernelGGL((block_floor_kernel<2>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act, L.pf);
   else if (D <= 4)
-    hipLaunchKernelGGL((block_floor_kernel<4>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act);
+    hipLaunchKernelGGL((block_floor_kernel<4>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act, L.pf);
   else if (D <= 10)
-    hipLaunchKernelGGL((block_floor_kernel<10>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act);
+    hipLaunchKernelGGL((block_floor_kernel<10>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act, L.pf);
   else
-    hipLaunchKernelGGL((block_floor_kernel<kBlockDMax>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act);
+    hipLaunchKernelGGL((block_floor_kernel<kBlockDMax>), grid, block, 0, s, D, N, rows, chivi ? 1 : 0, n_steps, W, out, n_act, L.pf);
   return hipGetLastError();
 }
 
