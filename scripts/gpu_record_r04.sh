@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-4 GPU record on the current tree: the full -m gpu suite, the driver's
+# bench command, and a rocprofv3 kernel trace + stats of that same command.
+# Each GPU step has its own time limit; the first failure ends the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
+  > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_gpu.log
+[ $rc -ge 2 ] && exit $rc
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
+tail -1 gpurun_out/smoke.log
+timeout -k 10 500 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || exit $?
+tail -c 300 gpurun_out/bench.log
+rm -rf gpurun_out/prof4
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o run --output-format csv -- \
+  python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/prof4.log 2>&1 || exit $?
+find gpurun_out/prof4 -name "*kernel_stats.csv"
