@@ -455,6 +455,45 @@ print('bitwise-equal')
 '''
 
 
+_OVERLAP = '''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import viabel_amd.vb as vb
+from viabel_amd import targets
+D, R, iters = 10, 10, 1300
+fam = vb.mean_field_t_variational_family(D, 40.0, rng='philox')
+obj = vb.black_box_klvi(fam, targets.eight_schools_ncp(), 100)
+rs = np.random.RandomState(3)
+init = rs.randn(R, 2 * D) * 0.5
+run = vb.DeviceRun(obj, iters, init, window=10, learning_rate=.01, learning_rate_end=.001)
+run.advance_philox(700, 0, 1, 0, stream_stride=1)
+run.advance_philox(600, 0, 1, 700, stream_stride=1)
+lam, hist, vals, smooth = run.result()
+np.savez(sys.argv[2], lam=lam, hist=hist, vals=vals)
+'''
+
+
+def test_predraw_overlap_is_bitwise_serial(tmp_path):
+    """The overlapped pre-draw (chunk k + 1 drawn on the odd CUs beside chunk k's
+    block kernel, two buffers, DESIGN §4) against the serial order
+    (VIABEL_AMD_PREDRAW_OVERLAP=0, read once per process: child processes): the same
+    trajectories, values and histories bit for bit, over 1 300 steps = 3 chunks of
+    10 problems (the overlap needs >= 8)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for mode in ('0', '1'):
+        f = str(tmp_path / ('ov%s.npz' % mode))
+        env = dict(os.environ, VIABEL_AMD_PREDRAW_OVERLAP=mode)
+        r = subprocess.run([sys.executable, '-c', _OVERLAP, root, f], env=env, capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        out[mode] = np.load(f)
+    for k in ('lam', 'hist', 'vals'):
+        np.testing.assert_array_equal(out['0'][k], out['1'][k])
+
+
 @pytest.mark.parametrize('target,N,nprob,objective', [('funnel', 128, 1, 'chivi'),
                                                       ('eight_schools_ncp', 100, 3, 'klvi')])
 def test_predraw_equals_in_kernel_draws_unsplit(target, N, nprob, objective):

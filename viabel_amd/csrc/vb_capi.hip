@@ -118,7 +118,18 @@ struct vb_ctx {
   bool own_stream = false;
   DevBuf slot[16];
   vbk::FrWork* fr = nullptr;  // full-rank workspace, created on first use
-  ~vb_ctx() { vbk::fr_work_destroy(fr); }
+  // pre-draw overlap (predraw_overlap_streams): two streams on disjoint CU halves
+  // and the events that chain them; created on first use, -1 not tried, 0 failed
+  int pd_ready = -1;
+  hipStream_t pd_stream = nullptr, blk_stream = nullptr;
+  hipEvent_t pd_ev[6] = {};
+  ~vb_ctx() {
+    vbk::fr_work_destroy(fr);
+    for (hipEvent_t& e : pd_ev)
+      if (e) (void)hipEventDestroy(e);
+    if (pd_stream) (void)hipStreamDestroy(pd_stream);
+    if (blk_stream) (void)hipStreamDestroy(blk_stream);
+  }
 };
 
 namespace {
@@ -190,6 +201,7 @@ int sync(vb_ctx* c) {
 // kPredrawBytes of draws and kPredrawMaxSteps steps.
 constexpr size_t kPredrawBytes = size_t(256) << 20;
 constexpr long long kPredrawMaxSteps = 512;
+constexpr long long kPredrawOverlapMinProblems = 8;   // overlapped pre-draw (below)
 int block_pf_enabled();
 
 // VIABEL_AMD_HOST_TRACE=1: per-call host timestamps of a launch path to stderr
@@ -256,6 +268,17 @@ int block_pf_enabled() {
   return on;
 }
 
+// VIABEL_AMD_PREDRAW_OVERLAP=0: the pre-draw of chunk k + 1 waits for the block
+// kernel of chunk k (one stream) instead of running beside it on the other half of
+// the CUs (predraw_overlap_streams)
+bool predraw_overlap_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("VIABEL_AMD_PREDRAW_OVERLAP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // VIABEL_AMD_SEP_FUSE_VALUES=1: short column-pair chunks reduce their per-step
 // values in the kernel's last block instead of a second launch
 // (sep_values_kernel).  Measured slower, so off: the 20-step headline launch's
@@ -274,6 +297,47 @@ int check_ctx(vb_ctx* c) {
   if (!c) return fail(VB_EINVAL, "null vb_ctx");
   VB_HIP(hipSetDevice(c->device));
   return VB_OK;
+}
+
+// The overlapped pre-draw's streams: the block kernel's latency-bound workgroups
+// (one per problem) on the even CUs, the throughput pre-draw of the next chunk on
+// the odd CUs (hipExtStreamCreateWithCUMask), so that neither shares a CU with the
+// other (a pre-draw beside the block kernel on shared CUs slowed the fit 18.7 ->
+// 26.5 ms).  Returns false (serial pre-draw) if the masks are refused.
+bool predraw_overlap_streams(vb_ctx* c) {
+  if (c->pd_ready >= 0) return c->pd_ready == 1;
+  c->pd_ready = 0;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
+      ncu < 8 || ncu > 1024) {
+    (void)hipGetLastError();
+    return false;
+  }
+  // VIABEL_AMD_PREDRAW_MASK (A/B): default the block kernel on the first half of the
+  // CU ids and the pre-draw on the second; "even" = even / odd CU ids; "free" = the
+  // block kernel on an unmasked stream (config 5's fit 14.8-14.9 / 15.0-15.3 /
+  // 15.2-15.3 ms, profiles/r04/predraw_mask_ab.log)
+  const char* mode = std::getenv("VIABEL_AMD_PREDRAW_MASK");
+  const int m = (mode && mode[0] == 'e') ? 0 : (mode && mode[0] == 'f') ? 2 : 1;
+  std::vector<uint32_t> even((ncu + 31) / 32, 0u), odd((ncu + 31) / 32, 0u);
+  for (int i = 0; i < ncu; ++i) {
+    const bool second = m == 1 ? i >= ncu / 2 : (i % 2) != 0;
+    (second ? odd : even)[i / 32] |= 1u << (i % 32);
+  }
+  hipError_t e1 = m == 2 ? hipStreamCreateWithFlags(&c->blk_stream, hipStreamNonBlocking)
+                         : hipExtStreamCreateWithCUMask(&c->blk_stream, (uint32_t)even.size(), even.data());
+  if (e1 != hipSuccess ||
+      hipExtStreamCreateWithCUMask(&c->pd_stream, (uint32_t)odd.size(), odd.data()) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  for (hipEvent_t& e : c->pd_ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+  c->pd_ready = 1;
+  return true;
 }
 
 struct FamInfo {
@@ -789,6 +853,7 @@ struct vb_run {
   DevBuf lam, ring, hist, values, vpart, noise, smooth;
   DevBuf ticket;  // column-pair path: the in-kernel value combine's block counter
   DevBuf noise_lq;  // pre-drawn log q partials (block kernel, predraw)
+  DevBuf noise2, noise_lq2;  // the second chunk buffer of the overlapped pre-draw
   // full-rank family / wide mean-field: one value_grad + update per step
   bool fr = false, wide = false;
   vbk::FrSpec spec{};
@@ -1168,21 +1233,59 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
       const size_t per_step = (size_t)r->nprob * N * (D + (need_lq ? 1 : 0)) * sizeof(double);
       const long long cap = std::max<long long>(1, (long long)(kPredrawBytes / per_step));
       const int cmax = (int)std::min<long long>({n_steps, cap, (long long)kPredrawMaxSteps});
-      VB_TRY(r->noise.reserve((size_t)r->nprob * cmax * N * D * sizeof(double)));
-      if (need_lq) VB_TRY(r->noise_lq.reserve((size_t)r->nprob * cmax * N * sizeof(double)));
-      for (long long off = 0; off < n_steps; off += cmax) {
+      const size_t nb = (size_t)r->nprob * cmax * N * D * sizeof(double);
+      const size_t lb = (size_t)r->nprob * cmax * N * sizeof(double);
+      VB_TRY(r->noise.reserve(nb));
+      if (need_lq) VB_TRY(r->noise_lq.reserve(lb));
+      // more than one chunk: chunk k + 1 is drawn on the odd CUs while the block
+      // kernel runs chunk k on the even ones (two buffers, events between the
+      // streams; the same draws and bits as the serial order)
+      // (the streams are made on the first pre-drawn advance, whether or not it
+      // overlaps: creating them costs milliseconds, paid outside later timed runs)
+      const bool streams = predraw_overlap_enabled() && predraw_overlap_streams(c);
+      // (several problems only: one problem's pre-draw is a few us per chunk, and
+      // the cross-queue waits cost configs 1 / 2 ~3 %, profiles/r04/predraw_overlap_ab2.log)
+      const bool overlap = n_steps > cmax && streams && r->nprob >= kPredrawOverlapMinProblems;
+      if (overlap) {
+        VB_TRY(r->noise2.reserve(nb));
+        if (need_lq) VB_TRY(r->noise_lq2.reserve(lb));
+      }
+      hipStream_t pd_s = overlap ? c->pd_stream : c->stream;
+      hipStream_t blk_s = overlap ? c->blk_stream : c->stream;
+      hipEvent_t* ev = c->pd_ev;   // [0] start, [1..2] pre-draw of buffer b, [3..4] block of buffer b, [5] end
+      if (overlap) {
+        VB_HIP(hipEventRecord(ev[0], c->stream));
+        VB_HIP(hipStreamWaitEvent(pd_s, ev[0], 0));
+        VB_HIP(hipStreamWaitEvent(blk_s, ev[0], 0));
+      }
+      int k = 0;
+      for (long long off = 0; off < n_steps; off += cmax, ++k) {
         const int cs = (int)std::min<long long>(cmax, n_steps - off);
+        const int bsel = overlap ? (k & 1) : 0;
+        double* nz = bsel ? r->noise2.d() : r->noise.d();
+        double* nlq = need_lq ? (bsel ? r->noise_lq2.d() : r->noise_lq.d()) : nullptr;
+        if (overlap && k >= 2) VB_HIP(hipStreamWaitEvent(pd_s, ev[3 + bsel], 0));  // buffer consumed
         VB_HIP(vbk::launch_block_predraw(r->fi.kind, D, N, cs, (int)r->nprob, k0, k1, a.stream,
                                          a.stream_stride, (long long)noise->step + off,
                                          r->fi.t_scale, r->fi.shape, r->fi.df, r->fi.t_const,
-                                         r->noise.d(), need_lq ? r->noise_lq.d() : nullptr,
-                                         c->stream));
+                                         nz, nlq, pd_s));
+        if (overlap) {
+          VB_HIP(hipEventRecord(ev[1 + bsel], pd_s));
+          VB_HIP(hipStreamWaitEvent(blk_s, ev[1 + bsel], 0));
+        }
         vbk::BlockArgs b = a;
         b.n_steps = cs;
         b.step0 = r->done + off;
-        b.noise = r->noise.d();
-        b.noise_lq = need_lq ? r->noise_lq.d() : nullptr;
-        VB_HIP(vbk::launch_block(r->fi.kind, r->tgt, true, b, (int)r->nprob, c->stream));
+        b.noise = nz;
+        b.noise_lq = nlq;
+        VB_HIP(vbk::launch_block(r->fi.kind, r->tgt, true, b, (int)r->nprob, blk_s));
+        if (overlap) VB_HIP(hipEventRecord(ev[3 + bsel], blk_s));
+      }
+      if (overlap) {
+        // the caller's stream resumes after both streams' work (the pre-draw stream
+        // finished before the last block launch it fed)
+        VB_HIP(hipEventRecord(ev[5], blk_s));
+        VB_HIP(hipStreamWaitEvent(c->stream, ev[5], 0));
       }
     } else {
       VB_HIP(vbk::launch_block(r->fi.kind, r->tgt, host, a, (int)r->nprob, c->stream));
