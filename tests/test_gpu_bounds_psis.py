@@ -176,6 +176,57 @@ def test_psislw_large_tail(n, reff):
     _close(out[:, 0], oout, rtol=1e-11, atol=1e-11)
 
 
+def test_psislw_tied_values_take_the_radix_path():
+    """Log weights on a grid of step 2 (value 8, where the order statistic falls,
+    is shared by ~8 500 of the 1e6 draws): the fast select's candidates -- every
+    draw at or above the order statistic's 22-bit key prefix -- exceed one
+    workgroup's sort, so the call takes the 8-pass radix select.  k equals the
+    oracle's; the smoothed weights are compared as a sorted multiset (np.argsort
+    orders ties arbitrarily, the device stably)."""
+    from viabel_amd import psis
+    from oracle import psis_oracle
+    rs = np.random.RandomState(11)
+    lw = 2.0 * np.round(rs.randn(1_000_000) * 1.5)
+    assert np.sum(lw == 8.0) > 8192
+    out, k = psis.psislw(lw)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        oout, ok = psis_oracle.psislw(lw.copy())
+    _close(k, ok, rtol=1e-9)
+    _close(np.sort(out), np.sort(oout), rtol=1e-11, atol=1e-11)
+
+
+_FAST = '''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from viabel_amd import psis
+rs = np.random.RandomState(5)
+lw = rs.standard_t(3, (300_000, 6)) * 1.4 - 3.0
+out, k, tails = psis.psislw_with_tail(lw)
+np.savez(sys.argv[2], out=out, k=k, t0=tails[0], t5=tails[5])
+'''
+
+
+def test_psis_fast_select_equals_radix_select(tmp_path):
+    """The two-digit select + candidate sort against the 8-pass radix select
+    (VIABEL_AMD_PSIS_FAST_SELECT=0, read once per process: child processes) on 6
+    columns: k, smoothed weights and tail orders bit for bit."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for mode in ('0', '1'):
+        f = str(tmp_path / ('f%s.npz' % mode))
+        env = dict(os.environ, VIABEL_AMD_PSIS_FAST_SELECT=mode)
+        r = subprocess.run([sys.executable, '-c', _FAST, root, f], env=env, capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        res[mode] = np.load(f)
+    for key in ('out', 'k', 't0', 't5'):
+        np.testing.assert_array_equal(res['0'][key], res['1'][key])
+
+
 def test_gpdfit_large():
     from viabel_amd import psis
     from oracle import psis_oracle

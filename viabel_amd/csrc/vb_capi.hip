@@ -1722,13 +1722,15 @@ static int psislw_impl(vb_ctx* c, const double* lw, int64_t n, int64_t m, long l
   OutT<long long> dti, dnt;
   VB_TRY(dti.stage(c, 4, reinterpret_cast<long long*>(tail_idx_out),
                    tail_idx_out ? (size_t)tail_cap * m : 0));
+  VB_TRY(c->slot[6].reserve(sizeof(unsigned) * (size_t)group));   // fast-select flags
   VB_TRY(dnt.stage(c, 5, reinterpret_cast<long long*>(n_tail_out), n_tail_out ? (size_t)m : 0));
   for (int64_t c0 = 0; c0 < m; c0 += group) {
     const int g = (int)std::min<int64_t>(group, m - c0);
     VB_HIP(vbk::psis_columns(dlw.d + c0 * cs, dout.d ? dout.d + c0 * cs : nullptr, n, g, rs, cs,
                              Mt, c->slot[3].p,
                              dk.d + c0, dti.d ? dti.d + (size_t)c0 * tail_cap : nullptr,
-                             (long long)tail_cap, dnt.d ? dnt.d + c0 : nullptr, c->stream));
+                             (long long)tail_cap, dnt.d ? dnt.d + c0 : nullptr, c->stream,
+                             static_cast<unsigned*>(c->slot[6].p)));
   }
   VB_TRY(dout.finish(c));
   VB_TRY(dk.finish(c));

@@ -174,7 +174,7 @@ size_t psis_col_stride(long long tail_cap);      // scratch bytes per column of 
 hipError_t psis_columns(const double* lw, double* out, long long n, int m, long long rs,
                         long long cs, long long Mt, void* scratch, double* k_dev,
                         long long* tail_idx_dev, long long tail_cap, long long* n_tail_dev,
-                        hipStream_t s);
+                        hipStream_t s, unsigned* flag_dev = nullptr);
 hipError_t psis_gpdfit(const double* x, long long n, void* scratch, double* out4,
                        double* ks_out, double* w_out, hipStream_t s);
 hipError_t psis_gpinv(const double* p, long long n, double k, double sigma, double* out,

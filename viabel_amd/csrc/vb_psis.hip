@@ -14,6 +14,13 @@
 //   3. stable compaction of x > cutoff (ascending index order, like np.where)
 //   4. one-workgroup LDS bitonic sort of the tail on the key (value, position)
 //      -> x2si (bit-exact tail order for distinct values)
+// Fast path for tails of <= kTailMax candidates (psis_columns, round 4): the
+// column max and an 11-bit histogram of the key in one pass, a second 11-bit
+// histogram inside the selected bin, then ONE compaction of every element whose
+// 22-bit key prefix is >= the selected one (the order statistic and everything
+// above it, ~M + a few dozen draws) and one LDS sort of those on (key of x - max,
+// index): the order statistic, the cutoff and the sorted tail fall out of the
+// sorted candidates.  3 passes over the column instead of 11; the same bits.
 //   5. GPD fit: one block per quadrature point b_j, then one combining block
 //   6. smoothing scatter + clamp, 7. log-sum-exp renormalisation.
 // All state between launches stays on the device (no host round trips), so a
@@ -22,6 +29,8 @@
 #include "vb_internal.hpp"
 
 #include <algorithm>
+#include <cstdlib>
+#include <vector>
 
 #include <hipcub/hipcub.hpp>
 
@@ -36,6 +45,15 @@ constexpr int kTailMax = 8192;  // tails up to this size: one workgroup's LDS bi
                                 // larger tails: stable device radix sort (hipcub)
 constexpr int kPsisBlocks = 512;
 
+// VIABEL_AMD_PSIS_FAST_SELECT=0: always the 8-pass radix select (A/B switch; same bits)
+static bool psis_fast_select_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("VIABEL_AMD_PSIS_FAST_SELECT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // device scratch layout for one column (see psis_scratch_doubles)
 struct PsisState {
   double mx;         // column max
@@ -49,7 +67,11 @@ struct PsisState {
   long long n2;      // tail size
   long long m;       // quadrature points
   long long nkeep;   // kept weights
+  long long above;   // two-digit select: elements above the selected bins
+  long long cand;    // candidates: elements whose 22-bit key prefix >= the selected one
+  unsigned long long cnt;   // candidate compaction counter
 };
+static_assert(sizeof(PsisState) <= 256, "PsisState fits its scratch slot");
 
 __device__ __forceinline__ unsigned long long dkey(double v) {
   const unsigned long long u = (unsigned long long)__double_as_longlong(v);
@@ -180,6 +202,238 @@ __global__ __launch_bounds__(256) void radix_init_kernel(PsisState* ps, unsigned
   ps->n2 = 0;
   ps->k = NAN;
   ps->sigma = NAN;
+}
+
+// ---- 2'. two-digit select + candidate compaction (fast path) -----------------
+constexpr int kSelBins = 2048;              // 11-bit digits
+constexpr int kSelShift1 = 53, kSelShift2 = 42;
+
+__global__ __launch_bounds__(256) void sel_init_kernel(PsisState* ps, unsigned* gh, long long rank,
+                                                       long long sb) {
+  gh = colp(gh, sb);
+  for (int b = threadIdx.x; b < kSelBins; b += 256) gh[b] = 0;
+  if (threadIdx.x != 0) return;
+  ps = colp(ps, sb);
+  ps->prefix = 0;
+  ps->mask = 0;
+  ps->rank = rank;
+  ps->n2 = 0;
+  ps->k = NAN;
+  ps->sigma = NAN;
+  ps->above = 0;
+  ps->cand = 0;
+  ps->cnt = 0;
+}
+
+// pass 1: the column max (block partials) and the histogram of the top 11 key bits
+__global__ __launch_bounds__(256) void sel_hist1_kernel(const double* x, long long n, long long rs,
+                                                        long long cs, double* part, unsigned* gh,
+                                                        long long sb) {
+  __shared__ unsigned h[kSelBins];
+  __shared__ double red[16];
+  for (int b = threadIdx.x; b < kSelBins; b += 256) h[b] = 0;
+  __syncthreads();
+  x += (long long)blockIdx.y * cs;
+  double m = -INFINITY;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const double v = x[i * rs];
+    m = fmax(m, v);
+    atomicAdd(&h[dkey(v) >> kSelShift1], 1u);
+  }
+  m = bmax(m, red);   // (its barriers also complete the LDS histogram)
+  if (threadIdx.x == 0) colp(part, sb)[blockIdx.x] = m;
+  unsigned* g = colp(gh, sb);
+  for (int b = threadIdx.x; b < kSelBins; b += 256)
+    if (h[b]) atomicAdd(&g[b], h[b]);
+}
+
+// pass 2: the next 11 key bits of the elements in the selected top bin
+__global__ __launch_bounds__(256) void sel_hist2_kernel(const double* x, long long n, long long rs,
+                                                        long long cs, const PsisState* ps,
+                                                        unsigned* gh, long long sb) {
+  __shared__ unsigned h[kSelBins];
+  for (int b = threadIdx.x; b < kSelBins; b += 256) h[b] = 0;
+  __syncthreads();
+  x += (long long)blockIdx.y * cs;
+  const unsigned long long top = colp(ps, sb)->prefix >> kSelShift1;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const unsigned long long k = dkey(x[i * rs]);
+    if ((k >> kSelShift1) == top) atomicAdd(&h[(k >> kSelShift2) & (kSelBins - 1)], 1u);
+  }
+  __syncthreads();
+  unsigned* g = colp(gh, sb);
+  for (int b = threadIdx.x; b < kSelBins; b += 256)
+    if (h[b]) atomicAdd(&g[b], h[b]);
+}
+
+// the bin holding ascending rank ps->rank of this stage's population (a parallel
+// scan over 2 048 bins), then clears the histogram; stage 2 also counts the
+// candidates (everything at or above the selected 22-bit prefix) and flags
+// whether they fit one workgroup's sort
+__global__ __launch_bounds__(256) void sel_pick_kernel(unsigned* gh, PsisState* ps, int stage,
+                                                       unsigned* flag, long long sb) {
+  __shared__ unsigned long long wsum[4];
+  gh = colp(gh, sb);
+  ps = colp(ps, sb);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  unsigned c[8];
+  unsigned long long sum = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    c[k] = gh[t * 8 + k];
+    sum += c[k];
+  }
+  unsigned long long inc = sum;
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long o = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += o;
+  }
+  if (lane == 63) wsum[w] = inc;
+  const long long r = ps->rank;
+  if (stage == 1 && t == 0) flag[blockIdx.y] = 0u;   // set by stage 2's pick
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) gh[t * 8 + k] = 0;
+  unsigned long long base = 0;
+  for (int q = 0; q < w; ++q) base += wsum[q];
+  const unsigned long long tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  const unsigned long long excl = base + inc - sum;
+  if ((long long)excl <= r && r < (long long)(excl + sum)) {   // exactly one thread
+    unsigned long long cum = excl;
+    int b = 0;
+    for (; b < 7; ++b) {
+      if ((long long)(cum + c[b]) > r) break;
+      cum += c[b];
+    }
+    const int shift = stage == 1 ? kSelShift1 : kSelShift2;
+    ps->prefix |= (unsigned long long)(t * 8 + b) << shift;
+    ps->mask |= (unsigned long long)(kSelBins - 1) << shift;
+    ps->rank = r - (long long)cum;
+    const long long above = (long long)(tot - cum - c[b]);
+    if (stage == 1) {
+      ps->above = above;
+    } else {
+      ps->above += above;
+      ps->cand = ps->above + (long long)c[b];
+      flag[blockIdx.y] = ps->cand <= kTailMax ? 1u : 0u;
+    }
+  }
+}
+
+// every element whose 22-bit key prefix is >= the selected one: (x - max, index),
+// in any order (the sort orders them), one counter per column
+__global__ __launch_bounds__(256) void sel_compact_kernel(const double* x, long long n, long long rs,
+                                                          long long cs, PsisState* ps, double* tv,
+                                                          long long* ti, long long sb) {
+  ps = colp(ps, sb);
+  if (ps->cand > kTailMax) return;
+  const unsigned long long p22 = ps->prefix >> kSelShift2;
+  const double mx = ps->mx;
+  x += (long long)blockIdx.y * cs;
+  tv = colp(tv, sb);
+  ti = colp(ti, sb);
+  const int lane = threadIdx.x & 63;
+  for (long long i0 = (long long)blockIdx.x * 256; i0 < n; i0 += (long long)gridDim.x * 256) {
+    const long long i = i0 + threadIdx.x;
+    bool f = false;
+    double v = 0.0;
+    if (i < n) {
+      const double xv = x[i * rs];
+      f = (dkey(xv) >> kSelShift2) >= p22;
+      v = xv - mx;
+    }
+    const unsigned long long bal = __ballot(f);
+    if (bal) {
+      unsigned long long b0 = 0;
+      if (lane == 0) b0 = atomicAdd(&ps->cnt, (unsigned long long)__popcll(bal));
+      b0 = __shfl(b0, 0, 64);
+      if (f) {
+        const unsigned long long pos = b0 + __popcll(bal & ((1ull << lane) - 1ull));
+        if (pos < (unsigned long long)kTailMax) {
+          tv[pos] = v;
+          ti[pos] = i;
+        }
+      }
+    }
+  }
+}
+
+// one workgroup per column: the candidates sorted on (key of x - max, index); the
+// order statistic at ascending rank n - Mt - 1 is candidate (n - Mt - 1) - (n - cand);
+// cutoff = max(its value, log(tiny)) as cutoff_kernel; the tail (x - max > cutoff)
+// is a run of the sorted candidates, written like tail_sort_kernel's output
+__global__ __launch_bounds__(1024) void sel_sort_kernel(const double* tv, const long long* ti,
+                                                        PsisState* ps, double* sv, long long* si,
+                                                        long long n, long long Mt, double cutoffmin,
+                                                        long long sb) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned long long* key = reinterpret_cast<unsigned long long*>(smem);
+  unsigned* idx = reinterpret_cast<unsigned*>(smem + sizeof(unsigned long long) * kTailMax);
+  __shared__ int s_first, s_cnt;
+  tv = colp(tv, sb);
+  ti = colp(ti, sb);
+  sv = colp(sv, sb);
+  si = colp(si, sb);
+  ps = colp(ps, sb);
+  const long long c = ps->cand;
+  if (c > kTailMax) return;
+  int np2 = 1;
+  while (np2 < c) np2 <<= 1;
+  for (int i = threadIdx.x; i < np2; i += 1024) {
+    key[i] = i < c ? dkey(tv[i]) : ~0ull;
+    idx[i] = i < c ? (unsigned)ti[i] : 0xFFFFFFFFu;
+  }
+  if (threadIdx.x == 0) {
+    s_first = (int)c;
+    s_cnt = 0;
+  }
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < np2; i += 1024) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool up = (i & k) == 0;
+          const unsigned long long ki = key[i], kl = key[l];
+          const unsigned pi = idx[i], pl = idx[l];
+          const bool gt = (ki > kl) || (ki == kl && pi > pl);
+          if (gt == up) {
+            key[i] = kl;
+            key[l] = ki;
+            idx[i] = pl;
+            idx[l] = pi;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const long long q = (n - Mt - 1) - (n - c);
+  const double xs = dval(key[q]);
+  const double xc = (cutoffmin > xs) ? cutoffmin : xs;
+  // the tail: candidates with value > cutoff (a contiguous run: NaNs, which never
+  // compare greater, sort to the ends)
+  int cnt = 0, first = (int)c;
+  for (int i = threadIdx.x; i < (int)c; i += 1024)
+    if (dval(key[i]) > xc) {
+      ++cnt;
+      first = min(first, i);
+    }
+  atomicAdd(&s_cnt, cnt);
+  atomicMin(&s_first, first);
+  __syncthreads();
+  const int n2 = s_cnt, t0 = s_first;
+  for (int i = threadIdx.x; i < n2; i += 1024) {
+    sv[i] = dval(key[t0 + i]);
+    si[i] = idx[t0 + i];
+  }
+  if (threadIdx.x == 0) {
+    ps->xcut = xc;
+    ps->expcut = exp(xc);
+    ps->n2 = n2;
+  }
 }
 
 // ---- 3. shift + stable compaction ------------------------------------------
@@ -585,7 +839,7 @@ static long long cap_of(long long cap) { return cap < kTailMax ? kTailMax : cap;
 size_t psis_scratch_bytes(long long tail_cap) {
   const long long cap = cap_of(tail_cap);
   // state + partials + radix hist + tail (value, index) x2 + y + grid arrays + sort temp
-  return 256 + sizeof(double) * kPsisBlocks * 2 + sizeof(unsigned) * 256 +
+  return 256 + sizeof(double) * kPsisBlocks * 2 + sizeof(unsigned) * kSelBins +
          sizeof(unsigned) * kPsisBlocks + 2 * cap * (sizeof(double) + sizeof(long long)) +
          sizeof(double) * cap + sizeof(double) * 8 * 256 + radix_temp_bytes(tail_cap) + 256;
 }
@@ -616,7 +870,7 @@ static PsisScratch carve(void* base, long long tail_cap) {
   s.part = reinterpret_cast<double*>(p);
   p += sizeof(double) * kPsisBlocks * 2;
   s.hist = reinterpret_cast<unsigned*>(p);
-  p += sizeof(unsigned) * 256;
+  p += sizeof(unsigned) * kSelBins;   // (the radix passes use the first 256)
   s.cnt = reinterpret_cast<unsigned*>(p);
   p += sizeof(unsigned) * kPsisBlocks;
   s.tv = reinterpret_cast<double*>(p);
@@ -683,43 +937,70 @@ size_t psis_col_stride(long long tail_cap) {
 hipError_t psis_columns(const double* lw, double* out, long long n, int m, long long rs,
                         long long cs, long long Mt, void* scratch, double* k_dev,
                         long long* tail_idx_dev, long long tail_cap, long long* n_tail_dev,
-                        hipStream_t s) {
+                        hipStream_t s, unsigned* flag_dev) {
   const long long cap = Mt < 1 ? 1 : Mt;   // the tail holds at most M_t draws
   const long long sb = (long long)psis_col_stride(cap);
   PsisScratch S = carve(scratch, cap);
   const int g = psis_grid(n);
-  // 1. max
-  hipLaunchKernelGGL(col_max_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.part, sb);
-  hipLaunchKernelGGL(max_final_kernel, dim3(1, m), dim3(256), 0, s, S.part, g, &S.ps->mx, sb);
-  // 2. radix select of ascending rank n - Mt - 1 (the pick clears the histogram)
-  hipLaunchKernelGGL(radix_init_kernel, dim3(1, m), dim3(256), 0, s, S.ps, S.hist, n - Mt - 1, sb);
-  for (int pass = 0; pass < 8; ++pass) {
-    const int shift = 56 - 8 * pass;
-    hipLaunchKernelGGL(radix_hist_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.ps, shift,
-                       S.hist, sb);
-    hipLaunchKernelGGL(radix_pick_kernel, dim3(1, m), dim3(256), 0, s, S.hist, shift, S.ps, sb);
+  const size_t sort_lds = (sizeof(unsigned long long) + sizeof(unsigned)) * kTailMax;
+  // fast path (see the header): 1 + 2 in two histogram passes; the host reads the
+  // per-column flags (one wait) and takes the radix path when any column's
+  // candidates exceed one workgroup's sort
+  bool fast = flag_dev && psis_fast_select_enabled() && cap <= kTailMax && n < (1LL << 31);
+  if (fast) {
+    hipLaunchKernelGGL(sel_init_kernel, dim3(1, m), dim3(256), 0, s, S.ps, S.hist, n - Mt - 1, sb);
+    hipLaunchKernelGGL(sel_hist1_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.part, S.hist,
+                       sb);
+    hipLaunchKernelGGL(max_final_kernel, dim3(1, m), dim3(256), 0, s, S.part, g, &S.ps->mx, sb);
+    hipLaunchKernelGGL(sel_pick_kernel, dim3(1, m), dim3(256), 0, s, S.hist, S.ps, 1, flag_dev, sb);
+    hipLaunchKernelGGL(sel_hist2_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.ps, S.hist,
+                       sb);
+    hipLaunchKernelGGL(sel_pick_kernel, dim3(1, m), dim3(256), 0, s, S.hist, S.ps, 2, flag_dev, sb);
+    std::vector<unsigned> fl((size_t)m, 0u);
+    hipError_t e = hipMemcpyAsync(fl.data(), flag_dev, sizeof(unsigned) * m, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    for (unsigned f : fl) fast = fast && f == 1u;
+  } else {
+    hipLaunchKernelGGL(col_max_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.part, sb);
+    hipLaunchKernelGGL(max_final_kernel, dim3(1, m), dim3(256), 0, s, S.part, g, &S.ps->mx, sb);
   }
-  hipLaunchKernelGGL(cutoff_kernel, dim3(1, m), dim3(64), 0, s, S.ps, log(DBL_MIN), sb);
-  // 3. shifted copy + stable tail compaction
-  const long long chunk = ((n + g - 1) / g + 255) / 256 * 256;
-  const int gc = (int)((n + chunk - 1) / chunk);
-  // (out null: k and the tails only -- the shift is applied on the fly and the
-  // smoothing / renormalisation below, which only feed out, are skipped)
-  const int unshifted = out ? 0 : 1;
-  const double* sx = out ? out : lw;
   if (out)
     hipLaunchKernelGGL(shift_kernel, dim3(g, m), dim3(256), 0, s, lw, out, n, rs, cs, S.ps, sb);
-  hipLaunchKernelGGL(tail_count_kernel, dim3(gc, m), dim3(256), 0, s, sx, n, rs, cs, chunk, S.ps,
-                     S.cnt, sb, unshifted);
-  hipLaunchKernelGGL(tail_scan_kernel, dim3(1, m), dim3(64), 0, s, S.cnt, gc, S.ps, sb);
-  if (cap > kTailMax)
-    hipLaunchKernelGGL(fill_inf_kernel, dim3((unsigned)((cap + 255) / 256), m), dim3(256), 0, s,
-                       S.tv, cap, sb);
-  hipLaunchKernelGGL(tail_compact_kernel, dim3(gc, m), dim3(256), 0, s, sx, n, rs, cs, chunk,
-                     S.ps, S.cnt, cap, S.tv, S.ti, sb, unshifted);
-  // 4. sort the tails
-  hipError_t e = sort_tail(S, cap, m, sb, s);
-  if (e != hipSuccess) return e;
+  if (fast) {
+    hipLaunchKernelGGL(sel_compact_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.ps, S.tv,
+                       S.ti, sb);
+    hipLaunchKernelGGL(sel_sort_kernel, dim3(1, m), dim3(1024), sort_lds, s, S.tv, S.ti, S.ps, S.sv,
+                       S.si, n, Mt, log(DBL_MIN), sb);
+  } else {
+    // 2. radix select of ascending rank n - Mt - 1 (the pick clears the histogram)
+    hipLaunchKernelGGL(radix_init_kernel, dim3(1, m), dim3(256), 0, s, S.ps, S.hist, n - Mt - 1, sb);
+    for (int pass = 0; pass < 8; ++pass) {
+      const int shift = 56 - 8 * pass;
+      hipLaunchKernelGGL(radix_hist_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.ps, shift,
+                         S.hist, sb);
+      hipLaunchKernelGGL(radix_pick_kernel, dim3(1, m), dim3(256), 0, s, S.hist, shift, S.ps, sb);
+    }
+    hipLaunchKernelGGL(cutoff_kernel, dim3(1, m), dim3(64), 0, s, S.ps, log(DBL_MIN), sb);
+    // 3. stable tail compaction of the shifted values
+    const long long chunk = ((n + g - 1) / g + 255) / 256 * 256;
+    const int gc = (int)((n + chunk - 1) / chunk);
+    // (out null: k and the tails only -- the shift is applied on the fly and the
+    // smoothing / renormalisation below, which only feed out, are skipped)
+    const int unshifted = out ? 0 : 1;
+    const double* sx = out ? out : lw;
+    hipLaunchKernelGGL(tail_count_kernel, dim3(gc, m), dim3(256), 0, s, sx, n, rs, cs, chunk, S.ps,
+                       S.cnt, sb, unshifted);
+    hipLaunchKernelGGL(tail_scan_kernel, dim3(1, m), dim3(64), 0, s, S.cnt, gc, S.ps, sb);
+    if (cap > kTailMax)
+      hipLaunchKernelGGL(fill_inf_kernel, dim3((unsigned)((cap + 255) / 256), m), dim3(256), 0, s,
+                         S.tv, cap, sb);
+    hipLaunchKernelGGL(tail_compact_kernel, dim3(gc, m), dim3(256), 0, s, sx, n, rs, cs, chunk,
+                       S.ps, S.cnt, cap, S.tv, S.ti, sb, unshifted);
+    // 4. sort the tails
+    hipError_t e = sort_tail(S, cap, m, sb, s);
+    if (e != hipSuccess) return e;
+  }
   // 5. GPD fit (skipped on device when n2 <= 4)
   hipLaunchKernelGGL(gpd_prep_kernel, dim3(32, m), dim3(256), 0, s, S.sv, S.ps, S.y, cap, sb);
   const int mmax = 30 + (int)std::sqrt((double)Mt) + 1;
