@@ -544,6 +544,31 @@ struct EightSchools {
     g[1] = gu;
     return lp;
   }
+  // log p alone with the LDS log table (log-weight kernels, which load the
+  // Box-Muller tables and discard the gradient): log1p(t5^2) through
+  // log1p_pos_tab (~1 ulp) instead of the double-double library log1p, which was
+  // ~100 of a draw row's ~2 500 instructions; non-finite arguments take the
+  // library form
+  template <int DMAX>
+  __device__ __forceinline__ static double lp_tab(const double* x, int /*D*/, const double2* lt) {
+    constexpr double y[8] = {28., 8., -3., 7., -1., 1., 18., 12.};
+    constexpr double is[8] = {1. / 15., 1. / 10., 1. / 16., 1. / 11.,
+                              1. / 9.,  1. / 11., 1. / 10., 1. / 18.};
+    const double mu = x[0], u = x[1], tau = exp(u);
+    const double t5 = tau * 0.2, m5 = mu * 0.2;
+    const double w = t5 * t5;
+    double l1;
+    if (w < 0x1p+1000) l1 = log1p_pos_tab(w, lt);
+    else l1 = log1p(w);
+    double lp = -0.5 * m5 * m5 - l1 + u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double th = x[2 + j];
+      const double r = (y[j] - mu - tau * th) * is[j];
+      lp += -0.5 * th * th - 0.5 * r * r;
+    }
+    return lp;
+  }
   // Split rows (see Funnel::row_half): lane 0 owns mu, log tau and theta_tilde
   // 0-2, lane 1 theta_tilde 3-7 (DH = 5); both compute tau.  The pair's mu and
   // log tau gradient parts are summed with one DPP swap each.

@@ -2204,7 +2204,13 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
       }
     }
   }
-  const double lp = RowOf<TGT>::template row<DMAX>(x, g, D);
+  double lp;
+  if constexpr (std::is_same_v<TGT, EightSchools> && !HOST) {
+    lp = TGT::template lp_tab<DMAX>(x, D, s_lt);
+    (void)g;
+  } else {
+    lp = RowOf<TGT>::template row<DMAX>(x, g, D);
+  }
   lw[r] = lp - lq;
 }
 
