@@ -374,3 +374,44 @@ def test_ill_conditioned_single_call(objective):
         ov, og = fo.chivi_value_grad(ofam, otgt, lam, N, 2.0)
     np.testing.assert_allclose(v, ov, rtol=1e-9)
     _close(g, og, 1e-7)
+
+
+_EPI = '''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from viabel_amd import vb, targets
+Dm = 512
+rs = np.random.RandomState(4)
+tri = np.tril_indices(Dm)
+free = rs.randn(len(tri[0])) * 0.01
+free[tri[0] == tri[1]] = rs.randn(Dm) * 0.1
+lam0 = np.concatenate([np.zeros(Dm), free])
+fam = vb.t_variational_family(Dm, 100.0, rng='philox')
+obj = vb.black_box_chivi(2.0, fam, targets.corr_gauss(Dm), 128)
+run = vb.DeviceRun(obj, 30, lam0, window=10, learning_rate=0.01, epsilon=0.1)
+run.advance_philox(30, 0, 1, 0)
+lam, hist, vals, _ = run.result()
+np.savez(sys.argv[2], lam=lam, vals=vals)
+'''
+
+
+def test_exact_epilogue_kernels_equal_the_generic_kernel(tmp_path):
+    """The GEMM kernels compiled for exact epilogue feature sets (DESIGN §4 round 4)
+    against the generic kernel (VIABEL_AMD_GEMM_EPI_EXACT=0, read once per process:
+    child processes): 30 config-4 steps agree to rounding (the two compilations
+    contract a few multiply-adds differently: ~1 ulp per step, 6e-16 absolute
+    after 30 steps; bar 1e-12 absolute, 1e-9 relative)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for mode in ('0', '1'):
+        f = str(tmp_path / ('e%s.npz' % mode))
+        env = dict(os.environ, VIABEL_AMD_GEMM_EPI_EXACT=mode)
+        r = subprocess.run([sys.executable, '-c', _EPI, root, f], env=env, capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        res[mode] = np.load(f)
+    for key in ('lam', 'vals'):
+        np.testing.assert_allclose(res['0'][key], res['1'][key], rtol=1e-9, atol=1e-12)

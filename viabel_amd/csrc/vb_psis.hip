@@ -235,8 +235,20 @@ __global__ __launch_bounds__(256) void sel_hist1_kernel(const double* x, long lo
   __syncthreads();
   x += (long long)blockIdx.y * cs;
   double m = -INFINITY;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
-       i += (long long)gridDim.x * 256) {
+  // four loads in flight per thread (one at a time left the pass latency-bound)
+  const long long st = (long long)gridDim.x * 256;
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * st < n; i += 4 * st) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = x[(i + u * st) * rs];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      m = fmax(m, v[u]);
+      atomicAdd(&h[dkey(v[u]) >> kSelShift1], 1u);
+    }
+  }
+  for (; i < n; i += st) {
     const double v = x[i * rs];
     m = fmax(m, v);
     atomicAdd(&h[dkey(v) >> kSelShift1], 1u);
@@ -257,8 +269,17 @@ __global__ __launch_bounds__(256) void sel_hist2_kernel(const double* x, long lo
   __syncthreads();
   x += (long long)blockIdx.y * cs;
   const unsigned long long top = colp(ps, sb)->prefix >> kSelShift1;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
-       i += (long long)gridDim.x * 256) {
+  const long long st = (long long)gridDim.x * 256;
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * st < n; i += 4 * st) {
+    unsigned long long k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k[u] = dkey(x[(i + u * st) * rs]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if ((k[u] >> kSelShift1) == top) atomicAdd(&h[(k[u] >> kSelShift2) & (kSelBins - 1)], 1u);
+  }
+  for (; i < n; i += st) {
     const unsigned long long k = dkey(x[i * rs]);
     if ((k >> kSelShift1) == top) atomicAdd(&h[(k >> kSelShift2) & (kSelBins - 1)], 1u);
   }
@@ -323,10 +344,18 @@ __global__ __launch_bounds__(256) void sel_pick_kernel(unsigned* gh, PsisState* 
 }
 
 // every element whose 22-bit key prefix is >= the selected one: (x - max, index),
-// in any order (the sort orders them), one counter per column
+// in any order (the sort orders them).  Each wave gathers its hits in LDS (ballot
+// offsets, no atomics), then the block reserves its run with ONE counter add
+// (a fetch-add per hit wave waited a round trip each: 378 us for the pass);
+// hits past a wave's LDS capacity go out directly with a wave-level add.
+constexpr int kCompactWaveCap = 128;
 __global__ __launch_bounds__(256) void sel_compact_kernel(const double* x, long long n, long long rs,
                                                           long long cs, PsisState* ps, double* tv,
                                                           long long* ti, long long sb) {
+  __shared__ double s_v[4][kCompactWaveCap];
+  __shared__ unsigned s_i[4][kCompactWaveCap];
+  __shared__ unsigned s_c[4];
+  __shared__ unsigned long long s_base;
   ps = colp(ps, sb);
   if (ps->cand > kTailMax) return;
   const unsigned long long p22 = ps->prefix >> kSelShift2;
@@ -334,8 +363,43 @@ __global__ __launch_bounds__(256) void sel_compact_kernel(const double* x, long 
   x += (long long)blockIdx.y * cs;
   tv = colp(tv, sb);
   ti = colp(ti, sb);
-  const int lane = threadIdx.x & 63;
-  for (long long i0 = (long long)blockIdx.x * 256; i0 < n; i0 += (long long)gridDim.x * 256) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  unsigned c = 0;   // this wave's hits so far (wave-uniform)
+  auto hit = [&](bool f, double v, long long i) __attribute__((always_inline)) {
+    const unsigned long long bal = __ballot(f);
+    if (!bal) return;
+    const unsigned pos = c + (unsigned)__popcll(bal & lt);
+    if (f && pos < (unsigned)kCompactWaveCap) {
+      s_v[w][pos] = v;
+      s_i[w][pos] = (unsigned)i;
+    }
+    const unsigned long long over = __ballot(f && pos >= (unsigned)kCompactWaveCap);
+    if (over) {
+      unsigned long long b0 = 0;
+      if (lane == 0) b0 = atomicAdd(&ps->cnt, (unsigned long long)__popcll(over));
+      b0 = __shfl(b0, 0, 64);
+      if (f && pos >= (unsigned)kCompactWaveCap) {
+        const unsigned long long q = b0 + __popcll(over & lt);
+        if (q < (unsigned long long)kTailMax) {
+          tv[q] = v;
+          ti[q] = i;
+        }
+      }
+    }
+    c += (unsigned)__popcll(bal);
+  };
+  const long long st = (long long)gridDim.x * 256;
+  long long i0 = (long long)blockIdx.x * 256;
+  for (; i0 + 3 * st + 255 < n; i0 += 4 * st) {   // four loads in flight (all in range)
+    double xv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xv[u] = x[(i0 + u * st + threadIdx.x) * rs];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      hit((dkey(xv[u]) >> kSelShift2) >= p22, xv[u] - mx, i0 + u * st + threadIdx.x);
+  }
+  for (; i0 < n; i0 += st) {
     const long long i = i0 + threadIdx.x;
     bool f = false;
     double v = 0.0;
@@ -344,18 +408,23 @@ __global__ __launch_bounds__(256) void sel_compact_kernel(const double* x, long 
       f = (dkey(xv) >> kSelShift2) >= p22;
       v = xv - mx;
     }
-    const unsigned long long bal = __ballot(f);
-    if (bal) {
-      unsigned long long b0 = 0;
-      if (lane == 0) b0 = atomicAdd(&ps->cnt, (unsigned long long)__popcll(bal));
-      b0 = __shfl(b0, 0, 64);
-      if (f) {
-        const unsigned long long pos = b0 + __popcll(bal & ((1ull << lane) - 1ull));
-        if (pos < (unsigned long long)kTailMax) {
-          tv[pos] = v;
-          ti[pos] = i;
-        }
-      }
+    hit(f, v, i);
+  }
+  const unsigned mine = c < (unsigned)kCompactWaveCap ? c : (unsigned)kCompactWaveCap;
+  if (lane == 0) s_c[w] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned tot = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+    s_base = tot ? atomicAdd(&ps->cnt, (unsigned long long)tot) : 0ull;
+  }
+  __syncthreads();
+  unsigned long long b = s_base;
+  for (int q = 0; q < w; ++q) b += s_c[q];
+  for (unsigned k = lane; k < mine; k += 64) {
+    const unsigned long long q = b + k;
+    if (q < (unsigned long long)kTailMax) {
+      tv[q] = s_v[w][k];
+      ti[q] = s_i[w][k];
     }
   }
 }
