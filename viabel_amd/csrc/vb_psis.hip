@@ -245,7 +245,18 @@ __global__ __launch_bounds__(256) void sel_hist1_kernel(const double* x, long lo
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       m = fmax(m, v[u]);
-      atomicAdd(&h[dkey(v[u]) >> kSelShift1], 1u);
+      // the top digit of log weights sits in a few bins: the lanes sharing the
+      // first lane's bin add their count with one atomic (a same-address LDS
+      // atomic from many lanes serialises), the others add their own
+      const unsigned b = (unsigned)(dkey(v[u]) >> kSelShift1);
+      const unsigned b0 = __builtin_amdgcn_readfirstlane(b);
+      const unsigned long long same = __ballot(b == b0);
+      if (b == b0) {
+        if ((threadIdx.x & 63) == (unsigned)__builtin_ctzll(same))
+          atomicAdd(&h[b0], (unsigned)__popcll(same));
+      } else {
+        atomicAdd(&h[b], 1u);
+      }
     }
   }
   for (; i < n; i += st) {
