@@ -16,5 +16,10 @@ timeout -k 10 500 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/be
 tail -c 300 gpurun_out/bench.log
 rm -rf gpurun_out/prof4
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o run --output-format csv -- \
-  python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/prof4.log 2>&1 || exit $?
+  python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/prof4.log 2>&1
+rc=$?
+# (the profiler's own teardown has segfaulted after a complete run with the CU-masked
+# pre-draw streams alive: the run counts when its JSON line and the stats are there)
+echo "rocprofv3 rc=$rc"
+grep -q '^{' gpurun_out/prof4.log && find gpurun_out/prof4 -name "*kernel_stats.csv" | grep -q . || exit 1
 find gpurun_out/prof4 -name "*kernel_stats.csv"
