@@ -460,10 +460,16 @@ struct Mixture {
     // 1 / (1 + exp(t)) = 1 / (1 + e) for t <= 0, e / (1 + e) for t > 0
     const double t = a - b;
     const double e = exp(-fabs(t));
-    const double r = 1.0 / (1.0 + e);
+    // e in (0, 1]: a refined reciprocal and the table-free log1p (~1 ulp each)
+    // instead of an IEEE division and the library's double-double log1p, which were
+    // most of a row's dependent chain in the block kernel (config 1)
+    const double d = 1.0 + e;
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(r, fma(-d, r, 1.0), r);
+    r = fma(r, fma(-d, r, 1.0), r);
     const double wb = t > 0.0 ? e * r : r;
     g = -(x + 2.0) + 4.0 * wb;
-    return (t > 0.0 ? a : b) + log1p(e) - kLn2;
+    return (t > 0.0 ? a : b) + log1p_pos_fast(e) - kLn2;
   }
 };
 
