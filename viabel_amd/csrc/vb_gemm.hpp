@@ -932,12 +932,27 @@ inline hipError_t gemm_group(const GemmOp* ops, int n, hipStream_t s) {
                           : dim3(ntn, (unsigned)((g.M + BT - 1) / BT), (unsigned)n);
   const bool ks = g.kscale != nullptr, dual = g.A2 != nullptr;
   if (ks && dual) return hipErrorInvalidValue;
-  // exact epilogue kernels: plain NN products whose ops share one listed set
+  // exact epilogue kernels: plain NN products whose ops share one listed set, and
+  // the NT Sigma = L L^T products (the step's first launch)
   int epi = kEpiAll;
-  if (!g.ta && !g.tb && !ks && !dual && gemm_epi_exact_enabled()) {
+  if (!g.ta && !ks && !dual && gemm_epi_exact_enabled()) {
     epi = epi_mask(gg.op[0]);
     for (int i = 1; i < n; ++i)
       if (epi_mask(gg.op[i]) != epi) epi = kEpiAll;
+  }
+  if (g.tb && epi != kEpiAll) {
+    switch (epi) {
+      case kEpiSym | kEpiSq:
+        hipLaunchKernelGGL((gemm_f64_kernel<false, true, false, false, kEpiSym | kEpiSq>), grid,
+                           dim3(NTH), 0, s, gg);
+        return hipGetLastError();
+      case kEpiSym | kEpiSq | kEpiQf:
+        hipLaunchKernelGGL((gemm_f64_kernel<false, true, false, false, kEpiSym | kEpiSq | kEpiQf>),
+                           grid, dim3(NTH), 0, s, gg);
+        return hipGetLastError();
+      default:
+        epi = kEpiAll;
+    }
   }
   switch (epi) {
 #define VB_EPI_CASE(M)                                                                      \
