@@ -914,6 +914,9 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
     }
   };
   const double dN = (double)N;
+  // 1 / N once per launch: the update multiplies (exact for a power-of-two N, within
+  // an ulp otherwise) instead of dividing on its serial chain
+  const double inv_dN = 1.0 / dN;
   // adagrad window sums: the copy wave adds up the older W - 1 slots of every
   // parameter while the rows run (same order, oldest first), so the update adds
   // only the newest square (the same bits as the whole loop)
@@ -1343,11 +1346,11 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
       const double sgp = s_sg[mean ? 0 : p - D];
       double gp;
       if (!a.chivi) {
-        const double cd = c / dN;
+        const double cd = c * inv_dN;
         gp = mean ? -cd : -(1.0 + sgp * cd);
       } else {
         const double Ssum = colsum(2 * DMAX);
-        gp = (mean ? a.alpha * c : a.alpha * (sgp * c + Ssum)) / dN;
+        gp = (mean ? a.alpha * c : a.alpha * (sgp * c + Ssum)) * inv_dN;
       }
       if (a.emit_grad) {
         a.grad[(long long)prob * P + p] = gp;
