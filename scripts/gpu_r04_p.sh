@@ -12,5 +12,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stage -o s
   python3 scripts/cfg5_stage_host.py > gpurun_out/prof_stage.log 2>&1
 f=$(find gpurun_out/prof_stage -name "*kernel_stats.csv" | head -1)
 [ -n "$f" ] && grep -E "sel_|gpd|lw_|logw" "$f" | cut -d, -f1-4
-LEGS=cfg5 LIBS="prev new" ROUNDS=4 bash scripts/gpu_ab_legs.sh > gpurun_out/psis_hotbin_ab.log 2>&1 || { cat gpurun_out/psis_hotbin_ab.log; tail gpurun_out/ab_legs.err; exit 1; }
-cat gpurun_out/psis_hotbin_ab.log
+LEGS=cfg5 LIBS="prev new" ROUNDS=4 bash scripts/gpu_ab_legs.sh > gpurun_out/psis_sort_barriers_ab.log 2>&1 || { cat gpurun_out/psis_sort_barriers_ab.log; tail gpurun_out/ab_legs.err; exit 1; }
+cat gpurun_out/psis_sort_barriers_ab.log
