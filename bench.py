@@ -755,11 +755,14 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     dist = None
     # one GPU per rank (LOCAL_RANK mod the visible devices, as restarts.bind_local_device);
-    # VIABEL_AMD_BENCH_BACKEND=gloo rehearses the N > 1 path on fewer GPUs than ranks
-    # (RCCL refuses two ranks on one GPU) -- the driver's runs use nccl (= RCCL)
+    # collectives over nccl (= RCCL) whenever every local rank has a GPU of its own;
+    # more local ranks than GPUs (a rehearsal of the N > 1 path on a one-GPU box,
+    # scripts/gpu_rehearse_ranks.sh) use gloo, since RCCL refuses two ranks on one GPU
     global COLL_CPU
-    backend = os.environ.get('VIABEL_AMD_BENCH_BACKEND', 'nccl')
-    local_dev = local % max(1, torch.cuda.device_count())
+    n_dev = max(1, torch.cuda.device_count())
+    local_world = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
+    backend = 'nccl' if local_world <= n_dev else 'gloo'
+    local_dev = local % n_dev
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local_dev)
@@ -768,6 +771,9 @@ def main():
         else:
             dist.init_process_group(backend)
             COLL_CPU = True
+            if rank == 0:
+                print('[bench] %d local ranks on %d GPU(s): gloo collectives (rehearsal)'
+                      % (local_world, n_dev), file=sys.stderr, flush=True)
     else:
         torch.cuda.set_device(0)
     dev = torch.device('cuda', local_dev)
@@ -853,6 +859,7 @@ def main():
             'roofline': roof,
             'valu': valu,
             'measured_peaks': measured,
+            'build_id': nat.lib().vb_build_id().decode(),
             'restart_summaries': gathered.tolist(),
         }
         if cpu:

@@ -174,6 +174,10 @@ typedef struct vb_run vb_run;
 /* ---- context --------------------------------------------------------- */
 int vb_abi_version(void);
 const char* vb_last_error(void);
+/* sha256 (first 16 hex digits) of the library's sources, in the fixed order of
+ * viabel_amd/csrc/Makefile's HASH_SRCS, fixed at build time: which sources the
+ * loaded binary was built from (measurement provenance; not part of the path). */
+const char* vb_build_id(void);
 /* `hip_stream` may be NULL (the context creates its own stream) or an
  * existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream). */
 int vb_ctx_create(int device, void* hip_stream, vb_ctx** out);

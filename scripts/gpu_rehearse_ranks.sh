@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-export VIABEL_AMD_BENCH_BACKEND=gloo
+# (bench.py picks gloo itself when local ranks outnumber the GPUs)
 for n in ${RANKS:-2 4}; do
   timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
     --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --steps 20 --warmup 5 \

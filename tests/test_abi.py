@@ -37,6 +37,28 @@ def test_library_exports_every_header_symbol():
     assert lib.vb_abi_version() == 1
 
 
+def source_hash():
+    """sha256 prefix of the library sources in Makefile HASH_SRCS order (the
+    recipe vb_build_id() was made with)."""
+    import hashlib
+    csrc = os.path.join(ROOT, 'viabel_amd', 'csrc')
+    mk = open(os.path.join(csrc, 'Makefile')).read()
+    names = re.search(r'HASH_SRCS = (.*?)\nSRC_HASH', mk, re.S).group(1).replace('\\\n', ' ').split()
+    h = hashlib.sha256()
+    for n in names:
+        h.update(open(os.path.join(csrc, n), 'rb').read())
+    return h.hexdigest()[:16]
+
+
+def test_library_was_built_from_these_sources():
+    """The loaded libviabel_amd.so carries the hash of the sources it was built
+    from (vb_build_id): it equals the hash of the tree the tests run in, so the
+    binary under test is the source under review (GPU box: the same check runs
+    as test_gpu_vb.py::test_gpu_library_was_built_from_these_sources)."""
+    from viabel_amd import _native
+    assert _native.lib().vb_build_id().decode() == source_hash()
+
+
 def test_exported_symbols_are_c_linkage():
     so = os.path.join(ROOT, 'viabel_amd', 'libviabel_amd.so')
     out = subprocess.check_output(['nm', '-D', '--defined-only', so]).decode()

@@ -311,6 +311,32 @@ def test_newton_schulz_retry_when_the_learnt_count_is_short(monkeypatch):
     _close(lam[0], ohist[-1], 1e-7)
 
 
+def test_retries_over_many_short_advances(monkeypatch):
+    """Reruns are counted per advance (vb_capi.hip vb_run_advance): a run
+    advanced one step at a time under a forced short Newton-Schulz count never
+    fails for the reruns of earlier advances, and every advance that reran leaves
+    the trajectory of the unforced run, bit for bit."""
+    vb, targets, fo, ro, vo = _mods()
+    D, N, n_iters = 64, 16, 24
+    lam0 = _lam(D, 12)
+
+    def device_run():
+        fam = vb.t_variational_family(D, 30.0, rng='philox')
+        obj = vb.black_box_chivi(2.0, fam, targets.corr_gauss(D), N)
+        run = vb.DeviceRun(obj, n_iters, lam0, learning_rate=0.02)
+        for k in range(n_iters):
+            run.advance_philox(1, 2, 5, k)
+        return run.fr_retries(), run.result()
+
+    _, (lam_p, hist_p, vals_p, _) = device_run()
+    monkeypatch.setenv('VIABEL_AMD_FR_NS_START', '3')
+    retries, (lam, hist, vals, _) = device_run()
+    assert retries > 0
+    assert np.array_equal(vals[0], vals_p[0]), np.max(np.abs(vals[0] - vals_p[0]))
+    assert np.array_equal(hist[0], hist_p[0])
+    assert np.array_equal(lam[0], lam_p[0])
+
+
 def test_ill_conditioned_sigma_trajectory():
     """Warm PCG steps stop at a relative residual of 1e-8, tightened by kappa / 2
     once the preconditioned condition number kappa = (2 + k + 1/k) / 4 (k =

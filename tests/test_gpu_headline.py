@@ -48,13 +48,12 @@ def test_config3_klvi_call_numpy_stream(N):
         _close(g, og, 1e-10)
 
 
-def test_config3_short_launches_values_in_kernel():
-    """The driver's shape (a 5-step warm-up launch, then 20-step launches): launches
-    of <= 24 steps reduce their per-step values inside sep_kernel (the last block
-    to finish sums the blocks' write-through partials; vb_capi.hip
-    sep_values_fused), longer ones in a second launch.  Launches of 5, 20 x 5, 1,
-    24 and 25 steps against the oracle on the C-oracle Philox draws: values,
-    history rows and lambda to 1e-7."""
+def test_config3_short_launches():
+    """The driver's shape (a 5-step warm-up launch, then 20-step launches; every
+    launch of sep_kernel is followed by sep_values_kernel, which reduces the
+    launch's per-step value partials).  Launches of 5, 20 x 5, 1, 24 and 25 steps
+    against the oracle on the C-oracle Philox draws: values, history rows and
+    lambda to 1e-7."""
     from viabel_amd import vb, targets
     from oracle import vb_oracle as vo, rng_oracle as ro
     N, W, LR, EPS = 128, 10, 0.01, 0.1

@@ -18,6 +18,16 @@ SMALL_TARGETS = [('isogauss', 6), ('mixture', 5), ('funnel', 10), ('eight_school
                  ('funnel', 2), ('isogauss', 1)]
 
 
+def test_gpu_library_was_built_from_these_sources():
+    """Build provenance on the GPU box: the library this process loads carries
+    the hash of the sources in the tree it runs from (vb_build_id,
+    tests/test_abi.py::source_hash), so the parity results below are those of
+    the committed sources."""
+    from tests.test_abi import source_hash
+    from viabel_amd import _native
+    assert _native.lib().vb_build_id().decode() == source_hash()
+
+
 def _mods():
     from viabel_amd import vb, targets
     from oracle import vb_oracle, rng_oracle

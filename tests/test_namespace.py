@@ -90,6 +90,24 @@ def test_flat_triang_round_trip():
     np.testing.assert_array_equal(F[:, 2], -flat)
 
 
+def test_triang_to_flat_follows_the_reference_loops():
+    """triang_to_flat on a random stack with a non-zero upper triangle (ignored)
+    against the reference's index loops restated (functions.py:126-136):
+    flat[count, d] = L[d, m, mm] for m = 0..M-1, mm = 0..m; shape [N, B]."""
+    from viabel.functions import triang_to_flat
+    rs = np.random.RandomState(3)
+    for B, M in ((1, 1), (2, 5), (7, 3)):
+        L = rs.randn(B, M, M)
+        flat = np.empty((M * (M + 1) // 2, B))
+        for d in range(B):
+            count = 0
+            for m in range(M):
+                for mm in range(m + 1):
+                    flat[count, d] = L[d, m, mm]
+                    count += 1
+        np.testing.assert_array_equal(triang_to_flat(L), flat)
+
+
 def test_compute_posterior_moments_is_the_conjugate_posterior():
     from viabel.functions import compute_posterior_moments
     rs = np.random.RandomState(3)

@@ -64,6 +64,7 @@ P = ctypes.POINTER
 _SIGNATURES = {
     'vb_abi_version': ([], ctypes.c_int),
     'vb_last_error': ([], ctypes.c_char_p),
+    'vb_build_id': ([], ctypes.c_char_p),
     'vb_ctx_create': ([ctypes.c_int, ctypes.c_void_p, P(ctypes.c_void_p)], ctypes.c_int),
     'vb_ctx_destroy': ([ctypes.c_void_p], ctypes.c_int),
     'vb_ctx_synchronize': ([ctypes.c_void_p], ctypes.c_int),

@@ -279,20 +279,6 @@ bool predraw_overlap_enabled() {
   return on;
 }
 
-// VIABEL_AMD_SEP_FUSE_VALUES=1: short column-pair chunks reduce their per-step
-// values in the kernel's last block instead of a second launch
-// (sep_values_kernel).  Measured slower, so off: the 20-step headline launch's
-// device span 81.3 -> 84 us, 5.34 -> 5.58 us/step (the blocks' write-through
-// partial stores and the last block's round trips outlast the 4.3 us launch;
-// profiles/r04/headline_fuse_values_rejected.log)
-bool sep_values_fused() {
-  static const bool on = [] {
-    const char* e = std::getenv("VIABEL_AMD_SEP_FUSE_VALUES");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 int check_ctx(vb_ctx* c) {
   if (!c) return fail(VB_EINVAL, "null vb_ctx");
   VB_HIP(hipSetDevice(c->device));
@@ -313,21 +299,14 @@ bool predraw_overlap_streams(vb_ctx* c) {
     (void)hipGetLastError();
     return false;
   }
-  // VIABEL_AMD_PREDRAW_MASK (A/B): default the block kernel on the first half of the
-  // CU ids and the pre-draw on the second; "even" = even / odd CU ids; "free" = the
-  // block kernel on an unmasked stream (config 5's fit 14.8-14.9 / 15.0-15.3 /
-  // 15.2-15.3 ms, profiles/r04/predraw_mask_ab.log)
-  const char* mode = std::getenv("VIABEL_AMD_PREDRAW_MASK");
-  const int m = (mode && mode[0] == 'e') ? 0 : (mode && mode[0] == 'f') ? 2 : 1;
-  std::vector<uint32_t> even((ncu + 31) / 32, 0u), odd((ncu + 31) / 32, 0u);
-  for (int i = 0; i < ncu; ++i) {
-    const bool second = m == 1 ? i >= ncu / 2 : (i % 2) != 0;
-    (second ? odd : even)[i / 32] |= 1u << (i % 32);
-  }
-  hipError_t e1 = m == 2 ? hipStreamCreateWithFlags(&c->blk_stream, hipStreamNonBlocking)
-                         : hipExtStreamCreateWithCUMask(&c->blk_stream, (uint32_t)even.size(), even.data());
+  // the block kernel on the first half of the CU ids, the pre-draw on the second
+  // (measured against even / odd ids and an unmasked block stream: config 5's fit
+  // 14.8-14.9 / 15.0-15.3 / 15.2-15.3 ms, profiles/r04/predraw_mask_ab.log)
+  std::vector<uint32_t> first((ncu + 31) / 32, 0u), second((ncu + 31) / 32, 0u);
+  for (int i = 0; i < ncu; ++i) (i >= ncu / 2 ? second : first)[i / 32] |= 1u << (i % 32);
+  hipError_t e1 = hipExtStreamCreateWithCUMask(&c->blk_stream, (uint32_t)first.size(), first.data());
   if (e1 != hipSuccess ||
-      hipExtStreamCreateWithCUMask(&c->pd_stream, (uint32_t)odd.size(), odd.data()) != hipSuccess) {
+      hipExtStreamCreateWithCUMask(&c->pd_stream, (uint32_t)second.size(), second.data()) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
@@ -540,6 +519,11 @@ extern "C" {
 int vb_abi_version(void) { return VB_ABI_VERSION; }
 
 const char* vb_last_error(void) { return g_err.c_str(); }
+
+#ifndef VB_SRC_HASH
+#define VB_SRC_HASH "unknown"
+#endif
+const char* vb_build_id(void) { return VB_SRC_HASH; }
 
 int vb_ctx_create(int device, void* hip_stream, vb_ctx** out) {
   if (!out) return fail(VB_EINVAL, "null output pointer");
@@ -851,7 +835,6 @@ struct vb_run {
   int n_waves = 0;
   int max_chunk = 256;
   DevBuf lam, ring, hist, values, vpart, noise, smooth;
-  DevBuf ticket;  // column-pair path: the in-kernel value combine's block counter
   DevBuf noise_lq;  // pre-drawn log q partials (block kernel, predraw)
   DevBuf noise2, noise_lq2;  // the second chunk buffer of the overlapped pre-draw
   // full-rank family / wide mean-field: one value_grad + update per step
@@ -987,13 +970,11 @@ int vb_run_create(vb_ctx* c, const vb_family* fam, const vb_target* tgt, const v
   if ((rc = r->smooth.reserve(sizeof(double) * P * n_problems)) != VB_OK) return bail(rc);
   if (sep && (rc = r->vpart.reserve(sizeof(double) * r->n_waves * r->max_chunk)) != VB_OK)
     return bail(rc);
-  if (sep && (rc = r->ticket.reserve(sizeof(unsigned))) != VB_OK) return bail(rc);
   In di;
   if ((rc = di.stage(c, 0, init, P * n_problems)) != VB_OK) return bail(rc);
   hipError_t e = hipMemcpyAsync(r->lam.p, di.d, sizeof(double) * P * n_problems,
                                 hipMemcpyDeviceToDevice, c->stream);
   if (e == hipSuccess) e = hipMemsetAsync(r->ring.p, 0, sizeof(double) * P * r->W * n_problems, c->stream);
-  if (e == hipSuccess && sep) e = hipMemsetAsync(r->ticket.p, 0, sizeof(unsigned), c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) return bail(fail(VB_EDEVICE, "run init failed: %s", hipGetErrorString(e)));
   *out = r;
@@ -1118,24 +1099,37 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
                             hipMemcpyDeviceToDevice, c->stream));
       if (int rc = vbk::fr_warm_save(W, c->stream)) return rc;
     }
-    for (bool rerun = false;; rerun = true) {
-      VB_TRY(advance_fr_steps(c, r, n_steps, noise, host, noise_base, per_step, k0, k1));
-      if (!r->fr) break;
-      VB_TRY(sync(c));
-      bool again = false;
-      if (int rc = vbk::fr_info(W, c->stream, snap ? &again : nullptr)) return rc;
-      if (!again) {
-        if (rerun) vbk::fr_retry_done(W);
-        break;
-      }
-      // fr_info raised a count (Newton-Schulz by 3 up to kFrNSMax, PCG x2 up to
-      // kFrPcgMax; past those it reports an error)
-      if (++r->fr_retries > 64) return fail(VB_EDEVICE, "full-rank advance: too many reruns");
+    // lambda and the adagrad window back to the snapshot (before a rerun, and
+    // before returning an error: a failed advance leaves the run as it was)
+    auto restore = [&]() -> int {
       VB_HIP(hipMemcpyAsync(r->lam.d(), r->backup.d(), P * sizeof(double),
                             hipMemcpyDeviceToDevice, c->stream));
       VB_HIP(hipMemcpyAsync(r->ring.d(), r->backup.d() + P, P * r->W * sizeof(double),
                             hipMemcpyDeviceToDevice, c->stream));
-      if (int rc = vbk::fr_warm_restore(W, c->stream)) return rc;
+      return vbk::fr_warm_restore(W, c->stream);
+    };
+    // reruns of THIS advance: fr_info raises a count each time (Newton-Schulz by 3
+    // up to kFrNSMax, PCG x2 up to kFrPcgMax) and reports an error past those, so
+    // the loop ends by itself; the cap is a backstop.  r->fr_retries only counts
+    // (vb_run_fr_retries).
+    int reruns = 0;
+    for (bool rerun = false;; rerun = true) {
+      int rc = advance_fr_steps(c, r, n_steps, noise, host, noise_base, per_step, k0, k1);
+      if (rc == VB_OK && r->fr) rc = sync(c);
+      bool again = false;
+      if (rc == VB_OK && r->fr) rc = vbk::fr_info(W, c->stream, snap ? &again : nullptr);
+      if (rc == VB_OK && again && ++reruns > 32)
+        rc = fail(VB_EDEVICE, "full-rank advance: too many reruns");
+      if (rc != VB_OK) {
+        if (snap) (void)restore();
+        return rc;
+      }
+      if (!again) {
+        if (rerun) vbk::fr_retry_done(W);
+        break;
+      }
+      ++r->fr_retries;
+      if (int rc2 = restore()) return rc2;
     }
   } else if (r->sep) {
     ht0.mark();
@@ -1168,26 +1162,28 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
       a.k0 = k0;
       a.k1 = k1;
       a.stream = noise->stream;
-      // short chunks: the per-step values inside the kernel (one launch per chunk)
-      a.fuse_values = (cs <= vbk::kSepFuseSteps && sep_values_fused()) ? 1 : 0;
-      a.ticket = static_cast<unsigned*>(r->ticket.p);
-      a.values = r->values.d();
-      a.c0 = sep_c0(r->fi, a.pd != 0);
       std::pair<hipEvent_t, hipEvent_t>* ev;
       HostTrace ht;
       VB_TRY(r->next_event(cs, &ev));
       ht.mark();
+      // timed runs: the pair's span from the sep kernel's start to the value
+      // kernel's end, stamped by the launches themselves (hipExtLaunchKernel)
+#ifdef VB_SEP_EVREC   // (experiment: event records around the pair)
       if (ev) VB_HIP(hipEventRecord(ev->first, c->stream));
+      VB_HIP(vbk::launch_sep(r->fi.kind, r->tgt, host, a, c->stream, nullptr));
       ht.mark();
-      VB_HIP(vbk::launch_sep(r->fi.kind, r->tgt, host, a, c->stream));
-      ht.mark();
-      if (!a.fuse_values)
-        VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, sep_c0(r->fi, a.pd != 0),
-                                      r->values.d() + a.step0, c->stream));
-      ht.mark();
+      VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, sep_c0(r->fi, a.pd != 0),
+                                    r->values.d() + a.step0, c->stream, nullptr));
       if (ev) VB_HIP(hipEventRecord(ev->second, c->stream));
       ht.mark();
-      ht.print("sep advance: next_event | record | launch_sep | launch_values | record");
+#else
+      VB_HIP(vbk::launch_sep(r->fi.kind, r->tgt, host, a, c->stream, ev ? ev->first : nullptr));
+      ht.mark();
+      VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, sep_c0(r->fi, a.pd != 0),
+                                    r->values.d() + a.step0, c->stream, ev ? ev->second : nullptr));
+      ht.mark();
+#endif
+      ht.print("sep advance: next_event | launch_sep | launch_values");
       off += cs;
     }
   } else {

@@ -27,6 +27,7 @@
 // mean_and_cov / pth_moment, off the optimisation loop.
 #include "vb_device.hpp"
 #include "vb_internal.hpp"
+#include "vb_symsum.hpp"
 
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
@@ -293,15 +294,23 @@ template <class Sched>
 __global__ __launch_bounds__(256) void fr_pack_kernel(int D, const double* GL, const double* L,
                                                       const double* scal, Sched* sc,
                                                       const double* rr_part, int n_rr,
-                                                      double* grad) {
+                                                      double* grad, double pcg_tol2 = 0.0,
+                                                      int pcg_last = -1) {
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0) {
+    __shared__ double red[16];
+    double rr = 0.0;
+    for (int k = threadIdx.x; k < n_rr; k += 256) rr += rr_part[k];
+    rr = block_sum(rr, red);
+    if (threadIdx.x == 0 && !sc->pcg_done) {
+      if (!(rr <= 1e-14 * sc->ee)) sc->status |= 2;  // relative residual above 1e-7
+      // the last launched iteration converged: no later launch tested it (the
+      // symmetric-sum loop tests R_i at the start of iteration i)
+      if (rr <= pcg_tol2 * sc->ee) sc->pcg_iter = pcg_last;
+    }
+  }
   if (idx == 0) {
     if (!sc->ns_conv && !sc->ns_fin) sc->status |= 1;
-    if (!sc->pcg_done) {
-      double rr = 0.0;
-      for (int k = 0; k < n_rr; ++k) rr += rr_part[k];
-      if (!(rr <= 1e-14 * sc->ee)) sc->status |= 2;  // relative residual above 1e-7
-    }
     if (sc->warm_step) {
       sc->hint_ns = max(sc->hint_ns, sc->ns_iter);
       sc->hint_pcg = max(sc->hint_pcg, sc->pcg_iter);
@@ -850,6 +859,8 @@ struct FrPackArgs {
   FrSched* sc;
   const double* rr_part;
   int n_rr;
+  double pcg_tol2;   // see fr_pack_kernel
+  int pcg_last;
   const double* gmu;   // mean gradient (pcg_init's colsum blocks)
   double* lam;
   double* ring;
@@ -899,14 +910,21 @@ __global__ __launch_bounds__(256) void fr_pack_update_kernel(FrPackArgs a) {
     return;
   }
   const long long p = (long long)b * 256 + threadIdx.x;
+  if (b == 0) {
+    // the last PCG residual, summed by the whole block (one thread's serial loop
+    // over the partials took ~20 us)
+    double rr = 0.0;
+    for (int k = threadIdx.x; k < a.n_rr; k += 256) rr += a.rr_part[k];
+    rr = block_sum(rr, red);
+    FrSched* sc = a.sc;
+    if (threadIdx.x == 0 && !sc->pcg_done) {
+      if (!(rr <= 1e-14 * sc->ee)) sc->status |= 2;  // relative residual above 1e-7
+      if (rr <= a.pcg_tol2 * sc->ee) sc->pcg_iter = a.pcg_last;
+    }
+  }
   if (p == 0) {
     FrSched* sc = a.sc;
     if (!sc->ns_conv && !sc->ns_fin) sc->status |= 1;
-    if (!sc->pcg_done) {
-      double rr = 0.0;
-      for (int k = 0; k < a.n_rr; ++k) rr += a.rr_part[k];
-      if (!(rr <= 1e-14 * sc->ee)) sc->status |= 2;  // relative residual above 1e-7
-    }
     if (sc->warm_step) {
       sc->hint_ns = max(sc->hint_ns, sc->ns_iter);
       sc->hint_pcg = max(sc->hint_pcg, sc->pcg_iter);
@@ -1137,6 +1155,186 @@ __global__ __launch_bounds__(256) void pcg_p_kernel(int D, int it, const double*
   }
 }
 
+// ---- PCG on symmetric-sum products (D % 64 == 0; vb_symsum.hpp) --------------
+// The same preconditioned CG as above (operator L(P) = Y P + P Y, preconditioner
+// M^-1(R) = (Z R + R Z) / 4, X_0 = 0, R_0 = Eh), with the preconditioned residual
+// carried by a recurrence instead of recomputed:
+//   A_i:  W = L(U_i);  beta = gamma_i / gamma_{i-1} (0 at i = 0);
+//         P_i = U_i + beta P_{i-1};  Q_i = W + beta Q_{i-1}  (= L(P_i));  pi_i = <P_i, Q_i>
+//   M_i:  V = M^-1(Q_i);  alpha = gamma_i / pi_i;
+//         X += alpha P_i;  R -= alpha Q_i;  U -= alpha V  (= M^-1(R));  gamma_{i+1} = <R, U>
+// Every update of launch k needs only whole entries of its own product (each block
+// owns complete entries of the symmetric result) and scalars summed from the
+// partials of launch k - 1, so the vector updates run in the products' epilogues:
+// two launches per iteration instead of two products and two update kernels.  In
+// exact arithmetic the iterates are the standard loop's.
+// Modes: 0 = M^-1(R_0) (U_0, gamma_0; block 0 stores ||E||^2), 1 = A_i, 2 = M_i.
+struct SsPcgArgs {
+  int D, mode, it;
+  const double* Mat;     // Z (modes 0, 2) or Y (mode 1)
+  const double* V;       // the product's CG operand: R (0), U (1), Q (2)
+  double *R, *U, *P, *Q, *X;
+  const double* ee_part;
+  int n_ee;
+  double* gam;           // [2][nblk]: gamma partials by iteration parity
+  double* pi;            // [nblk]
+  double* rho;           // [nblk]: ||R||^2 partials (convergence, status)
+  FrSched* sc;
+  double tol2;           // converged when ||R||^2 <= tol2 ||E||^2 (ee)
+};
+
+// per-thread share of sum(p[0 .. n)) in the fixed order of symsum::block_sum8
+__device__ __forceinline__ double part_share(const double* p, int n) {
+  double a = 0.0;
+  for (int i = threadIdx.x; i < n; i += symsum::NTH) a += p[i];
+  return a;
+}
+
+template <int KT>
+__global__ __launch_bounds__(symsum::NTH) void fr_pcg_ss_kernel(SsPcgArgs a) {
+  using namespace symsum;
+  extern __shared__ double lds[];
+  __shared__ double scr[8];
+  __shared__ int s_skip;
+  kernarg_warm(a);
+  const int D = a.D, nt = D / 32, nblk = nt * nt, t = threadIdx.x, b = blockIdx.x;
+  const int mode = a.mode, it = a.it;
+  FrSched* sc = a.sc;
+  if (mode != 0) {
+    // iterations past convergence return at once (a flag holding this launch's
+    // own tag was set by a peer block: ignored)
+    const int tag = it + 1;
+    if (t == 0) {
+      const int f = __hip_atomic_load(&sc->pcg_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_skip = (f != 0 && !(mode == 1 && f == tag)) ? 1 : 0;
+    }
+    __syncthreads();
+    if (s_skip) return;
+  }
+  const Geo g = geo(b, nt);
+  const int nown = n_own(g);
+  // everything the epilogue reads is loaded before the product, so the load
+  // latencies hide under it: the scalars' partials of the previous launches and
+  // this block's own entries of the CG vectors (only this block writes them; the
+  // product reads the whole operand, which no block of this launch writes)
+  double s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  double o0[2] = {0.0, 0.0}, o1[2] = {0.0, 0.0}, o2[2] = {0.0, 0.0}, o3[2] = {0.0, 0.0},
+         o4[2] = {0.0, 0.0};
+  long long idx[2];
+  for (int k = 0; k < 2; ++k) {
+    const int e = t + NTH * (k < nown ? k : 0), r = e >> 5, c = e & 31;
+    idx[k] = (long long)(g.r0 + r) * D + g.c0 + c;
+  }
+  if (mode == 0) {
+    if (b == 0) s1 = part_share(a.ee_part, a.n_ee);
+    for (int k = 0; k < nown; ++k) o0[k] = a.R[idx[k]];
+  } else if (mode == 1) {
+    s1 = part_share(a.gam + (it & 1) * nblk, nblk);
+    if (it >= 1) {
+      s2 = part_share(a.gam + ((it - 1) & 1) * nblk, nblk);
+      s3 = part_share(a.rho, nblk);
+    }
+    for (int k = 0; k < nown; ++k) {
+      o0[k] = a.U[idx[k]];
+      if (it >= 1) {
+        o1[k] = a.P[idx[k]];
+        o2[k] = a.Q[idx[k]];
+      }
+    }
+  } else {
+    s1 = part_share(a.gam + (it & 1) * nblk, nblk);
+    s2 = part_share(a.pi, nblk);
+    for (int k = 0; k < nown; ++k) {
+      o0[k] = a.P[idx[k]];
+      o1[k] = a.Q[idx[k]];
+      o2[k] = a.R[idx[k]];
+      o3[k] = a.U[idx[k]];
+      if (it >= 1) o4[k] = a.X[idx[k]];
+    }
+  }
+  product<KT>(a.Mat, a.V, D, g, lds);
+  if (mode == 1 && it >= 1) {
+    // A_i tests R_i (M_{i-1}'s partials) after its product: with the learnt
+    // iteration count the test usually fails, so it stays off the launch's
+    // critical path; a converged launch writes nothing.  Every block sums the
+    // same partials in the same order and decides alike.
+    const double rr = block_sum8(s3, scr);
+    if (rr <= a.tol2 * sc->ee) {
+      if (t == 0) {
+        sc->pcg_iter = it - 1;
+        __hip_atomic_store(&sc->pcg_done, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+  }
+  double* vt = lds + RED;               // the block's result entries (stride VS)
+  double* xt = vt + 32 * VS;            // mode 2: X's new entries (mirror staging)
+  const double wgt = own_weight(g);
+  double acc1 = 0.0, acc2 = 0.0;
+  if (mode == 0) {
+    const double ee = b == 0 ? block_sum8(s1, scr) : 0.0;
+    if (b == 0 && t == 0) sc->ee = ee * sc->ee_scale;
+    for (int k = 0; k < nown; ++k) {
+      const int e = t + NTH * k, r = e >> 5, c = e & 31;
+      const double u = 0.25 * vt[r * VS + c];
+      vt[r * VS + c] = u;
+      a.U[idx[k]] = u;
+      acc1 = fma(o0[k], u, acc1);
+    }
+    acc1 = block_sum8(wgt * acc1, scr);
+    if (t == 0) a.gam[b] = acc1;
+  } else if (mode == 1) {
+    const double gam = block_sum8(s1, scr);
+    const double gam0 = it >= 1 ? block_sum8(s2, scr) : 1.0;
+    const double beta = it >= 1 ? gam / gam0 : 0.0;
+    for (int k = 0; k < nown; ++k) {
+      const int e = t + NTH * k, r = e >> 5, c = e & 31;
+      const double w = vt[r * VS + c];
+      const double p = it >= 1 ? fma(beta, o1[k], o0[k]) : o0[k];
+      const double q = it >= 1 ? fma(beta, o2[k], w) : w;
+      vt[r * VS + c] = q;
+      a.P[idx[k]] = p;
+      a.Q[idx[k]] = q;
+      acc1 = fma(p, q, acc1);
+    }
+    acc1 = block_sum8(wgt * acc1, scr);   // (its barriers also complete vt)
+    if (t == 0) a.pi[b] = acc1;
+  } else {
+    const double gam = block_sum8(s1, scr);
+    const double alpha = gam / block_sum8(s2, scr);
+    for (int k = 0; k < nown; ++k) {
+      const int e = t + NTH * k, r = e >> 5, c = e & 31;
+      const double v = 0.25 * vt[r * VS + c];
+      const double x = it >= 1 ? fma(alpha, o0[k], o4[k]) : alpha * o0[k];
+      const double rn = fma(-alpha, o1[k], o2[k]), un = fma(-alpha, v, o3[k]);
+      vt[r * VS + c] = un;
+      xt[r * VS + c] = x;
+      a.X[idx[k]] = x;
+      a.R[idx[k]] = rn;
+      a.U[idx[k]] = un;
+      acc1 = fma(rn, un, acc1);
+      acc2 = fma(rn, rn, acc2);
+    }
+    acc1 = block_sum8(wgt * acc1, scr);
+    acc2 = block_sum8(wgt * acc2, scr);
+    if (t == 0) {
+      a.gam[((it + 1) & 1) * nblk + b] = acc1;
+      a.rho[b] = acc2;
+    }
+  }
+  // mirror entries of the operands of later products (U, Q) and of X: thread t
+  // -> column c, row r of the transposed half (block_sum8's barriers ordered the
+  // staged entries above)
+  if (!g.diag) {
+    const int c = t >> 4, r = t & 15;
+    const long long m = (long long)(g.c0 + c) * D + g.r0 + r;
+    const double v = vt[r * VS + c];
+    if (mode == 0 || mode == 2) a.U[m] = v;
+    if (mode == 1) a.Q[m] = v;
+    if (mode == 2) a.X[m] = xt[r * VS + c];
+  }
+}
+
 }  // namespace
 
 // ---- workspace ---------------------------------------------------------------
@@ -1180,6 +1378,8 @@ struct FrWork {
   int retry_pcg = 0;              // PCG floor after a call / advance ran again
   const void* retry_owner = nullptr;  // the run the floors belong to
   int kpcg_max_seen = 0;          // most PCG iterations launched since the last fr_info
+  int pcg_last = 0;               // the last PCG call: index of its last launched iteration
+  double pcg_tol2 = 1e-18;        // and its convergence bar (||R||^2 / ||E||^2)
   bool eig_pending = false;       // a dsyevd ran since the last fr_info
   bool sqrt_pending = false;      // a Newton-Schulz / PCG status to read at fr_info
   bool last_hz = false;           // the last root's schedule had a Z power vector (uZ valid)
@@ -1219,6 +1419,16 @@ FrWork* fr_work_create() { return new (std::nothrow) FrWork(); }
 void fr_work_destroy(FrWork* w) { delete w; }
 
 namespace {
+
+// VIABEL_AMD_FR_PCG_SS=0: the PCG runs its products and vector updates as separate
+// launches (pcg_xr / pcg_p) even where the symmetric-sum loop applies (A/B switch)
+bool pcg_ss_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("VIABEL_AMD_FR_PCG_SS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 // VIABEL_AMD_FR_SCHED_FUSE=0: the schedule kernel runs on its own (A/B switch)
 bool sched_fused() {
@@ -1413,12 +1623,8 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
   // sets the sticky status and, inside a run's advance, makes the advance run
   // again with a larger count -- vb_run_advance keeps a snapshot), others at
   // least 12 (l_0 = 0.05 needs ~9 at rounding level)
-  static const int spare = [] {   // VIABEL_AMD_FR_NS_SPARE: spare warm iterations (A/B)
-    const char* e = std::getenv("VIABEL_AMD_FR_NS_SPARE");
-    return e ? std::max(0, std::atoi(e)) : 0;
-  }();
   const int kmax =
-      std::min(warm ? std::max({W->ns_kmax + spare, W->retry_kmax, 3})
+      std::min(warm ? std::max({W->ns_kmax, W->retry_kmax, 3})
                     : std::max({W->ns_kmax + 1, 12, W->retry_kmax}),
                kFrNSMax);
   W->last_warm = warm;
@@ -1525,24 +1731,79 @@ int fr_pcg(FrWork* W, int D, hipStream_t st, int N = 0, const double* rw = nullp
   hipLaunchKernelGGL(pcg_init_kernel, dim3(nt, nt + (n_cs ? 1 : 0)), dim3(256), 0, st, D,
                      W->GS.d(), sc, W->Eh.d(), W->R.d(), W->Xs.d(), W->ee_part.d(), n_cs, N, rw,
                      Gm, gmu);
+  // warm roots launch the learnt count (fr_info), others at least 16; a rerun
+  // after a residual above the status bar launches at least its floor
+  const int kpcg = std::min(kFrPcgMax, std::max(W->last_warm ? std::max(W->pcg_kmax, 3)
+                                                             : std::max(W->pcg_kmax, 16),
+                                                W->retry_pcg));
+  W->kpcg_max_seen = std::max(W->kpcg_max_seen, kpcg);
+  // converged when ||R|| <= tol ||E||: X then carries at most the preconditioned
+  // condition number (< 1.2 at config 4) x tol of relative error.  tol = 1e-9 for
+  // cold roots (single value-and-gradient calls), 1e-8 for the warm steps of an
+  // optimisation run (one CG iteration fewer at config 4; still three orders
+  // inside the 1e-5 parity bar of north_star, and far below the step's Monte
+  // Carlo noise); the sticky status flags residuals above 1e-7 (a learnt count
+  // one short)
+  const double tol2 = W->last_warm ? 1e-16 : 1e-18;
+  W->pcg_last = kpcg - 1;
+  W->pcg_tol2 = tol2;
+  if (symsum::usable(D, W->Zf, W->R.d()) && symsum::usable(D, W->Yf, W->Xs.d()) &&
+      pcg_ss_enabled()) {
+    // symmetric-sum products with the updates in their epilogues (fr_pcg_ss_kernel)
+    SsPcgArgs a{};
+    a.D = D;
+    a.R = W->R.d();
+    a.U = W->C2.d();
+    a.P = W->P.d();
+    a.Q = W->C1.d();
+    a.X = W->Xs.d();
+    a.ee_part = W->ee_part.d();
+    a.n_ee = nblk;
+    a.gam = W->rz_part.d();
+    a.pi = W->pq_part.d();
+    a.rho = W->rr_part.d();
+    a.sc = sc;
+    a.tol2 = tol2;
+    const dim3 grid((unsigned)((D / 32) * (D / 32)));
+    auto launch = [&]() {
+      if (symsum::kt_for(D) == 128)
+        hipLaunchKernelGGL(fr_pcg_ss_kernel<128>, grid, dim3(symsum::NTH), symsum::Cfg<128>::LDS_BYTES,
+                           st, a);
+      else
+        hipLaunchKernelGGL(fr_pcg_ss_kernel<64>, grid, dim3(symsum::NTH), symsum::Cfg<64>::LDS_BYTES,
+                           st, a);
+    };
+    a.mode = 0;
+    a.it = 0;
+    a.Mat = W->Zf;
+    a.V = a.R;
+    launch();
+    for (int it = 0; it < kpcg; ++it) {
+      a.it = it;
+      a.mode = 1;
+      a.Mat = W->Yf;
+      a.V = a.U;
+      launch();
+      a.mode = 2;
+      a.Mat = W->Zf;
+      a.V = a.Q;
+      launch();
+    }
+    FR_HIP(hipGetLastError());
+    return 0;
+  }
   // P_0 = M^-1(R_0) from C2 = Z R_0, <R_0, Z R_0> in the epilogue
   auto zr = [&](int it) {
     GemmOp g = mm(D, D, D, W->Zf, false, W->R.d(), false, W->C2.d());
     g.dot_with = W->R.d();
     g.dot_part = W->rz_part.d();
     g.skip_flag = &sc->pcg_done;
-    // converged when ||R|| <= tol ||E||: X then carries at most the preconditioned
-    // condition number (< 1.2 at config 4) x tol of relative error.  tol = 1e-9 for
-    // cold roots (single value-and-gradient calls), 1e-8 for the warm steps of an
-    // optimisation run (one CG iteration fewer at config 4; still three orders
-    // inside the 1e-5 parity bar of north_star, and far below the step's Monte
-    // Carlo noise); the sticky status flags residuals above 1e-7 (a learnt count
-    // one short)
+    // (the tolerance: see above)
     if (it >= 0) {
       g.conv_part = W->rr_part.d();
       g.conv_n = nblk;
       g.conv_ref_dev = &sc->ee;
-      g.conv_tol2 = W->last_warm ? 1e-16 : 1e-18;
+      g.conv_tol2 = tol2;
       g.conv_iter_out = &sc->pcg_iter;
       g.conv_iter = it;
       g.skip_tag = it + 1;
@@ -1552,12 +1813,6 @@ int fr_pcg(FrWork* W, int D, hipStream_t st, int N = 0, const double* rw = nullp
   FR_HIP(gemm(zr(-1), st));
   hipLaunchKernelGGL(pcg_p_kernel, tg, dim3(256), 0, st, D, -1, W->C2.d(), W->rz_part.d(),
                      4 * nblk, W->ee_part.d(), nblk, sc, W->P.d());
-  // warm roots launch the learnt count (fr_info), others at least 16; a rerun
-  // after a residual above the status bar launches at least its floor
-  const int kpcg = std::min(kFrPcgMax, std::max(W->last_warm ? std::max(W->pcg_kmax, 3)
-                                                             : std::max(W->pcg_kmax, 16),
-                                                W->retry_pcg));
-  W->kpcg_max_seen = std::max(W->kpcg_max_seen, kpcg);
   for (int it = 0; it < kpcg; ++it) {
     GemmOp g = mm(D, D, D, W->Yf, false, W->P.d(), false, W->C1.d());
     g.dot_with = W->P.d();
@@ -1705,7 +1960,8 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
   FrSched* sc = static_cast<FrSched*>(W->sched.p);
   if (!fused) {
     hipLaunchKernelGGL(fr_pack_kernel, dim3(blocks((long long)D * D)), dim3(256), 0, st, D, W->H.d(),
-                       W->L.d(), W->scal.d(), sc, W->rr_part.d(), nt * nt, grad);
+                       W->L.d(), W->scal.d(), sc, W->rr_part.d(), nt * nt, grad, W->pcg_tol2,
+                       W->pcg_last);
     FR_HIP(hipGetLastError());
     return 0;
   }
@@ -1723,6 +1979,8 @@ int fr_value_grad(FrWork* W, const FrSpec& f, const double* lam, const double* h
   a.sc = sc;
   a.rr_part = W->rr_part.d();
   a.n_rr = nt * nt;
+  a.pcg_tol2 = W->pcg_tol2;
+  a.pcg_last = W->pcg_last;
   a.gmu = grad;
   a.lam = const_cast<double*>(lam);
   a.ring = up->ring;

@@ -42,17 +42,7 @@ struct SepArgs {
   const double* noise;    // host noise [n_steps][N][D] or null
   uint32_t k0, k1, stream;
   int pairs2, blocks2, blocks1;  // filled by the launcher (2-pair / 1-pair split)
-  // in-kernel per-step values (n_steps <= kSepFuseSteps): blocks sum their pairs'
-  // partials in LDS, store one partial per (step, block) into vpart with
-  // write-through stores, and the last block to finish (ticket) sums them in a
-  // fixed order into values[step0 .. step0 + n_steps) = -(c0 + sum); else
-  // launch_sep_values does it (a second launch)
-  int fuse_values;
-  unsigned* ticket;       // zero between launches (the last block resets it)
-  double* values;
-  double c0;
 };
-constexpr int kSepFuseSteps = 24;
 
 // Arguments of the block-per-problem kernel (any target, D <= kBlockDMax).
 struct BlockArgs {
@@ -80,7 +70,9 @@ struct BlockArgs {
 };
 
 // family kind 0 = mf gaussian, 1 = mf t; target kind per vb_target_kind.
-hipError_t launch_sep(int fam, int tgt, bool host_noise, const SepArgs& a, hipStream_t s);
+// start (optional): an event stamped at the kernel's start (timed runs)
+hipError_t launch_sep(int fam, int tgt, bool host_noise, const SepArgs& a, hipStream_t s,
+                      hipEvent_t start = nullptr);
 // block step skeleton without draws / target (vb_block_floor)
 hipError_t launch_block_floor(int D, int N, bool host_layout, bool chivi, int n_steps, int nprob,
                               double* out, hipStream_t s, int pf = 0);
@@ -99,8 +91,9 @@ hipError_t launch_block_predraw(int fam, int D, int N, int n_steps, int n_proble
                                 double t_const, double* noise, double* lq, hipStream_t s);
 
 // values[i] = -(c0 + sum_w vpart[s][w]) for i = step0 + s
+// stop (optional): an event stamped at the kernel's end (timed runs)
 hipError_t launch_sep_values(const double* vpart, int n_steps, int n_waves, double c0,
-                             double* values_at_step0, hipStream_t s);
+                             double* values_at_step0, hipStream_t s, hipEvent_t stop = nullptr);
 // out[p] = mean over rows of hist [rows][P]   (per problem block of rows)
 hipError_t launch_row_mean(const double* hist, long long rows, long long P, long long n_problems,
                            double* out, hipStream_t s);

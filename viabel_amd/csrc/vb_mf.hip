@@ -21,6 +21,8 @@
 #include "vb_device.hpp"
 #include "vb_internal.hpp"
 
+#include <hip/hip_ext.h>
+
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -165,7 +167,7 @@ __device__ unsigned long long g_sep_clk[kTsWaves][16];  // s_memtime (core clock
 template <class TGT, bool TFAM, bool HOST, int PPW, bool REGRING>
 __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, int wave,
                                          const double2* sct, const double2* ltab,
-                                         unsigned long long t_entry = 0, double* s_vp = nullptr) {
+                                         unsigned long long t_entry = 0) {
   constexpr int LPP = 64 / PPW;       // lanes per column pair
   constexpr int SL = LPP / 4;         // slot lanes per parameter
 #ifdef VB_SEP_PROF
@@ -298,10 +300,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
     if ((s & 3) == 3 || s + 1 == a.n_steps) {
       const double tot = reduce4<PPW>(lane, v3, v2, v1, v0);  // owner q: step s - 3 + q
       const int st = s - 3 + own;
-      if (rep && live && st >= (s & ~3)) {
-        if (s_vp) s_vp[st * 16 + (threadIdx.x >> 6) * PPW + grp] = tot;   // block-local pair
-        else a.vpart[(long long)st * a.n_waves + w] = tot;
-      }
+      if (rep && live && st >= (s & ~3)) a.vpart[(long long)st * a.n_waves + w] = tot;
     }
 
     if (a.emit_grad) {
@@ -415,75 +414,18 @@ void sep_kernel(SepArgs a) {
   }
   const int wid = threadIdx.x >> 6;
   double* ring = REGRING ? nullptr : &s_ring[REGRING ? 0 : wid][0];
-  // per-step value partials of the block's (up to 16) column pairs (fuse_values)
-  __shared__ double s_vp[kSepFuseSteps * 16];
-  __shared__ int s_last;
-  const bool fuse = a.fuse_values != 0;
-  if (fuse) {
-    for (int i = threadIdx.x; i < kSepFuseSteps * 16; i += blockDim.x) s_vp[i] = 0.0;
-    __syncthreads();
-  }
   if ((int)blockIdx.x < a.blocks2) {
     const int wave = blockIdx.x * 4 + wid;
+#ifdef VB_SEP_PRIO   // (experiment: the multi-pair waves, the critical path, first)
+    __builtin_amdgcn_s_setprio(VB_SEP_PRIO);
+#endif
     if (wave * PPW_BIG < a.pairs2)
-      sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave, s_sct, s_lt, t_entry,
-                                                  fuse ? s_vp : nullptr);
+      sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave, s_sct, s_lt, t_entry);
   } else {
     const int pair = a.pairs2 + (blockIdx.x - a.blocks2) * 4 + wid;
     if (pair < a.n_pairs)
-      sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair, s_sct, s_lt, t_entry,
-                                            fuse ? s_vp : nullptr);
+      sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair, s_sct, s_lt, t_entry);
   }
-  if (!fuse) return;
-  // the block's partial of every step (its pairs in order), write-through so the
-  // last block sees it from any XCD; then one ticket per block
-  __syncthreads();
-  const int t = threadIdx.x, ns = a.n_steps, nb = (int)gridDim.x;
-  if (t < ns) {
-    double v = 0.0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) v += s_vp[t * 16 + k];
-    __hip_atomic_store(a.vpart + (long long)t * nb + blockIdx.x, v, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    const unsigned old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == (unsigned)(nb - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  // last block: values[step] = -(c0 + sum over blocks in order); thread t reads
-  // blocks t, t + 256, ... of every step (write-through loads, all of a round
-  // in flight at once), a fixed-order tree over the lanes, then over the waves
-  __shared__ double s_red[kSepFuseSteps * 4];
-  double acc[kSepFuseSteps];
-#pragma unroll
-  for (int st = 0; st < kSepFuseSteps; ++st) acc[st] = 0.0;
-  for (int b = t; b < nb; b += 256) {
-    double v[kSepFuseSteps];
-#pragma unroll
-    for (int st = 0; st < kSepFuseSteps; ++st)
-      v[st] = st < ns ? __hip_atomic_load(a.vpart + (long long)st * nb + b, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT)
-                      : 0.0;
-#pragma unroll
-    for (int st = 0; st < kSepFuseSteps; ++st) acc[st] += v[st];
-  }
-#pragma unroll
-  for (int st = 0; st < kSepFuseSteps; ++st) {
-    if (st < ns) {
-      const double v = wave_sum_dpp(acc[st]);
-      if ((t & 63) == 0) s_red[st * 4 + (t >> 6)] = v;
-    }
-  }
-  __syncthreads();
-  if (t < ns) {
-    const double v = (s_red[t * 4] + s_red[t * 4 + 1]) + (s_red[t * 4 + 2] + s_red[t * 4 + 3]);
-    a.values[a.step0 + t] = -(a.c0 + v);
-  }
-  if (t == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // values[i] = -(c0 + sum_w vpart[s][w]), fixed-order tree reduction.  One
@@ -2267,38 +2209,43 @@ static int sep_split(SepArgs& a, int& big) {
   return big;
 }
 
+// (hipExtLaunchKernel: the optional start event is stamped at the kernel's own
+// start, one host call instead of an event record plus a launch)
 template <class TGT, bool TFAM, bool HOST, bool REG>
-static void sep_launch_ppw(int big, const SepArgs& a, hipStream_t s) {
+static void sep_launch_ppw(int big, const SepArgs& a, hipStream_t s, hipEvent_t start) {
   const dim3 grid(a.blocks2 + a.blocks1), block(256);
   if (big == 4)
-    hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 4, REG>), grid, block, 0, s, a);
+    hipExtLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 4, REG>), grid, block, 0, s, start, nullptr, 0,
+                          a);
   else
-    hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 2, REG>), grid, block, 0, s, a);
+    hipExtLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 2, REG>), grid, block, 0, s, start, nullptr, 0,
+                          a);
 }
 
 template <class TGT>
-static hipError_t sep_dispatch(int fam, bool host, SepArgs a, hipStream_t s) {
+static hipError_t sep_dispatch(int fam, bool host, SepArgs a, hipStream_t s, hipEvent_t start) {
   int big;
   sep_split(a, big);
   const bool reg = a.W <= 16 || a.emit_grad;
   if (host) {
     // host noise holds standardized draws for either family
-    if (reg) sep_launch_ppw<TGT, false, true, true>(big, a, s);
-    else sep_launch_ppw<TGT, false, true, false>(big, a, s);
+    if (reg) sep_launch_ppw<TGT, false, true, true>(big, a, s, start);
+    else sep_launch_ppw<TGT, false, true, false>(big, a, s, start);
   } else if (fam == 1) {
-    if (reg) sep_launch_ppw<TGT, true, false, true>(big, a, s);
-    else sep_launch_ppw<TGT, true, false, false>(big, a, s);
+    if (reg) sep_launch_ppw<TGT, true, false, true>(big, a, s, start);
+    else sep_launch_ppw<TGT, true, false, false>(big, a, s, start);
   } else {
-    if (reg) sep_launch_ppw<TGT, false, false, true>(big, a, s);
-    else sep_launch_ppw<TGT, false, false, false>(big, a, s);
+    if (reg) sep_launch_ppw<TGT, false, false, true>(big, a, s, start);
+    else sep_launch_ppw<TGT, false, false, false>(big, a, s, start);
   }
   return hipGetLastError();
 }
 
-hipError_t launch_sep(int fam, int tgt, bool host, const SepArgs& a, hipStream_t s) {
+hipError_t launch_sep(int fam, int tgt, bool host, const SepArgs& a, hipStream_t s,
+                      hipEvent_t start) {
   switch (tgt) {
-    case 0: return sep_dispatch<IsoGauss>(fam, host, a, s);
-    case 1: return sep_dispatch<Mixture>(fam, host, a, s);
+    case 0: return sep_dispatch<IsoGauss>(fam, host, a, s, start);
+    case 1: return sep_dispatch<Mixture>(fam, host, a, s, start);
     default: return hipErrorInvalidValue;
   }
 }
@@ -2398,9 +2345,9 @@ extern "C" int vb_debug_sep_ts(unsigned long long* out, int n_waves) {
 #endif
 
 hipError_t launch_sep_values(const double* vpart, int n_steps, int n_waves, double c0,
-                             double* values, hipStream_t s) {
-  hipLaunchKernelGGL(sep_values_kernel, dim3(n_steps), dim3(kValThreads), 0, s, vpart, n_waves,
-                     c0, values);
+                             double* values, hipStream_t s, hipEvent_t stop) {
+  hipExtLaunchKernelGGL(sep_values_kernel, dim3(n_steps), dim3(kValThreads), 0, s, nullptr, stop, 0,
+                        vpart, n_waves, c0, values);
   return hipGetLastError();
 }
 

@@ -23,14 +23,20 @@
 // sorted candidates.  3 passes over the column instead of 11; the same bits.
 //   5. GPD fit: one block per quadrature point b_j, then one combining block
 //   6. smoothing scatter + clamp, 7. log-sum-exp renormalisation.
-// All state between launches stays on the device (no host round trips), so a
-// column is one stream-ordered chain of small launches.
+// All state between launches stays on the device, so a column is one
+// stream-ordered chain of small launches -- except for one host round trip on
+// the fast path: after the two histogram passes the host reads the per-column
+// "candidates fit" flags (into a pinned buffer, one stream wait) and launches
+// either the candidate sort or the radix path.  Keeping both paths' launches
+// with device-side early exits instead would add ~20 empty launches (~40 us) to
+// every call; the round trip costs one wait (~10 us).  (So psis_columns cannot
+// be captured into a hipGraph.)
 #include "vb_device.hpp"
 #include "vb_internal.hpp"
 
 #include <algorithm>
 #include <cstdlib>
-#include <vector>
+
 
 #include <hipcub/hipcub.hpp>
 
@@ -1036,11 +1042,22 @@ hipError_t psis_columns(const double* lw, double* out, long long n, int m, long 
     hipLaunchKernelGGL(sel_hist2_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.ps, S.hist,
                        sb);
     hipLaunchKernelGGL(sel_pick_kernel, dim3(1, m), dim3(256), 0, s, S.hist, S.ps, 2, flag_dev, sb);
-    std::vector<unsigned> fl((size_t)m, 0u);
-    hipError_t e = hipMemcpyAsync(fl.data(), flag_dev, sizeof(unsigned) * m, hipMemcpyDeviceToHost, s);
+    // the flags land in a pinned buffer of the calling thread (grown on demand,
+    // kept for the life of the thread: released by the driver at process exit)
+    static thread_local unsigned* fl = nullptr;
+    static thread_local int fl_cap = 0;
+    if (m > fl_cap) {
+      if (fl) (void)hipHostFree(fl);
+      fl = nullptr;
+      fl_cap = 0;
+      const hipError_t ea = hipHostMalloc(reinterpret_cast<void**>(&fl), sizeof(unsigned) * m);
+      if (ea != hipSuccess) return ea;
+      fl_cap = m;
+    }
+    hipError_t e = hipMemcpyAsync(fl, flag_dev, sizeof(unsigned) * m, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
-    for (unsigned f : fl) fast = fast && f == 1u;
+    for (int c = 0; c < m; ++c) fast = fast && fl[c] == 1u;
   } else {
     hipLaunchKernelGGL(col_max_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.part, sb);
     hipLaunchKernelGGL(max_final_kernel, dim3(1, m), dim3(256), 0, s, S.part, g, &S.ps->mx, sb);

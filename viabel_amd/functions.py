@@ -127,7 +127,12 @@ def flat_to_triang(flat_mat):
 
 
 def triang_to_flat(L):
-    """[B, M, M] stack of lower triangles -> [M(M+1)/2, B] (functions.py:126-136)."""
+    """[B, M, M] stack of lower triangles -> [M(M+1)/2, B] (functions.py:126-136):
+    column d holds L[d]'s lower triangle in row-major order, (m, 0..m) for m =
+    0..M-1.  Not differentiable: the reference declares it an autograd
+    @primitive with flat_to_triang as its VJP (functions.py:120-125); autograd
+    is not part of this implementation, so code that differentiates through it
+    must apply that VJP itself."""
     L = np.asarray(L)
     B, _, M = L.shape
     rows, cols = np.tril_indices(M)
