@@ -369,13 +369,23 @@ def measure_peaks():
     return out
 
 
+# the HBM copy rate MI355X_MICROARCH.md measured (float4 copy); the probe's best copy
+# form reaches ~5.7 TB/s on the box (profiles/r05/hbm_probe2.log), so HBM rooflines
+# carry the fraction against this figure too
+GUIDE_HBM_COPY_GBS = 6290.0
+
+
 def add_measured(roof, measured, key):
-    """frac against the measured peak beside the spec one."""
+    """frac against the measured peak beside the spec one (and, for HBM, against the
+    guide's measured copy rate)."""
     m = measured.get(key) if measured else None
     if roof and m and roof.get('achieved'):
         roof['measured_peak'] = m
         roof['measured_peak_source'] = key
         roof['frac_of_measured_peak'] = roof['achieved'] / m
+    if roof and roof.get('achieved') and key == 'hbm_copy':
+        roof['guide_copy_peak'] = GUIDE_HBM_COPY_GBS
+        roof['frac_of_guide_copy_peak'] = roof['achieved'] / GUIDE_HBM_COPY_GBS
 
 
 def _sync():

@@ -1166,24 +1166,17 @@ int vb_run_advance(vb_run* r, int64_t n_steps, const vb_noise* noise) {
       HostTrace ht;
       VB_TRY(r->next_event(cs, &ev));
       ht.mark();
-      // timed runs: the pair's span from the sep kernel's start to the value
-      // kernel's end, stamped by the launches themselves (hipExtLaunchKernel)
-#ifdef VB_SEP_EVREC   // (experiment: event records around the pair)
+      // timed runs: the pair bracketed by event records (hipExtLaunchKernel's own
+      // start / stop stamps instead measured ~0.2 us/step slower on the host path,
+      // interleaved, profiles/r05/headline_ab_c.log)
       if (ev) VB_HIP(hipEventRecord(ev->first, c->stream));
-      VB_HIP(vbk::launch_sep(r->fi.kind, r->tgt, host, a, c->stream, nullptr));
+      VB_HIP(vbk::launch_sep(r->fi.kind, r->tgt, host, a, c->stream));
       ht.mark();
       VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, sep_c0(r->fi, a.pd != 0),
-                                    r->values.d() + a.step0, c->stream, nullptr));
+                                    r->values.d() + a.step0, c->stream));
       if (ev) VB_HIP(hipEventRecord(ev->second, c->stream));
       ht.mark();
-#else
-      VB_HIP(vbk::launch_sep(r->fi.kind, r->tgt, host, a, c->stream, ev ? ev->first : nullptr));
-      ht.mark();
-      VB_HIP(vbk::launch_sep_values(a.vpart, cs, a.n_waves, sep_c0(r->fi, a.pd != 0),
-                                    r->values.d() + a.step0, c->stream, ev ? ev->second : nullptr));
-      ht.mark();
-#endif
-      ht.print("sep advance: next_event | launch_sep | launch_values");
+      ht.print("sep advance: next_event | record + launch_sep | launch_values + record");
       off += cs;
     }
   } else {

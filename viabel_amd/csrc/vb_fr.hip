@@ -1183,83 +1183,88 @@ struct SsPcgArgs {
   double tol2;           // converged when ||R||^2 <= tol2 ||E||^2 (ee)
 };
 
-// per-thread share of sum(p[0 .. n)) in the fixed order of symsum::block_sum8
-__device__ __forceinline__ double part_share(const double* p, int n) {
-  double a = 0.0;
-  for (int i = threadIdx.x; i < n; i += symsum::NTH) a += p[i];
-  return a;
-}
+// Partials of earlier launches, loaded before a product and summed after it: the
+// first two per-thread values are plain loads at clamped indices, their validity
+// applied at the sum (a select or a loop around a load made the compiler wait for
+// it at once, before the product); partials past 2 NTH (D > 724) load at the sum.
+struct PartLoad {
+  double v0, v1;
+  __device__ __forceinline__ void load(const double* p, int n) {
+    const int t = threadIdx.x;
+    v0 = p[t < n ? t : 0];
+    v1 = p[t + symsum::NTH < n ? t + symsum::NTH : 0];
+  }
+  // this thread's share of sum(p[0 .. n)) (block_sum8 then gives the fixed-order total)
+  __device__ __forceinline__ double share(const double* p, int n) const {
+    const int t = threadIdx.x;
+    double a = (t < n ? v0 : 0.0) + (t + symsum::NTH < n ? v1 : 0.0);
+    for (int i = t + 2 * symsum::NTH; i < n; i += symsum::NTH) a += p[i];
+    return a;
+  }
+};
 
 template <int KT>
 __global__ __launch_bounds__(symsum::NTH) void fr_pcg_ss_kernel(SsPcgArgs a) {
   using namespace symsum;
   extern __shared__ double lds[];
-  __shared__ double scr[8];
-  __shared__ int s_skip;
+  __shared__ double scr[24];
   kernarg_warm(a);
   const int D = a.D, nt = D / 32, nblk = nt * nt, t = threadIdx.x, b = blockIdx.x;
   const int mode = a.mode, it = a.it;
   FrSched* sc = a.sc;
-  if (mode != 0) {
-    // iterations past convergence return at once (a flag holding this launch's
-    // own tag was set by a peer block: ignored)
-    const int tag = it + 1;
-    if (t == 0) {
-      const int f = __hip_atomic_load(&sc->pcg_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_skip = (f != 0 && !(mode == 1 && f == tag)) ? 1 : 0;
-    }
-    __syncthreads();
-    if (s_skip) return;
-  }
+  // Everything before the product's first wait is issued at once: the skip flag,
+  // the scalars' partials of the previous launches, this block's own entries of the
+  // CG vectors (only this block writes them; the product reads the whole operand,
+  // which no block of this launch writes) and the product's first stage.  All
+  // straight-line loads at clamped indices (entry 1 of a half block re-reads entry
+  // 0; sources a mode does not use read another vector), so no wait precedes it.
+  // Iterations past convergence then return (every wave reads the flag itself; a
+  // flag holding this launch's own tag was set by a peer block and is ignored).
+  // (a per-lane load: the compiler moves a uniform one to a scalar register, and
+  // waits for it, right where it is loaded)
+  int lane0;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(lane0));
+  const int fv = __hip_atomic_load(&sc->pcg_done + lane0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const Geo g = geo(b, nt);
   const int nown = n_own(g);
-  // everything the epilogue reads is loaded before the product, so the load
-  // latencies hide under it: the scalars' partials of the previous launches and
-  // this block's own entries of the CG vectors (only this block writes them; the
-  // product reads the whole operand, which no block of this launch writes)
-  double s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  double o0[2] = {0.0, 0.0}, o1[2] = {0.0, 0.0}, o2[2] = {0.0, 0.0}, o3[2] = {0.0, 0.0},
-         o4[2] = {0.0, 0.0};
   long long idx[2];
+#pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int e = t + NTH * (k < nown ? k : 0), r = e >> 5, c = e & 31;
     idx[k] = (long long)(g.r0 + r) * D + g.c0 + c;
   }
-  if (mode == 0) {
-    if (b == 0) s1 = part_share(a.ee_part, a.n_ee);
-    for (int k = 0; k < nown; ++k) o0[k] = a.R[idx[k]];
-  } else if (mode == 1) {
-    s1 = part_share(a.gam + (it & 1) * nblk, nblk);
-    if (it >= 1) {
-      s2 = part_share(a.gam + ((it - 1) & 1) * nblk, nblk);
-      s3 = part_share(a.rho, nblk);
-    }
-    for (int k = 0; k < nown; ++k) {
-      o0[k] = a.U[idx[k]];
-      if (it >= 1) {
-        o1[k] = a.P[idx[k]];
-        o2[k] = a.Q[idx[k]];
-      }
-    }
-  } else {
-    s1 = part_share(a.gam + (it & 1) * nblk, nblk);
-    s2 = part_share(a.pi, nblk);
-    for (int k = 0; k < nown; ++k) {
-      o0[k] = a.P[idx[k]];
-      o1[k] = a.Q[idx[k]];
-      o2[k] = a.R[idx[k]];
-      o3[k] = a.U[idx[k]];
-      if (it >= 1) o4[k] = a.X[idx[k]];
-    }
-  }
-  product<KT>(a.Mat, a.V, D, g, lds);
+  const double* pa1 = mode == 0 ? a.ee_part : a.gam + (it & 1) * nblk;
+  const double* pa2 = mode == 1 ? a.gam + ((it > 0 ? it - 1 : 0) & 1) * nblk : a.pi;
+  const int n1 = mode == 0 ? (b == 0 ? a.n_ee : 0) : nblk;
+  const int n2 = (mode == 1 && it >= 1) || mode == 2 ? nblk : 0;
+  const int n3 = mode == 1 && it >= 1 ? nblk : 0;
+  PartLoad l1, l2, l3;
+  l1.load(pa1, n1);
+  l2.load(pa2, n2);
+  l3.load(a.rho, n3);
+  // own entries o[j]: mode 0 R; mode 1 U, P, Q (it >= 1); mode 2 P, Q, R, U, X (it >= 1)
+  const double* src[5] = {mode == 0 ? a.R : (mode == 1 ? a.U : a.P), mode == 1 ? a.P : a.Q,
+                          mode == 1 ? a.Q : a.R, a.U, a.X};
+  double o[5][2];
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) o[j][k] = src[j][idx[k]];
+  const bool go = product<KT>(a.Mat, a.V, D, g, lds, [&]() {
+    const int f = mode != 0 ? __builtin_amdgcn_readfirstlane(fv) : 0;
+    return !(f != 0 && !(mode == 1 && f == it + 1));
+  });
+  if (!go) return;
+  // the scalars: one block reduction of every partial share (gamma_i, gamma_{i-1}
+  // or pi_i, ||R_i||^2)
+  double sc3[3] = {l1.share(pa1, n1), l2.share(pa2, n2), l3.share(a.rho, n3)};
+  if (mode != 0 || b == 0) block_sum8v(sc3, scr);
   if (mode == 1 && it >= 1) {
     // A_i tests R_i (M_{i-1}'s partials) after its product: with the learnt
     // iteration count the test usually fails, so it stays off the launch's
     // critical path; a converged launch writes nothing.  Every block sums the
     // same partials in the same order and decides alike.
-    const double rr = block_sum8(s3, scr);
-    if (rr <= a.tol2 * sc->ee) {
+    if (sc3[2] <= a.tol2 * sc->ee) {
       if (t == 0) {
         sc->pcg_iter = it - 1;
         __hip_atomic_store(&sc->pcg_done, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1270,56 +1275,55 @@ __global__ __launch_bounds__(symsum::NTH) void fr_pcg_ss_kernel(SsPcgArgs a) {
   double* vt = lds + RED;               // the block's result entries (stride VS)
   double* xt = vt + 32 * VS;            // mode 2: X's new entries (mirror staging)
   const double wgt = own_weight(g);
-  double acc1 = 0.0, acc2 = 0.0;
+  double acc[2] = {0.0, 0.0};
   if (mode == 0) {
-    const double ee = b == 0 ? block_sum8(s1, scr) : 0.0;
-    if (b == 0 && t == 0) sc->ee = ee * sc->ee_scale;
+    if (b == 0 && t == 0) sc->ee = sc3[0] * sc->ee_scale;
     for (int k = 0; k < nown; ++k) {
       const int e = t + NTH * k, r = e >> 5, c = e & 31;
       const double u = 0.25 * vt[r * VS + c];
       vt[r * VS + c] = u;
       a.U[idx[k]] = u;
-      acc1 = fma(o0[k], u, acc1);
+      acc[0] = fma(o[0][k], u, acc[0]);
     }
-    acc1 = block_sum8(wgt * acc1, scr);
-    if (t == 0) a.gam[b] = acc1;
+    double red1[1] = {wgt * acc[0]};
+    block_sum8v(red1, scr);
+    if (t == 0) a.gam[b] = red1[0];
   } else if (mode == 1) {
-    const double gam = block_sum8(s1, scr);
-    const double gam0 = it >= 1 ? block_sum8(s2, scr) : 1.0;
-    const double beta = it >= 1 ? gam / gam0 : 0.0;
+    const double beta = it >= 1 ? sc3[0] / sc3[1] : 0.0;
     for (int k = 0; k < nown; ++k) {
       const int e = t + NTH * k, r = e >> 5, c = e & 31;
       const double w = vt[r * VS + c];
-      const double p = it >= 1 ? fma(beta, o1[k], o0[k]) : o0[k];
-      const double q = it >= 1 ? fma(beta, o2[k], w) : w;
+      const double p = it >= 1 ? fma(beta, o[1][k], o[0][k]) : o[0][k];
+      const double q = it >= 1 ? fma(beta, o[2][k], w) : w;
       vt[r * VS + c] = q;
       a.P[idx[k]] = p;
       a.Q[idx[k]] = q;
-      acc1 = fma(p, q, acc1);
+      acc[0] = fma(p, q, acc[0]);
     }
-    acc1 = block_sum8(wgt * acc1, scr);   // (its barriers also complete vt)
-    if (t == 0) a.pi[b] = acc1;
+    double red1[1] = {wgt * acc[0]};
+    block_sum8v(red1, scr);   // (its barriers also complete vt)
+    if (t == 0) a.pi[b] = red1[0];
   } else {
-    const double gam = block_sum8(s1, scr);
-    const double alpha = gam / block_sum8(s2, scr);
+    const double alpha = sc3[0] / sc3[1];
     for (int k = 0; k < nown; ++k) {
       const int e = t + NTH * k, r = e >> 5, c = e & 31;
       const double v = 0.25 * vt[r * VS + c];
-      const double x = it >= 1 ? fma(alpha, o0[k], o4[k]) : alpha * o0[k];
-      const double rn = fma(-alpha, o1[k], o2[k]), un = fma(-alpha, v, o3[k]);
+      const double x = it >= 1 ? fma(alpha, o[0][k], o[4][k]) : alpha * o[0][k];
+      const double rn = fma(-alpha, o[1][k], o[2][k]), un = fma(-alpha, v, o[3][k]);
       vt[r * VS + c] = un;
       xt[r * VS + c] = x;
       a.X[idx[k]] = x;
       a.R[idx[k]] = rn;
       a.U[idx[k]] = un;
-      acc1 = fma(rn, un, acc1);
-      acc2 = fma(rn, rn, acc2);
+      acc[0] = fma(rn, un, acc[0]);
+      acc[1] = fma(rn, rn, acc[1]);
     }
-    acc1 = block_sum8(wgt * acc1, scr);
-    acc2 = block_sum8(wgt * acc2, scr);
+    acc[0] *= wgt;
+    acc[1] *= wgt;
+    block_sum8v(acc, scr);
     if (t == 0) {
-      a.gam[((it + 1) & 1) * nblk + b] = acc1;
-      a.rho[b] = acc2;
+      a.gam[((it + 1) & 1) * nblk + b] = acc[0];
+      a.rho[b] = acc[1];
     }
   }
   // mirror entries of the operands of later products (U, Q) and of X: thread t

@@ -479,6 +479,9 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
 #else
       acc[f & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[f], fb[f], acc[f & 3], 0, 0, 0);
 #endif
+// (rejected: issuing the next stage's LDS-DMA pieces one per MFMA step instead
+      // of after the barrier -- 9.66 / 9.78 vs 9.67 / 9.51 us per cold 512^3
+      // product, scripts/ubench/gemm_chain.cpp, profiles/r05/dma_interleave_rejected.log)
       if (f + 4 < NST) {
         asm volatile("ds_read_b64 %0, %1" : "=v"(fa[f + 4]) : "v"(xa[f + 4] + so));
         asm volatile("ds_read_b64 %0, %1" : "=v"(fb[f + 4]) : "v"(xb[f + 4] + so));

@@ -70,9 +70,7 @@ struct BlockArgs {
 };
 
 // family kind 0 = mf gaussian, 1 = mf t; target kind per vb_target_kind.
-// start (optional): an event stamped at the kernel's start (timed runs)
-hipError_t launch_sep(int fam, int tgt, bool host_noise, const SepArgs& a, hipStream_t s,
-                      hipEvent_t start = nullptr);
+hipError_t launch_sep(int fam, int tgt, bool host_noise, const SepArgs& a, hipStream_t s);
 // block step skeleton without draws / target (vb_block_floor)
 hipError_t launch_block_floor(int D, int N, bool host_layout, bool chivi, int n_steps, int nprob,
                               double* out, hipStream_t s, int pf = 0);
@@ -91,9 +89,8 @@ hipError_t launch_block_predraw(int fam, int D, int N, int n_steps, int n_proble
                                 double t_const, double* noise, double* lq, hipStream_t s);
 
 // values[i] = -(c0 + sum_w vpart[s][w]) for i = step0 + s
-// stop (optional): an event stamped at the kernel's end (timed runs)
 hipError_t launch_sep_values(const double* vpart, int n_steps, int n_waves, double c0,
-                             double* values_at_step0, hipStream_t s, hipEvent_t stop = nullptr);
+                             double* values_at_step0, hipStream_t s);
 // out[p] = mean over rows of hist [rows][P]   (per problem block of rows)
 hipError_t launch_row_mean(const double* hist, long long rows, long long P, long long n_problems,
                            double* out, hipStream_t s);

@@ -21,8 +21,6 @@
 #include "vb_device.hpp"
 #include "vb_internal.hpp"
 
-#include <hip/hip_ext.h>
-
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -164,10 +162,42 @@ __device__ unsigned long long g_sep_ts[kTsWaves][16];
 __device__ unsigned long long g_sep_clk[kTsWaves][16];  // s_memtime (core clock) beside it
 #endif
 
+// lambda and the register window of a wave's owner lanes, loaded before the
+// kernel's table barrier (the loads then overlap the table loads instead of
+// following them; sep_body's lane mapping)
+template <int PPW>
+struct SepPre {
+  double lam = 0.0;
+  double rg[PPW] = {};
+};
+template <int PPW, bool REGRING>
+__device__ __forceinline__ SepPre<PPW> sep_pre(const SepArgs& a, int wave) {
+  constexpr int LPP = 64 / PPW, SL = LPP / 4;
+  const int lane = threadIdx.x & 63, grp = lane / LPP, gl = lane & (LPP - 1);
+  const int w = wave * PPW + grp, D = a.D;
+  const bool live = w < a.n_pairs, hasB = live && 2 * w + 1 < D;
+  const int own = PPW == 1 ? lane >> 4 : lane & 3;
+  const int sub = PPW == 1 ? lane & 15 : gl >> 2;
+  const long long own_idx = (own & 2 ? D : 0) + (own & 1 ? 2 * w + 1 : 2 * w);
+  const bool own_ok = live && (hasB || !(own & 1));
+  SepPre<PPW> p;
+  p.lam = own_ok ? a.lam[own_idx] : 0.0;
+  if constexpr (REGRING) {
+    if (!a.emit_grad) {
+#pragma unroll
+      for (int j = 0; j < PPW; ++j) {
+        const int sl = j * SL + sub;
+        if (sl < a.W && own_ok) p.rg[j] = a.ring[(long long)sl * 2LL * D + own_idx];
+      }
+    }
+  }
+  return p;
+}
+
 template <class TGT, bool TFAM, bool HOST, int PPW, bool REGRING>
 __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, int wave,
                                          const double2* sct, const double2* ltab,
-                                         unsigned long long t_entry = 0) {
+                                         const SepPre<PPW>& pre, unsigned long long t_entry = 0) {
   constexpr int LPP = 64 / PPW;       // lanes per column pair
   constexpr int SL = LPP / 4;         // slot lanes per parameter
 #ifdef VB_SEP_PROF
@@ -190,7 +220,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
   const long long own_idx = (own & 2 ? D : 0) + (own & 1 ? dB : dA);
   const bool own_ok = live && (hasB || !(own & 1));
   const bool updater = rep && own_ok;
-  double lam_own = own_ok ? a.lam[own_idx] : 0.0;
+  double lam_own = pre.lam;
   double s_own = exp(lam_own);
   double muA = group_bcast<PPW, 0>(lam_own, grp), muB = group_bcast<PPW, 1>(lam_own, grp);
   double sA = group_bcast<PPW, 2>(s_own, grp), sB = group_bcast<PPW, 3>(s_own, grp);
@@ -202,10 +232,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
   if (!a.emit_grad) {
     if constexpr (REGRING) {
 #pragma unroll
-      for (int j = 0; j < PPW; ++j) {
-        const int sl = j * SL + sub;
-        if (sl < W && own_ok) rg[j] = a.ring[(long long)sl * P + own_idx];
-      }
+      for (int j = 0; j < PPW; ++j) rg[j] = pre.rg[j];
     } else {
       if (rep)
         for (int k = 0; k < W; ++k)
@@ -408,23 +435,31 @@ void sep_kernel(SepArgs a) {
   // Box-Muller tables (vb_tables.hpp) for the in-kernel Philox draws
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
+  const int wid = threadIdx.x >> 6;
+  const bool big = (int)blockIdx.x < a.blocks2;
+  const int wave = blockIdx.x * 4 + wid;
+  const int pair = a.pairs2 + (blockIdx.x - a.blocks2) * 4 + wid;
+  SepPre<PPW_BIG> pb;
+  SepPre<1> p1;
+  // the lambda and register-window loads are issued before the table barrier
+  // (after it, as before round 5: 5.15-5.37 vs 5.14-5.35 us/step, launch pair 79.6
+  // vs 78.1 us; profiles/r05/headline_prefetch_ab_d.log)
+  if (big) {
+    if (wave * PPW_BIG < a.pairs2) pb = sep_pre<PPW_BIG, REGRING>(a, wave);
+  } else if (pair < a.n_pairs) {
+    p1 = sep_pre<1, REGRING>(a, pair);
+  }
   if constexpr (!HOST) {
     load_bm_tables(s_sct, s_lt);
     __syncthreads();
   }
-  const int wid = threadIdx.x >> 6;
   double* ring = REGRING ? nullptr : &s_ring[REGRING ? 0 : wid][0];
-  if ((int)blockIdx.x < a.blocks2) {
-    const int wave = blockIdx.x * 4 + wid;
-#ifdef VB_SEP_PRIO   // (experiment: the multi-pair waves, the critical path, first)
-    __builtin_amdgcn_s_setprio(VB_SEP_PRIO);
-#endif
+  if (big) {
     if (wave * PPW_BIG < a.pairs2)
-      sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave, s_sct, s_lt, t_entry);
+      sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave, s_sct, s_lt, pb, t_entry);
   } else {
-    const int pair = a.pairs2 + (blockIdx.x - a.blocks2) * 4 + wid;
     if (pair < a.n_pairs)
-      sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair, s_sct, s_lt, t_entry);
+      sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair, s_sct, s_lt, p1, t_entry);
   }
 }
 
@@ -2209,43 +2244,38 @@ static int sep_split(SepArgs& a, int& big) {
   return big;
 }
 
-// (hipExtLaunchKernel: the optional start event is stamped at the kernel's own
-// start, one host call instead of an event record plus a launch)
 template <class TGT, bool TFAM, bool HOST, bool REG>
-static void sep_launch_ppw(int big, const SepArgs& a, hipStream_t s, hipEvent_t start) {
+static void sep_launch_ppw(int big, const SepArgs& a, hipStream_t s) {
   const dim3 grid(a.blocks2 + a.blocks1), block(256);
   if (big == 4)
-    hipExtLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 4, REG>), grid, block, 0, s, start, nullptr, 0,
-                          a);
+    hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 4, REG>), grid, block, 0, s, a);
   else
-    hipExtLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 2, REG>), grid, block, 0, s, start, nullptr, 0,
-                          a);
+    hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 2, REG>), grid, block, 0, s, a);
 }
 
 template <class TGT>
-static hipError_t sep_dispatch(int fam, bool host, SepArgs a, hipStream_t s, hipEvent_t start) {
+static hipError_t sep_dispatch(int fam, bool host, SepArgs a, hipStream_t s) {
   int big;
   sep_split(a, big);
   const bool reg = a.W <= 16 || a.emit_grad;
   if (host) {
     // host noise holds standardized draws for either family
-    if (reg) sep_launch_ppw<TGT, false, true, true>(big, a, s, start);
-    else sep_launch_ppw<TGT, false, true, false>(big, a, s, start);
+    if (reg) sep_launch_ppw<TGT, false, true, true>(big, a, s);
+    else sep_launch_ppw<TGT, false, true, false>(big, a, s);
   } else if (fam == 1) {
-    if (reg) sep_launch_ppw<TGT, true, false, true>(big, a, s, start);
-    else sep_launch_ppw<TGT, true, false, false>(big, a, s, start);
+    if (reg) sep_launch_ppw<TGT, true, false, true>(big, a, s);
+    else sep_launch_ppw<TGT, true, false, false>(big, a, s);
   } else {
-    if (reg) sep_launch_ppw<TGT, false, false, true>(big, a, s, start);
-    else sep_launch_ppw<TGT, false, false, false>(big, a, s, start);
+    if (reg) sep_launch_ppw<TGT, false, false, true>(big, a, s);
+    else sep_launch_ppw<TGT, false, false, false>(big, a, s);
   }
   return hipGetLastError();
 }
 
-hipError_t launch_sep(int fam, int tgt, bool host, const SepArgs& a, hipStream_t s,
-                      hipEvent_t start) {
+hipError_t launch_sep(int fam, int tgt, bool host, const SepArgs& a, hipStream_t s) {
   switch (tgt) {
-    case 0: return sep_dispatch<IsoGauss>(fam, host, a, s, start);
-    case 1: return sep_dispatch<Mixture>(fam, host, a, s, start);
+    case 0: return sep_dispatch<IsoGauss>(fam, host, a, s);
+    case 1: return sep_dispatch<Mixture>(fam, host, a, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -2345,9 +2375,9 @@ extern "C" int vb_debug_sep_ts(unsigned long long* out, int n_waves) {
 #endif
 
 hipError_t launch_sep_values(const double* vpart, int n_steps, int n_waves, double c0,
-                             double* values, hipStream_t s, hipEvent_t stop) {
-  hipExtLaunchKernelGGL(sep_values_kernel, dim3(n_steps), dim3(kValThreads), 0, s, nullptr, stop, 0,
-                        vpart, n_waves, c0, values);
+                             double* values, hipStream_t s) {
+  hipLaunchKernelGGL(sep_values_kernel, dim3(n_steps), dim3(kValThreads), 0, s, vpart, n_waves,
+                     c0, values);
   return hipGetLastError();
 }
 

@@ -2,11 +2,11 @@
 // roofline fractions; BASELINE.md §2: "both peaks must be confirmed with
 // microbenchmarks on the box").  No reference counterpart.
 //
-//   kind 0  HBM copy     16-byte loads + stores over two buffers far past the
-//                        256 MB Infinity Cache, one slab per block; GB/s of read +
-//                        written bytes
-//   kind 1  HBM read     nontemporal 16-byte loads folded into one XOR per thread;
-//                        GB/s read
+//   kind 0  HBM copy     nontemporal 16-byte loads + stores over two buffers far
+//                        past the 256 MB Infinity Cache, one slab per 1024-thread
+//                        block; GB/s of read + written bytes
+//   kind 1  HBM read     nontemporal 16-byte loads, one slab per block, folded into
+//                        one XOR per thread; GB/s read
 //   kind 2  fp64 MFMA    v_mfma_f64_16x16x4_f64, 4 independent accumulators per
 //                        wave, 4 waves per SIMD; TFLOP/s
 //   kind 3  fp64 VALU    v_fma_f64, 8 independent chains per lane, 4 waves per
@@ -24,37 +24,44 @@ namespace {
 using u4 = unsigned __attribute__((ext_vector_type(4)));
 using d4 = double __attribute__((ext_vector_type(4)));
 
-// copy: each block streams one contiguous slab (4 vectors in flight per thread);
-// of the forms tried (grid-stride, 8-deep, nontemporal, 4-32 blocks per CU,
-// scripts/ubench/hbm_probe.hip, profiles/r04/hbm_probe_variants.log) the slab
-// form reaches the highest copy rate, 5.37-5.41 TB/s against 4.4-4.6 grid-stride
-__global__ __launch_bounds__(256) void probe_copy_kernel(const u4* __restrict__ src,
-                                                         u4* __restrict__ dst, long long n) {
+// copy: each 1024-thread block (one per CU) streams one contiguous slab with
+// nontemporal loads and stores, 4 vectors in flight per thread -- the fastest
+// copy form of the round-5 sweep (scripts/ubench/hbm_probe2.hip,
+// profiles/r05/hbm_probe2.log: 5.71-5.73 TB/s against 5.31-5.45 for 256-thread
+// slabs with plain loads / stores, 4.99 for hipMemcpy device-to-device; round 4's
+// grid-stride forms 4.2-5.2, profiles/r04/hbm_probe_variants.log).  Still below
+// the 6.29 TB/s float4 copy of MI355X_MICROARCH.md, so bench.py reports the
+// fractions against that figure as well.
+__global__ __launch_bounds__(1024) void probe_copy_kernel(const u4* __restrict__ src,
+                                                          u4* __restrict__ dst, long long n) {
   const long long per = (n + gridDim.x - 1) / gridDim.x;
   const long long b0 = (long long)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
   long long i = b0 + threadIdx.x;
-  for (; i + 3 * 256 < b1; i += 4 * 256) {
-    const u4 a = src[i], b = src[i + 256], c = src[i + 512], d = src[i + 768];
-    dst[i] = a;
-    dst[i + 256] = b;
-    dst[i + 512] = c;
-    dst[i + 768] = d;
+  for (; i + 3 * 1024 < b1; i += 4 * 1024) {
+    const u4 a = __builtin_nontemporal_load(src + i), b = __builtin_nontemporal_load(src + i + 1024),
+             c = __builtin_nontemporal_load(src + i + 2048), d = __builtin_nontemporal_load(src + i + 3072);
+    __builtin_nontemporal_store(a, dst + i);
+    __builtin_nontemporal_store(b, dst + i + 1024);
+    __builtin_nontemporal_store(c, dst + i + 2048);
+    __builtin_nontemporal_store(d, dst + i + 3072);
   }
-  for (; i < b1; i += 256) dst[i] = src[i];
+  for (; i < b1; i += 1024) dst[i] = src[i];
 }
 
-// read: nontemporal 16-byte loads, 8 in flight per thread (the fastest read form,
-// 5.5-6.0 TB/s in the same sweep)
+// read: each 256-thread block (two per CU) streams one slab with nontemporal
+// 16-byte loads, 8 in flight per thread, folded into one XOR per thread: 6.7-7.1
+// TB/s in the round-5 sweep (the grid-stride form of round 4: 5.5-6.0)
 __global__ __launch_bounds__(256) void probe_read_kernel(const u4* __restrict__ src, long long n,
                                                          unsigned* __restrict__ out) {
-  const long long stride = (long long)gridDim.x * 256;
-  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long per = (n + gridDim.x - 1) / gridDim.x;
+  const long long b0 = (long long)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
+  long long i = b0 + threadIdx.x;
   u4 acc = {0u, 0u, 0u, 0u};
-  for (; i + 7 * stride < n; i += 8 * stride) {
+  for (; i + 7 * 256 < b1; i += 8 * 256) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc ^= __builtin_nontemporal_load(src + i + u * stride);
+    for (int u = 0; u < 8; ++u) acc ^= __builtin_nontemporal_load(src + i + u * 256);
   }
-  for (; i < n; i += stride) acc ^= src[i];
+  for (; i < b1; i += 256) acc ^= src[i];
   out[(long long)blockIdx.x * 256 + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
 }
 
@@ -115,7 +122,7 @@ int probe_rate(int kind, long long n, int reps, hipStream_t st, double* out) {
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   void *a = nullptr, *b = nullptr;
   const long long nv = kind <= 1 ? n / 16 : 0;        // 16-byte vectors
-  const unsigned blocks = kind == 0 ? (unsigned)ncu * 16 : kind == 1 ? (unsigned)ncu * 32 : (unsigned)ncu * 4;
+  const unsigned blocks = kind == 0 ? (unsigned)ncu : kind == 1 ? (unsigned)ncu * 2 : (unsigned)ncu * 4;
   const size_t abytes = kind <= 1 ? (size_t)nv * 16 : 0;
   const size_t bbytes = kind == 0 ? abytes : sizeof(double) * blocks * 256;
   if (abytes && hipMalloc(&a, abytes) != hipSuccess) {
@@ -135,7 +142,7 @@ int probe_rate(int kind, long long n, int reps, hipStream_t st, double* out) {
   auto launch = [&]() {
     switch (kind) {
       case 0:
-        hipLaunchKernelGGL(probe_copy_kernel, dim3(blocks), dim3(256), 0, st, (const u4*)a, (u4*)b, nv);
+        hipLaunchKernelGGL(probe_copy_kernel, dim3(blocks), dim3(1024), 0, st, (const u4*)a, (u4*)b, nv);
         break;
       case 1:
         hipLaunchKernelGGL(probe_read_kernel, dim3(blocks), dim3(256), 0, st, (const u4*)a, nv,

@@ -96,10 +96,12 @@ __device__ __forceinline__ double own_weight(const Geo& g) { return g.diag ? 1.0
 
 // V of the block into vt (rows 0..15 or 0..31, stride VS), unscaled: entries of
 // A X + X A.  lds: Cfg<KT>::LDS_DOUBLES of dynamic LDS; vt = lds + RED.  Ends with
-// a barrier (vt complete; the stage buffers are free again).
-template <int KT>
-__device__ __forceinline__ void product(const double* __restrict__ Am, const double* __restrict__ Xm,
-                                        int D, const Geo& g, double* lds) {
+// a barrier (vt complete; the stage buffers are free again).  go() is asked after
+// the first stage is issued (its loads in flight): false (the same in every wave
+// of the block) drains them and returns false before any barrier.
+template <int KT, class Go>
+__device__ __forceinline__ bool product(const double* __restrict__ Am, const double* __restrict__ Xm,
+                                        int D, const Geo& g, double* lds, Go&& go) {
   using C = Cfg<KT>;
   constexpr int GS = C::GS, TA = C::TA, ST = C::ST, NA = C::NA, NB = C::NB, NS = C::NS;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -153,6 +155,10 @@ __device__ __forceinline__ void product(const double* __restrict__ Am, const dou
   for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
   issue(0, 0);
   if (GS >= 3 && nst > 1) issue(1, 1);
+  if (!go()) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return false;
+  }
   // stage it's buffer, and the buffer of the stage issued after its barrier
   int slot = 0, slot2 = GS >= 3 ? 2 : 1;
   for (int it = 0; it < nst; ++it) {
@@ -183,6 +189,7 @@ __device__ __forceinline__ void product(const double* __restrict__ Am, const dou
       else if (ahead == 1) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(fa[s]), "+v"(fb[s]));
       else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[s]), "+v"(fb[s]));
       acc[s & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[s], fb[s], acc[s & 3], 0, 0, 0);
+// (rejected: the next stage's DMA pieces one per MFMA step: 12.05 vs 11.50 us)
       if (s + 4 < NS) {
         asm volatile("ds_read_b64 %0, %1" : "=v"(fa[s + 4]) : "v"(xa[s + 4] + so));
         asm volatile("ds_read_b64 %0, %1" : "=v"(fb[s + 4]) : "v"(xb[s + 4] + so));
@@ -231,6 +238,12 @@ __device__ __forceinline__ void product(const double* __restrict__ Am, const dou
     }
     __syncthreads();
   }
+  return true;
+}
+template <int KT>
+__device__ __forceinline__ void product(const double* __restrict__ Am, const double* __restrict__ Xm,
+                                        int D, const Geo& g, double* lds) {
+  product<KT>(Am, Xm, D, g, lds, [] { return true; });
 }
 
 // Block sum of one value per thread (fixed order: DPP wave sums, then the 8 waves
@@ -244,6 +257,26 @@ __device__ __forceinline__ double block_sum8(double v, double* scratch) {
                    ((scratch[4] + scratch[5]) + (scratch[6] + scratch[7]));
   __syncthreads();
   return s;
+}
+
+// Block sums of NV values per thread at once (one LDS exchange, two barriers):
+// each v[j] becomes its block total, in block_sum8's fixed order.  scratch: 8 NV
+// doubles of LDS.
+template <int NV>
+__device__ __forceinline__ void block_sum8v(double (&v)[NV], double* scratch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    v[j] = vbd::wave_sum_dpp(v[j]);
+    if (lane == 0) scratch[8 * j + w] = v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const double* q = scratch + 8 * j;
+    v[j] = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+  }
+  __syncthreads();
 }
 
 // Plain symmetric-sum product C = alpha (A X + X A) (measurement / tests).
