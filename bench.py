@@ -40,8 +40,6 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X dense fp64 MFMA spec peak
 # wave64 fp64 VALU issue: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per instruction
 # (profiles/r01/ubench_instr_costs.txt)
 VALU_PEAK_GINSTR = 256 * 4 * 2.4 / 4
-# config 4: products of 2 D^3 one profiled step executes (see leg_cfg4)
-EXEC_PRODUCTS_CFG4 = 14 * 136 / 256 + 3 * 0.25 + 11 + 1
 CHUNK = 256                    # steps per sep_kernel launch (vb_capi.hip max_chunk)
 
 
@@ -497,9 +495,9 @@ def latency_roofline(step_s, d, n, chivi, host_layout, n_problems, note):
 def cfg5_stage_valu(stage_s, local, n_restarts):
     """VALU issue fraction of config 5's bounds / PSIS stage: the stage's
     SQ_INSTS_VALU from a committed counter pass over the same stage
-    (profiles/r03/cfg5/bounds_stage_pmc.json, scripts/gpu_cfg5_pmc.sh; 64
+    (profiles/r05/cfg5/bounds_stage_pmc.json, scripts/gpu_cfg5_pmc.sh; 64
     restarts x M = 1e6, scaled to this rank's restarts) over the live stage time."""
-    p = os.path.join(ROOT, 'profiles', 'r03', 'cfg5', 'bounds_stage_pmc.json')
+    p = os.path.join(ROOT, 'profiles', 'r05', 'cfg5', 'bounds_stage_pmc.json')
     try:
         prof = json.load(open(p))
     except (OSError, ValueError):
@@ -511,7 +509,7 @@ def cfg5_stage_valu(stage_s, local, n_restarts):
     return {'valu_instr': vi, 'achieved': vi / stage_s / 1e9, 'peak': VALU_PEAK_GINSTR,
             'unit': 'G wave-instr/s', 'frac': vi / stage_s / 1e9 / VALU_PEAK_GINSTR,
             'logw_kernel_valu_frac': k.get('valu_frac'),
-            'source': 'SQ_INSTS_VALU of the stage (profiles/r03/cfg5/bounds_stage_pmc.json) / '
+            'source': 'SQ_INSTS_VALU of the stage (profiles/r05/cfg5/bounds_stage_pmc.json) / '
                       'live stage seconds; the log-weight kernel fraction is from the profile'}
 
 
@@ -549,10 +547,14 @@ def leg_cfg4(cpu, host, steps=30):
     run = vb.DeviceRun(obj, steps + 3, lam0)
     run.advance_philox(3, 0, 1, 0)
     _sync()
+    from viabel_amd import _native as nat
+    nat.lib().vb_flop_tally(1)
     t0 = time.perf_counter()
     run.advance_philox(steps, 0, 1, 3)
     _sync()
     dt = (time.perf_counter() - t0) / steps
+    # matrix-core flops of the products the timed advance launched (library tally)
+    exec_flops = nat.lib().vb_flop_tally(0) / steps
     flops = 8 * n * Dm * Dm + 20 * Dm ** 3          # SURVEY §8d config 4 algorithmic flops / step
     ach = flops / dt / 1e12
     out = {'config': 4, 'workload': 'full-rank t D=512 df=100 CHIVI a=2 N=128 corr_gauss, adagrad',
@@ -560,18 +562,13 @@ def leg_cfg4(cpu, host, steps=30):
            'roofline': {'bound': 'mfma', 'achieved': ach, 'peak': FP64_PEAK_TFLOPS,
                         'unit': 'TFLOP/s', 'frac': ach / FP64_PEAK_TFLOPS,
                         'algorithmic_flops_per_step': flops,
-                        # ESTIMATE from one profiled step, not counted in this run
-                        # (rocprofv3 timeline, profiles/r03/cfg4/step_timeline.txt): Sigma
-                        # and the Newton-Schulz products are symmetric (upper-triangle
-                        # tiles, 136/256 of a product): Sigma + iteration 0 + 4 x (T, Y, Z)
-                        # = 14 x 0.531; x / grad / G_S 3 x 0.25; PCG 1 + 5 x 2; G_L 1:
-                        # 20.19 products of 2 D^3
-                        'executed_flops_per_step_est': EXEC_PRODUCTS_CFG4 * 2 * Dm ** 3,
-                        'executed_tflops_est': EXEC_PRODUCTS_CFG4 * 2 * Dm ** 3 / dt / 1e12,
+                        'executed_flops_per_step': exec_flops,
+                        'executed_tflops': exec_flops / dt / 1e12,
+                        'executed_frac': exec_flops / dt / 1e12 / FP64_PEAK_TFLOPS,
                         'note': 'whole step (all launches) timed on the host clock; flops = '
-                                '8 N D^2 + 20 D^3 (SURVEY §8d); executed_*_est = the GEMM '
-                                'flops of one profiled step (a fixed estimate: the counts the '
-                                'device learns can differ by an iteration)'}}
+                                '8 N D^2 + 20 D^3 (SURVEY §8d); executed_* = the matrix-core '
+                                'flops of every product the timed steps launched (tiles x tile '
+                                'area x depth x 2, counted by the library: vb_flop_tally)'}}
     if cpu:
         from oracle import fullrank_oracle as fo
         ofam = fo.FullRankT(Dm, 100.0)

@@ -178,6 +178,11 @@ const char* vb_last_error(void);
  * viabel_amd/csrc/Makefile's HASH_SRCS, fixed at build time: which sources the
  * loaded binary was built from (measurement provenance; not part of the path). */
 const char* vb_build_id(void);
+/* Matrix-core flops of the products the calling thread has launched since the
+ * last reset (each launch: tiles computed x tile area x depth x 2; launches the
+ * device skips past convergence count too); reset != 0 zeroes the tally.  Measurement
+ * aid for the full-rank step's executed-flop figure; not part of the reference API. */
+double vb_flop_tally(int reset);
 /* `hip_stream` may be NULL (the context creates its own stream) or an
  * existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream). */
 int vb_ctx_create(int device, void* hip_stream, vb_ctx** out);

@@ -441,3 +441,26 @@ def test_exact_epilogue_kernels_equal_the_generic_kernel(tmp_path):
         res[mode] = np.load(f)
     for key in ('lam', 'vals'):
         np.testing.assert_allclose(res['0'][key], res['1'][key], rtol=1e-9, atol=1e-12)
+
+
+def test_flop_tally_counts_the_launched_products():
+    """vb_flop_tally (the executed-flop figure of bench.py's config-4 leg): a
+    reset zeroes it, a full-rank advance at D = 64 adds the matrix-core work of its
+    products (at least the PCG's symmetric sums, 4 D^3 each, and the Sigma = L L^T
+    product), and a read without reset leaves it unchanged."""
+    vb, targets, _, _, _ = _mods()
+    from viabel_amd import _native as nat
+    D, N = 64, 16
+    fam = vb.t_variational_family(D, 30.0, rng='philox')
+    run = vb.DeviceRun(vb.black_box_chivi(2.0, fam, targets.corr_gauss(D), N), 4, _lam(D, 3))
+    run.advance_philox(1, 0, 1, 0)
+    nat.context().synchronize()
+    nat.lib().vb_flop_tally(1)
+    assert nat.lib().vb_flop_tally(0) == 0.0
+    run.advance_philox(3, 0, 1, 1)
+    nat.context().synchronize()
+    f = nat.lib().vb_flop_tally(0)
+    assert f >= 3 * (4 * D ** 3 + D ** 3), f
+    assert f < 3 * 200 * 2 * D ** 3, f
+    assert nat.lib().vb_flop_tally(1) == f
+    assert nat.lib().vb_flop_tally(0) == 0.0

@@ -65,6 +65,7 @@ _SIGNATURES = {
     'vb_abi_version': ([], ctypes.c_int),
     'vb_last_error': ([], ctypes.c_char_p),
     'vb_build_id': ([], ctypes.c_char_p),
+    'vb_flop_tally': ([ctypes.c_int], ctypes.c_double),
     'vb_ctx_create': ([ctypes.c_int, ctypes.c_void_p, P(ctypes.c_void_p)], ctypes.c_int),
     'vb_ctx_destroy': ([ctypes.c_void_p], ctypes.c_int),
     'vb_ctx_synchronize': ([ctypes.c_void_p], ctypes.c_int),

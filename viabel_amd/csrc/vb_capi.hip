@@ -525,6 +525,12 @@ const char* vb_last_error(void) { return g_err.c_str(); }
 #endif
 const char* vb_build_id(void) { return VB_SRC_HASH; }
 
+double vb_flop_tally(int reset) {
+  const double t = vbk::gemm_flop_tally();
+  if (reset) vbk::gemm_flop_tally() = 0.0;
+  return t;
+}
+
 int vb_ctx_create(int device, void* hip_stream, vb_ctx** out) {
   if (!out) return fail(VB_EINVAL, "null output pointer");
   *out = nullptr;

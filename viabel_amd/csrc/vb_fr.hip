@@ -1181,25 +1181,29 @@ struct SsPcgArgs {
   double* rho;           // [nblk]: ||R||^2 partials (convergence, status)
   FrSched* sc;
   double tol2;           // converged when ||R||^2 <= tol2 ||E||^2 (ee)
+  int pcg_call;          // (VB_SS_PROF: index of the PCG call in the workspace's life)
 };
 
-// Partials of earlier launches, loaded before a product and summed after it: the
-// first two per-thread values are plain loads at clamped indices, their validity
-// applied at the sum (a select or a loop around a load made the compiler wait for
-// it at once, before the product); partials past 2 NTH (D > 724) load at the sum.
+// Partials of earlier launches, loaded before a product and summed after it by
+// every wave on its own (no block barrier; every wave of every block forms the
+// same total in the same order): lane l holds partials l + 64 k (k < 4) as plain
+// loads at clamped indices, their validity applied at the sum (a select or a loop
+// around a load made the compiler wait for it at once, before the product);
+// partials past 256 (D > 512) load at the sum.
 struct PartLoad {
-  double v0, v1;
+  double v[4];
   __device__ __forceinline__ void load(const double* p, int n) {
-    const int t = threadIdx.x;
-    v0 = p[t < n ? t : 0];
-    v1 = p[t + symsum::NTH < n ? t + symsum::NTH : 0];
+    const int l = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = p[l + 64 * k < n ? l + 64 * k : 0];
   }
-  // this thread's share of sum(p[0 .. n)) (block_sum8 then gives the fixed-order total)
-  __device__ __forceinline__ double share(const double* p, int n) const {
-    const int t = threadIdx.x;
-    double a = (t < n ? v0 : 0.0) + (t + symsum::NTH < n ? v1 : 0.0);
-    for (int i = t + 2 * symsum::NTH; i < n; i += symsum::NTH) a += p[i];
-    return a;
+  __device__ __forceinline__ double total(const double* p, int n) const {
+    const int l = threadIdx.x & 63;
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a += l + 64 * k < n ? v[k] : 0.0;
+    for (int i = l + 256; i < n; i += 64) a += p[i];
+    return vbd::wave_sum_dpp(a);
   }
 };
 
@@ -1208,6 +1212,9 @@ __global__ __launch_bounds__(symsum::NTH) void fr_pcg_ss_kernel(SsPcgArgs a) {
   using namespace symsum;
   extern __shared__ double lds[];
   __shared__ double scr[24];
+#ifdef VB_SS_PROF
+  const unsigned long long p_entry = __builtin_amdgcn_s_memrealtime();
+#endif
   kernarg_warm(a);
   const int D = a.D, nt = D / 32, nblk = nt * nt, t = threadIdx.x, b = blockIdx.x;
   const int mode = a.mode, it = a.it;
@@ -1225,7 +1232,7 @@ __global__ __launch_bounds__(symsum::NTH) void fr_pcg_ss_kernel(SsPcgArgs a) {
   int lane0;
   asm volatile("v_mov_b32 %0, 0" : "=v"(lane0));
   const int fv = __hip_atomic_load(&sc->pcg_done + lane0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const Geo g = geo(b, nt);
+  const Geo g = geo_xcd(b, nt);
   const int nown = n_own(g);
   long long idx[2];
 #pragma unroll
@@ -1250,15 +1257,27 @@ __global__ __launch_bounds__(symsum::NTH) void fr_pcg_ss_kernel(SsPcgArgs a) {
   for (int j = 0; j < 5; ++j)
 #pragma unroll
     for (int k = 0; k < 2; ++k) o[j][k] = src[j][idx[k]];
+#ifdef VB_SS_PROF
+  unsigned long long pst[6];
+  pst[2] = __builtin_amdgcn_s_memrealtime();   // (after the first batch of loads was issued)
+#endif
   const bool go = product<KT>(a.Mat, a.V, D, g, lds, [&]() {
     const int f = mode != 0 ? __builtin_amdgcn_readfirstlane(fv) : 0;
     return !(f != 0 && !(mode == 1 && f == it + 1));
-  });
+  }
+#ifdef VB_SS_PROF
+  , pst
+#endif
+  );
   if (!go) return;
-  // the scalars: one block reduction of every partial share (gamma_i, gamma_{i-1}
-  // or pi_i, ||R_i||^2)
-  double sc3[3] = {l1.share(pa1, n1), l2.share(pa2, n2), l3.share(a.rho, n3)};
-  if (mode != 0 || b == 0) block_sum8v(sc3, scr);
+#ifdef VB_SS_PROF
+  pst[3] = __builtin_amdgcn_s_memrealtime();
+#endif
+  // the scalars (gamma_i, gamma_{i-1} or pi_i, ||R_i||^2), summed by each wave
+  const double sc3[3] = {l1.total(pa1, n1), l2.total(pa2, n2), l3.total(a.rho, n3)};
+#ifdef VB_SS_PROF
+  pst[4] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (mode == 1 && it >= 1) {
     // A_i tests R_i (M_{i-1}'s partials) after its product: with the learnt
     // iteration count the test usually fails, so it stays off the launch's
@@ -1337,6 +1356,18 @@ __global__ __launch_bounds__(symsum::NTH) void fr_pcg_ss_kernel(SsPcgArgs a) {
     if (mode == 1) a.Q[m] = v;
     if (mode == 2) a.X[m] = xt[r * VS + c];
   }
+#ifdef VB_SS_PROF
+  // one line per block of every launch of the VB_SS_PROF-th PCG call (entry
+  // stamp, first batch issued, first stage landed, main loop done, product done,
+  // scalars summed, end; CU id from HW_ID)
+  pst[5] = __builtin_amdgcn_s_memrealtime();
+  if (t == 0) {
+    if (a.pcg_call == VB_SS_PROF)
+      printf("SSPROF %d %d %d %u %llu %llu %llu %llu %llu %llu %llu\n", mode, it, b,
+             __builtin_amdgcn_s_getreg(63508), p_entry, pst[2], pst[0], pst[1], pst[3], pst[4],
+             pst[5]);
+  }
+#endif
 }
 
 }  // namespace
@@ -1383,6 +1414,7 @@ struct FrWork {
   const void* retry_owner = nullptr;  // the run the floors belong to
   int kpcg_max_seen = 0;          // most PCG iterations launched since the last fr_info
   int pcg_last = 0;               // the last PCG call: index of its last launched iteration
+  int pcg_calls = 0;              // symmetric-sum PCG calls so far (VB_SS_PROF)
   double pcg_tol2 = 1e-18;        // and its convergence bar (||R||^2 / ||E||^2)
   bool eig_pending = false;       // a dsyevd ran since the last fr_info
   bool sqrt_pending = false;      // a Newton-Schulz / PCG status to read at fr_info
@@ -1768,8 +1800,10 @@ int fr_pcg(FrWork* W, int D, hipStream_t st, int N = 0, const double* rw = nullp
     a.rho = W->rr_part.d();
     a.sc = sc;
     a.tol2 = tol2;
+    a.pcg_call = W->pcg_calls++;
     const dim3 grid((unsigned)((D / 32) * (D / 32)));
     auto launch = [&]() {
+      gemm_flop_tally() += 4.0 * D * (double)D * D;   // nt^2 blocks x 16 x 32 x 2D x 2
       if (symsum::kt_for(D) == 128)
         hipLaunchKernelGGL(fr_pcg_ss_kernel<128>, grid, dim3(symsum::NTH), symsum::Cfg<128>::LDS_BYTES,
                            st, a);

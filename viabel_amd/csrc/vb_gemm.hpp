@@ -904,6 +904,14 @@ inline int epi_mask(const GemmOp& o) {
   X(kEpiRpW)                                         /* corr_gauss target */
 }  // namespace gemm_detail
 
+// Matrix-core flops of the products this thread has launched (vb_flop_tally):
+// per launch, the tiles its grid computes x BT^2 x K x 2 (device-skipped launches
+// count too), so a measured step reports the work it ran, not a model
+inline double& gemm_flop_tally() {
+  static thread_local double t = 0.0;
+  return t;
+}
+
 // number of 4-per-block partial sums of an n x n result (sym: upper triangle)
 inline int gemm_parts(int n, bool sym) {
   const int t = (n + gemm_detail::BT - 1) / gemm_detail::BT;
@@ -935,6 +943,7 @@ inline hipError_t gemm_group(const GemmOp* ops, int n, hipStream_t s) {
                           : dim3(ntn, (unsigned)((g.M + BT - 1) / BT), (unsigned)n);
   const bool ks = g.kscale != nullptr, dual = g.A2 != nullptr;
   if (ks && dual) return hipErrorInvalidValue;
+  gemm_flop_tally() += (double)grid.x * grid.y * grid.z * BT * BT * g.K * 2.0 * (dual ? 2 : 1);
   // exact epilogue kernels: plain NN products whose ops share one listed set, and
   // the NT Sigma = L L^T products (the step's first launch)
   int epi = kEpiAll;
@@ -1000,6 +1009,7 @@ inline hipError_t gemm_hook(const GemmOp& g0, const typename Hook::Args& hook, h
   if (gg.op[0].sym && (g0.M != g0.N || g0.rp_part)) return hipErrorInvalidValue;
   const unsigned ntn = (unsigned)((g0.N + BT - 1) / BT);
   const dim3 grid = gg.op[0].sym ? dim3(ntn * (ntn + 1) / 2) : dim3(ntn, (unsigned)((g0.M + BT - 1) / BT));
+  gemm_flop_tally() += (double)grid.x * grid.y * BT * BT * g0.K * 2.0;
   // the hook's own feature set (Hook::kEpi) when the op matches it exactly
   const bool exact = gemm_epi_exact_enabled() && epi_mask(gg.op[0]) == Hook::kEpi;
   if (!g0.ta && !g0.tb && exact)

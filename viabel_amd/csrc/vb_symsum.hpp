@@ -66,7 +66,7 @@ struct Geo {
   int bi, bj, r0, c0;
   bool diag;
 };
-__device__ __forceinline__ Geo geo(int b, int nt) {
+__host__ __device__ __forceinline__ Geo geo(int b, int nt) {
   const int no = nt * (nt - 1) / 2;
   Geo g;
   if (b < 2 * no) {
@@ -88,6 +88,53 @@ __device__ __forceinline__ Geo geo(int b, int nt) {
   return g;
 }
 
+// The same units in XCD-grouped order.  The dispatcher places block b on XCD b % 8
+// (each with its own L2); with nt % 4 == 0 the XCDs take one band block each of the
+// 4 x 4 grid of nt/4-tile bands -- (0,1) (0,2) (0,3) (1,2) (1,3) (2,3) -- and the
+// diagonal band blocks in pairs, (0,0) + (3,3) and (1,1) + (2,2): nt^2 / 8 units
+// each.  An XCD then reads the row and column panels of two bands of each operand
+// (1.75-3 MB at D = 512) instead of all of both (4 MB, its whole L2): 11.57 -> 10.77
+// us per cold 512^3 symmetric sum (scripts/ubench/symsum_bench.cpp).  Other nt:
+// geo()'s order.
+__host__ __device__ __forceinline__ Geo geo_xcd(int b, int nt) {
+#ifdef VB_SS_NO_XCD
+  return geo(b, nt);
+#endif
+  if (nt % 4 != 0) return geo(b, nt);
+  const int x = b & 7, q = b >> 3, m = nt >> 2;
+  Geo g;
+  if (x < 6) {
+    const int ra = x < 3 ? 0 : (x < 5 ? 1 : 2);
+    const int cb = x < 3 ? x + 1 : (x < 5 ? x - 1 : 3);
+    const int t = q >> 1;
+    g.bi = ra * m + t / m;
+    g.bj = cb * m + t % m;
+    g.diag = false;
+    g.r0 = 32 * g.bi + 16 * (q & 1);
+  } else {
+    const int per = m * m, no = m * (m - 1) / 2;
+    const int band = x == 6 ? (q < per ? 0 : 3) : (q < per ? 1 : 2);
+    const int u = q < per ? q : q - per;
+    if (u < 2 * no) {
+      int t = u >> 1, i = 0;
+      while (t >= m - 1 - i) {
+        t -= m - 1 - i;
+        ++i;
+      }
+      g.bi = band * m + i;
+      g.bj = band * m + i + 1 + t;
+      g.diag = false;
+      g.r0 = 32 * g.bi + 16 * (u & 1);
+    } else {
+      g.bi = g.bj = band * m + (u - 2 * no);
+      g.diag = true;
+      g.r0 = 32 * g.bi;
+    }
+  }
+  g.c0 = 32 * g.bj;
+  return g;
+}
+
 // Entries a block owns: off-diagonal half 16 x 32 (thread t: row t / 32, column
 // t % 32), diagonal tile 32 x 32 (thread t: entries t and t + 512).  weight: the
 // entry's share of a Frobenius inner product over the whole symmetric matrix.
@@ -99,9 +146,16 @@ __device__ __forceinline__ double own_weight(const Geo& g) { return g.diag ? 1.0
 // a barrier (vt complete; the stage buffers are free again).  go() is asked after
 // the first stage is issued (its loads in flight): false (the same in every wave
 // of the block) drains them and returns false before any barrier.
+#ifdef VB_SS_PROF
+// phase stamps of the calling thread (s_memrealtime, 100 MHz): first stage landed,
+// main loop done
+#define VB_SS_STAMPS , unsigned long long* vb_ss_stamp
+#else
+#define VB_SS_STAMPS
+#endif
 template <int KT, class Go>
 __device__ __forceinline__ bool product(const double* __restrict__ Am, const double* __restrict__ Xm,
-                                        int D, const Geo& g, double* lds, Go&& go) {
+                                        int D, const Geo& g, double* lds, Go&& go VB_SS_STAMPS) {
   using C = Cfg<KT>;
   constexpr int GS = C::GS, TA = C::TA, ST = C::ST, NA = C::NA, NB = C::NB, NS = C::NS;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -167,6 +221,9 @@ __device__ __forceinline__ bool product(const double* __restrict__ Am, const dou
     if (GS >= 3 && it + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NB) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+#ifdef VB_SS_PROF
+    if (it == 0) vb_ss_stamp[0] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (it + GS - 1 < nst) issue(it + GS - 1, slot2);
     if (g.diag && it == NT1) {   // the tile's first 16 rows are done
       top = (acc[0] + acc[1]) + (acc[2] + acc[3]);
@@ -198,6 +255,9 @@ __device__ __forceinline__ bool product(const double* __restrict__ Am, const dou
     slot = slot + 1 == GS ? 0 : slot + 1;
     slot2 = slot2 + 1 == GS ? 0 : slot2 + 1;
   }
+#ifdef VB_SS_PROF
+  vb_ss_stamp[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   const d4 r4 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   // k parts 1..3 hand their quadrants to part 0 through LDS (fixed order)
   __syncthreads();
@@ -243,7 +303,12 @@ __device__ __forceinline__ bool product(const double* __restrict__ Am, const dou
 template <int KT>
 __device__ __forceinline__ void product(const double* __restrict__ Am, const double* __restrict__ Xm,
                                         int D, const Geo& g, double* lds) {
+#ifdef VB_SS_PROF
+  unsigned long long st[2];
+  product<KT>(Am, Xm, D, g, lds, [] { return true; }, st);
+#else
   product<KT>(Am, Xm, D, g, lds, [] { return true; });
+#endif
 }
 
 // Block sum of one value per thread (fixed order: DPP wave sums, then the 8 waves
@@ -284,7 +349,7 @@ template <int KT>
 __global__ __launch_bounds__(NTH) void symsum_plain_kernel(const double* A, const double* X, int D,
                                                            double alpha, double* C) {
   extern __shared__ double lds[];
-  const Geo g = geo(blockIdx.x, D / 32);
+  const Geo g = geo_xcd(blockIdx.x, D / 32);
   product<KT>(A, X, D, g, lds);
   const double* vt = lds + RED;
   const int t = threadIdx.x;
