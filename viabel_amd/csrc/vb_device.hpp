@@ -205,7 +205,10 @@ __device__ __forceinline__ double log1p_pos_tab(double y, const double2* ltab) {
 __device__ __forceinline__ double log_u01_tab(double u, const double2* ltab) {
   int e;
   const double m = frexp(u, &e);
-  const double2 t = ltab[kLogN + (int)rint(fma(m, 256.0, -128.0))];  // j in [0, 128]
+  // j = rint(256 m) - 128 in [0, 128] (= rint(256 m - 128): the shift is an even
+  // integer); 256 m by ldexp, the -128 folded into the LDS read offset (an fma
+  // needed its two constants in VGPRs, re-made every call)
+  const double2 t = ltab[kLogN - 128 + (int)rint(ldexp(m, 8))];
   const double r = fma(m, t.x, -1.0);
   double p = 0.14285714285714285;                // 1/7
   p = hfma(p, r, -0.16666666666666666);

@@ -212,6 +212,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
   const long long P = 2LL * D;
   const int dA = 2 * w, dB = 2 * w + 1;
   const bool hasB = live && dB < D;
+  const double hbw = hasB ? 1.0 : 0.0;   // (the separable targets' lp1 is finite)
   double* ring = ring_base + grp * 4;  // LDS ring [slot][PPW * 4]
 
   const int own = PPW == 1 ? lane >> 4 : lane & 3;        // 0 muA, 1 muB, 2 lsA, 3 lsB
@@ -261,8 +262,11 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
     const long long i = a.step0 + s;
     const uint32_t ri = (uint32_t)(a.rng_step0 + s);
     double gA = 0.0, gB = 0.0, hA = 0.0, hB = 0.0, v = 0.0;
-    // reparameterise one sample row of the pair, evaluate the target, accumulate
-    auto consume = [&](double eA, double eB) {
+    // reparameterise one sample row of the pair, evaluate the target, accumulate;
+    // PD (a.pd as a compile-time tag: the sample loop is instantiated per form, so
+    // no run-time test sits in it)
+    auto consume = [&](double eA, double eB, auto pdc) {
+      constexpr int PD = decltype(pdc)::value;
       double dg;
       const double xA = eA * sA + muA;
       double lpA = TGT::lp1(xA, dg);
@@ -270,25 +274,23 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
       hA += dg * eA;
       const double xB = eB * sB + muB;
       double lpB = TGT::lp1(xB, dg);
-      if (a.pd) {
-        // -log q(x) without its per-pair constants: 1/2 eps^2 (Gaussian) or
-        // (df + 1)/2 log1p(eps^2 / df) (t, df = 2 shape)
-        // (the form is a run-time field: host-noise launches do not instantiate TFAM)
-        if (a.pd == 2) {
-          const double df = 2.0 * a.shape;
-          lpA += 0.5 * (df + 1.0) * log1p(eA * eA / df);
-          lpB += 0.5 * (df + 1.0) * log1p(eB * eB / df);
-        } else {
-          lpA += 0.5 * eA * eA;
-          lpB += 0.5 * eB * eB;
-        }
+      // -log q(x) without its per-pair constants: 1/2 eps^2 (Gaussian) or
+      // (df + 1)/2 log1p(eps^2 / df) (t, df = 2 shape)
+      // (the form is a run-time field: host-noise launches do not instantiate TFAM)
+      if constexpr (PD == 2) {
+        const double df = 2.0 * a.shape;
+        lpA += 0.5 * (df + 1.0) * log1p(eA * eA / df);
+        lpB += 0.5 * (df + 1.0) * log1p(eB * eB / df);
+      } else if constexpr (PD == 1) {
+        lpA += 0.5 * eA * eA;
+        lpB += 0.5 * eB * eB;
       }
-      v += hasB ? lpA + lpB : lpA;
+      v += fma(hbw, lpB, lpA);   // lpA + lpB, or lpA on a lane without column B
       gB += dg;
       hB += dg * eB;
     };
     // draw sample row n (host noise, or Philox normals [+ gamma for t]) and consume it
-    auto sample = [&](int n) {
+    auto sample = [&](int n, auto pdc) {
       double eA, eB;
       if constexpr (HOST) {
         const double* row = a.noise + ((long long)s * N + n) * D;
@@ -303,16 +305,27 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
           eB = a.t_scale * eB / sqrt(GB);
         }
       }
-      consume(eA, eB);
+      consume(eA, eB, pdc);
     };
-    int n = gl;
-    if constexpr (PIPE) {
-      // sample row gl was drawn during the previous step's update
-      if (n < N) consume(pA, pB);
-      n += LPP;
-    }
+    // sample rows gl + k LPP: a loop with a uniform trip count over the rows every
+    // lane has (scalar loop control, no exec-mask bookkeeping per row), then the
+    // ragged remainder row of the lanes below N % LPP
+    auto rows = [&](auto pdc) {
+      int k0 = 0;
+      if constexpr (PIPE) {
+        // sample row gl was drawn during the previous step's update
+        if (gl < N) consume(pA, pB, pdc);
+        k0 = 1;
+      }
+      const int kfull = N / LPP;
 #pragma unroll 1
-    for (; n < N; n += LPP) sample(n);
+      for (int k = k0; k < kfull; ++k) sample(gl + k * LPP, pdc);
+      const int kr = kfull > k0 ? kfull : k0;
+      if (gl + kr * LPP < N) sample(gl + kr * LPP, pdc);
+    };
+    if (a.pd == 0) rows(std::integral_constant<int, 0>{});
+    else if (a.pd == 2) rows(std::integral_constant<int, 2>{});
+    else rows(std::integral_constant<int, 1>{});
     const double S = reduce4<PPW>(lane, gA, gB, hA, hB);
     // d/dmu = -mean g ; d/dlog sigma = -(1 + sigma * mean(g * eps))
     const double m = S * invN;
