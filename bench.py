@@ -291,7 +291,7 @@ def load_valu_busy():
     at), from the committed record scripts/gpu_valu_busy.sh wrote.  A measured
     counterpart to the instruction-count model's frac, which prices every VALU
     instruction at 4 cycles."""
-    p = os.path.join(ROOT, 'profiles', 'r04', 'valu_busy_headline.json')
+    p = os.path.join(ROOT, 'profiles', 'r05', 'valu_busy_headline.json')
     try:
         with open(p) as f:
             d = json.load(f)
@@ -300,7 +300,7 @@ def load_valu_busy():
     disp = d.get('dispatches') or []
     return {'busy': d.get('timed_dispatch_valu_busy'),
             'clock_ghz': disp[-1].get('clock_ghz') if disp else None,
-            'formula': d.get('formula'), 'source': 'profiles/r04/valu_busy_headline.json'}
+            'formula': d.get('formula'), 'source': 'profiles/r05/valu_busy_headline.json'}
 
 
 def roofline_cfg3(launches, n, traffic):
