@@ -1216,17 +1216,19 @@ __global__ __launch_bounds__(symsum::NTH) void fr_pcg_ss_kernel(SsPcgArgs a) {
   const unsigned long long p_entry = __builtin_amdgcn_s_memrealtime();
 #endif
   kernarg_warm(a);
+  asm volatile("" ::"s"(a.n_ee));   // (in the first kernarg batch: read later, in mode 0)
   const int D = a.D, nt = D / 32, nblk = nt * nt, t = threadIdx.x, b = blockIdx.x;
   const int mode = a.mode, it = a.it;
   FrSched* sc = a.sc;
   // Everything before the product's first wait is issued at once: the skip flag,
-  // the scalars' partials of the previous launches, this block's own entries of the
-  // CG vectors (only this block writes them; the product reads the whole operand,
-  // which no block of this launch writes) and the product's first stage.  All
-  // straight-line loads at clamped indices (entry 1 of a half block re-reads entry
-  // 0; sources a mode does not use read another vector), so no wait precedes it.
-  // Iterations past convergence then return (every wave reads the flag itself; a
-  // flag holding this launch's own tag was set by a peer block and is ignored).
+  // the product's first stage, then the epilogue's inputs -- the scalars' partials
+  // of the previous launches and this block's own entries of the CG vectors (only
+  // this block writes them; the product reads the whole operand, which no block of
+  // this launch writes).  All straight-line loads at clamped indices (entry 1 of a
+  // half block re-reads entry 0; sources a mode does not use read another vector),
+  // so no wait precedes them.  Iterations past convergence then return (every wave
+  // reads the flag itself; a flag holding this launch's own tag was set by a peer
+  // block and is ignored).
   // (a per-lane load: the compiler moves a uniform one to a scalar register, and
   // waits for it, right where it is loaded)
   int lane0;
@@ -1246,22 +1248,25 @@ __global__ __launch_bounds__(symsum::NTH) void fr_pcg_ss_kernel(SsPcgArgs a) {
   const int n2 = (mode == 1 && it >= 1) || mode == 2 ? nblk : 0;
   const int n3 = mode == 1 && it >= 1 ? nblk : 0;
   PartLoad l1, l2, l3;
-  l1.load(pa1, n1);
-  l2.load(pa2, n2);
-  l3.load(a.rho, n3);
   // own entries o[j]: mode 0 R; mode 1 U, P, Q (it >= 1); mode 2 P, Q, R, U, X (it >= 1)
   const double* src[5] = {mode == 0 ? a.R : (mode == 1 ? a.U : a.P), mode == 1 ? a.P : a.Q,
                           mode == 1 ? a.Q : a.R, a.U, a.X};
   double o[5][2];
-#pragma unroll
-  for (int j = 0; j < 5; ++j)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) o[j][k] = src[j][idx[k]];
 #ifdef VB_SS_PROF
   unsigned long long pst[6];
-  pst[2] = __builtin_amdgcn_s_memrealtime();   // (after the first batch of loads was issued)
 #endif
   const bool go = product<KT>(a.Mat, a.V, D, g, lds, [&]() {
+    // (after the first stage's loads were issued)
+    l1.load(pa1, n1);
+    l2.load(pa2, n2);
+    l3.load(a.rho, n3);
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) o[j][k] = src[j][idx[k]];
+#ifdef VB_SS_PROF
+    pst[2] = __builtin_amdgcn_s_memrealtime();
+#endif
     const int f = mode != 0 ? __builtin_amdgcn_readfirstlane(fv) : 0;
     return !(f != 0 && !(mode == 1 && f == it + 1));
   }
