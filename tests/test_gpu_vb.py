@@ -325,13 +325,14 @@ def test_device_philox_noise_equals_c_oracle(kind, df, D):
                                rtol=2e-14, atol=1e-13)
 
 
-@pytest.mark.parametrize('mode', ['1', '2', '4', 'mix', 'q'])
-@pytest.mark.parametrize('kind,df,D', [('gauss', None, 9001), ('t', 40.0, 8200), ('gauss', None, 17)])
-def test_sep_layouts_agree(mode, kind, df, D, monkeypatch):
-    """The column-pair kernel's layouts (1 or 2 pairs per wavefront, or the
-    mixed grid) give the oracle's trajectory (Philox noise)."""
+@pytest.mark.parametrize('kind,df,D', [('gauss', None, 17), ('t', 40.0, 8200), ('gauss', None, 9001),
+                                       ('gauss', None, 18432), ('t', 40.0, 40000)])
+def test_sep_layouts_agree(kind, df, D):
+    """Every branch of the column-pair kernel's grid split (vb_mf.hip sep_split)
+    gives the oracle's trajectory (Philox noise): 1-pair waves only (D = 17), one
+    4-pair wave per SIMD + 1-pair waves (8200, 9001: partial blocks of each kind),
+    two layers of 4-pair waves + 1-pair waves (18 432), all 4-pair waves (40 000)."""
     vb, targets, vo, ro = _mods()
-    monkeypatch.setenv('VB_SEP_MODE', mode)
     N, n_iters = 100, 24
     fam = _family(vb, kind, df, D, 'philox')
     ofam = vo.Family(kind, D, df)

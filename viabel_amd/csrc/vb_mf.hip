@@ -2215,37 +2215,24 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
 // -------------------------------------------------------------------------
 bool target_separable(int tgt) { return tgt == 0 || tgt == 1; }
 
-// Split of the column pairs between multi-pair (PPW_BIG) and 1-pair waves.
-// VB_SEP_MODE: "1" all single; "2" / "4" all 2- / 4-pair; "mix": per SIMD
-// (1024 of them) two 2-pair waves, then 1-pair waves for the rest; "q"
-// (default below 8 192 pairs, measured fastest at D = 1e4:
-// profiles/r01/ab_layouts_q.json): one 4-pair wave per SIMD, then 1-pair waves;
-// larger D generalises it (see the default branch).  Blocks of big waves come
-// first so round-robin dispatch deals the same mix to every CU.
-static int sep_split(SepArgs& a, int& big) {
-  const char* e = getenv("VB_SEP_MODE");
+// Split of the column pairs between multi-pair (PPW_BIG) and 1-pair waves: below
+// 8 192 pairs one 4-pair wave per SIMD (1 024 of them), then 1-pair waves -- measured
+// fastest at D = 1e4 (profiles/r01/ab_layouts_q.json; round 5: two 2-pair waves + 1-pair
+// waves per SIMD 87 us, all 2-pair 97, all 1-pair 104, a 4-pair wave on every SIMD
+// 75.0, against 75.1 us for this split, profiles/r05/headline_layout*.log); larger D
+// generalises it (see the second branch).  Blocks of big waves come first so
+// round-robin dispatch deals the same mix to every CU.
+static void sep_split(SepArgs& a) {
+  constexpr int big = 4;
   const int np = a.n_pairs;
   int pairs2;
-  big = 2;
-  if (e && e[0] == '1') {
-    pairs2 = 0;
-  } else if (e && e[0] == '2') {
-    pairs2 = np;
-  } else if (e && e[0] == '4') {
-    big = 4;
-    pairs2 = np;
-  } else if (e && e[0] == 'm') {  // "mix": two 2-pair waves + 1-pair waves per SIMD
-    const int cap2 = 1024 * 2 * 2;
-    pairs2 = np >= cap2 + 1024 ? cap2 : (np > 4096 ? np - 1024 : 0);
-  } else if (np < 2 * 4096) {      // default "q": one 4-pair wave + 1-pair waves per SIMD
-    big = 4;
+  if (np < 2 * 4096) {
     pairs2 = np > 4096 + 1024 ? 4096 : (np > 1024 ? np - 1024 : 0);
   } else {
     // larger D: L layers of one 4-pair wave per SIMD and the rest in 1-pair
     // waves while that stays within ~4 resident waves per SIMD; beyond, all
     // 4-pair waves (their fixed per-step cost per pair is ~4x lower:
     // profiles/r01_sweep_layouts.json)
-    big = 4;
     const int layers = np / 4096, rest = np - 4096 * layers;
     pairs2 = layers + (rest + 1023) / 1024 <= 4 ? 4096 * layers : np;
   }
@@ -2254,33 +2241,28 @@ static int sep_split(SepArgs& a, int& big) {
   a.blocks2 = pairs2 / (4 * big);
   const int rest = np - pairs2;
   a.blocks1 = (rest + 3) / 4;
-  return big;
 }
 
 template <class TGT, bool TFAM, bool HOST, bool REG>
-static void sep_launch_ppw(int big, const SepArgs& a, hipStream_t s) {
-  const dim3 grid(a.blocks2 + a.blocks1), block(256);
-  if (big == 4)
-    hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 4, REG>), grid, block, 0, s, a);
-  else
-    hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 2, REG>), grid, block, 0, s, a);
+static void sep_launch(const SepArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 4, REG>), dim3(a.blocks2 + a.blocks1), dim3(256),
+                     0, s, a);
 }
 
 template <class TGT>
 static hipError_t sep_dispatch(int fam, bool host, SepArgs a, hipStream_t s) {
-  int big;
-  sep_split(a, big);
+  sep_split(a);
   const bool reg = a.W <= 16 || a.emit_grad;
   if (host) {
     // host noise holds standardized draws for either family
-    if (reg) sep_launch_ppw<TGT, false, true, true>(big, a, s);
-    else sep_launch_ppw<TGT, false, true, false>(big, a, s);
+    if (reg) sep_launch<TGT, false, true, true>(a, s);
+    else sep_launch<TGT, false, true, false>(a, s);
   } else if (fam == 1) {
-    if (reg) sep_launch_ppw<TGT, true, false, true>(big, a, s);
-    else sep_launch_ppw<TGT, true, false, false>(big, a, s);
+    if (reg) sep_launch<TGT, true, false, true>(a, s);
+    else sep_launch<TGT, true, false, false>(a, s);
   } else {
-    if (reg) sep_launch_ppw<TGT, false, false, true>(big, a, s);
-    else sep_launch_ppw<TGT, false, false, false>(big, a, s);
+    if (reg) sep_launch<TGT, false, false, true>(a, s);
+    else sep_launch<TGT, false, false, false>(a, s);
   }
   return hipGetLastError();
 }
