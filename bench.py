@@ -887,3 +887,8 @@ if __name__ == '__main__':
         os.environ.setdefault(k, '1')
     os.environ.setdefault('VIABEL_AMD_PROGRESS', '0')     # no progress bars in the legs
     main()
+    # the library's runs, contexts and streams (the CU-masked pre-draw ones included)
+    # are released while the HIP runtime is alive: under rocprofv3 the process's
+    # static teardown has crashed with them still open after a complete run
+    from viabel_amd import _native
+    _native.release_all()

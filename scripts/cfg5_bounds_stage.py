@@ -22,16 +22,11 @@ def main():
     nat.context().synchronize()
     print('total_s %.4f bounds_psis_s %.4f' % (time.perf_counter() - t0, tm.get('bounds_psis_s', -1)),
           flush=True)
-    # release the library's objects while the HIP runtime is alive (under
-    # rocprofv3 this run once crashed in the process's static teardown)
-    import gc
-    gc.collect()
-    for d, c in list(nat._ctx.items()):
-        c.synchronize()
-        nat.lib().vb_ctx_destroy(c.handle)
-        c.handle = None
-        del nat._ctx[d]
 
 
 if __name__ == '__main__':
     main()
+    # release the library's objects while the HIP runtime is alive (under
+    # rocprofv3 this run once crashed in the process's static teardown)
+    from viabel_amd import _native
+    _native.release_all()

@@ -7,6 +7,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+if [ -z "${TRACE_ONLY:-}" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread \
   > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_gpu.log
@@ -15,7 +16,9 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -1 gpurun_out/smoke.log
 timeout -k 10 500 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || exit $?
 tail -c 400 gpurun_out/bench.log
+fi
 rm -rf gpurun_out/prof2/trace
+mkdir -p gpurun_out/prof2
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof2/trace -o run --output-format csv -- \
   python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/prof2/trace.log 2>&1
 rc=$?

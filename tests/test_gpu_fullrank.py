@@ -446,8 +446,9 @@ def test_exact_epilogue_kernels_equal_the_generic_kernel(tmp_path):
 def test_flop_tally_counts_the_launched_products():
     """vb_flop_tally (the executed-flop figure of bench.py's config-4 leg): a
     reset zeroes it, a full-rank advance at D = 64 adds the matrix-core work of its
-    products (at least the PCG's symmetric sums, 4 D^3 each, and the Sigma = L L^T
-    product), and a read without reset leaves it unchanged."""
+    products (per step at least three of the PCG's symmetric sums, 2 D^3 each -- D^2 / 2
+    complete entries of depth 2D -- and the Sigma = L L^T product, 3 of its 4 tiles at
+    D = 64), and a read without reset leaves it unchanged."""
     vb, targets, _, _, _ = _mods()
     from viabel_amd import _native as nat
     D, N = 64, 16
@@ -460,7 +461,7 @@ def test_flop_tally_counts_the_launched_products():
     run.advance_philox(3, 0, 1, 1)
     nat.context().synchronize()
     f = nat.lib().vb_flop_tally(0)
-    assert f >= 3 * (4 * D ** 3 + D ** 3), f
+    assert f >= 3 * (3 * 2 * D ** 3 + 0.75 * 2 * D ** 3), f
     assert f < 3 * 200 * 2 * D ** 3, f
     assert nat.lib().vb_flop_tally(1) == f
     assert nat.lib().vb_flop_tally(0) == 0.0

@@ -245,6 +245,28 @@ def shutting_down():
     return _SHUTDOWN[0]
 
 
+def release_all():
+    """At the end of a program: collect the objects no longer referenced (their
+    native release runs first), then synchronize and destroy every context (its
+    streams, the CU-masked pre-draw streams included) while the HIP runtime is
+    still alive.  The library is not used afterwards (later finalizers skip their
+    native release).  Under a profiler, the process's teardown has crashed with
+    such streams still alive after a complete run."""
+    import gc
+    gc.collect()
+    for d, c in list(_ctx.items()):
+        try:
+            c.synchronize()
+            if c.handle and _lib is not None:
+                _lib.vb_ctx_destroy(c.handle)
+        finally:
+            c.handle = None
+            del _ctx[d]
+    # native objects still referenced are left to process teardown (their finalizers
+    # must not call into a destroyed context)
+    _SHUTDOWN[0] = True
+
+
 _ctx = {}
 _default_device = [int(os.environ.get('VIABEL_AMD_DEVICE', '0'))]
 

@@ -1808,7 +1808,7 @@ int fr_pcg(FrWork* W, int D, hipStream_t st, int N = 0, const double* rw = nullp
     a.pcg_call = W->pcg_calls++;
     const dim3 grid((unsigned)((D / 32) * (D / 32)));
     auto launch = [&]() {
-      gemm_flop_tally() += 4.0 * D * (double)D * D;   // nt^2 blocks x 16 x 32 x 2D x 2
+      gemm_flop_tally() += 2.0 * D * (double)D * D;   // nt^2 blocks x 16 x 32 x 2D x 2
       if (symsum::kt_for(D) == 128)
         hipLaunchKernelGGL(fr_pcg_ss_kernel<128>, grid, dim3(symsum::NTH), symsum::Cfg<128>::LDS_BYTES,
                            st, a);
