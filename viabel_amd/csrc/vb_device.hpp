@@ -200,7 +200,7 @@ __device__ __forceinline__ double log1p_pos_tab(double y, const double2* ltab) {
 // log(u) for u in (0, 1) (Box-Muller radius and acceptance uniforms, never 0):
 // u = m 2^e with m in [1/2, 1) and e <= 0, so e ln2, log c and log1p(r) never
 // cancel; c = 1/2 + j/256 the nearest table point, |r| <= 1/256, log1p to r^7.
-// The LDS log table holds kLogTab followed by kLogU01Tab (load_bm_tables); at
+// The LDS log table holds kBmTab's log rows, then its (0, 1) rows (load_bm_tables); at
 // m ~ 1 the entry is exactly (1, 0).
 __device__ __forceinline__ double log_u01_tab(double u, const double2* ltab) {
   int e;
@@ -265,14 +265,23 @@ __device__ __forceinline__ void normal_pair_tab(u4 w, double& z0, double& z1, co
   z1 = r * s;
 }
 
-// Fill the LDS tables (all threads of the block; caller synchronises).
+// Fill the LDS tables (all threads of the block; caller synchronises): rows
+// [0, kSinCosN) of kBmTab to sct, the rest to ltab.
 __device__ __forceinline__ void load_bm_tables(double2* sct, double2* ltab) {
-  for (int i = threadIdx.x; i < kSinCosN; i += blockDim.x)
-    sct[i] = double2{kSinCosPiTab[i][0], kSinCosPiTab[i][1]};
-  for (int i = threadIdx.x; i < kLogN; i += blockDim.x)
-    ltab[i] = double2{kLogTab[i][0], kLogTab[i][1]};
-  for (int i = threadIdx.x; i < kLogU01N; i += blockDim.x)
-    ltab[kLogN + i] = double2{kLogU01Tab[i][0], kLogU01Tab[i][1]};
+  auto dst = [&](int i) { return i < kSinCosN ? sct + i : ltab + (i - kSinCosN); };
+  const double2* src = reinterpret_cast<const double2*>(kBmTab);
+  const int t = threadIdx.x, nt = blockDim.x;
+  if (2 * nt >= kBmTabN) {
+    // both of a thread's rows loaded before either is stored: one memory latency
+    // for the whole fill (a loop per table waited for every load in turn)
+    const int i0 = t, i1 = t + nt;
+    const double2 v0 = src[i0 < kBmTabN ? i0 : 0];
+    const double2 v1 = src[i1 < kBmTabN ? i1 : 0];
+    if (i0 < kBmTabN) *dst(i0) = v0;
+    if (i1 < kBmTabN) *dst(i1) = v1;
+  } else {
+    for (int i = t; i < kBmTabN; i += nt) *dst(i) = src[i];
+  }
 }
 
 // Two standard normals from one Philox block (Box-Muller).
