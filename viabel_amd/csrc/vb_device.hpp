@@ -515,9 +515,12 @@ struct Funnel {
   // and the gradients of its coordinates [h DH, h DH + DH) (xh / gh); x1 = log sigma
   // is computed by both lanes.  The pair's gv parts are summed with one DPP swap
   // (both lanes active) and land on coordinate 1's owner.
+  template <int DH>
+  __device__ __forceinline__ static void lane_const(int /*h*/, double* /*lk*/) {}
   template <int DMAX, int DH>
   __device__ __forceinline__ static double row_half(const double* xh, double* gh, int h, int D,
-                                                    double /*x0*/, double x1) {
+                                                    double /*x0*/, double x1,
+                                                    const double* /*lk*/) {
     constexpr double s0 = 1.35, is0 = 1.0 / 1.35;
     const double v = x1;
     // (multiplications by 1 / 1.35 rounded at compile time instead of two IEEE
@@ -601,13 +604,29 @@ struct EightSchools {
   // Split rows (see Funnel::row_half): lane 0 owns mu, log tau and theta_tilde
   // 0-2, lane 1 theta_tilde 3-7 (DH = 5); both compute tau.  The pair's mu and
   // log tau gradient parts are summed with one DPP swap each.
-  template <int DMAX, int DH>
-  __device__ __forceinline__ static double row_half(const double* xh, double* gh, int h, int /*D*/,
-                                                    double x0, double x1) {
+  // lk: the lane's y_j and 1 / sigma_j (lane_const), made once per thread before
+  // the step loop.  Selected here per row (h ? y[j1] : y[j0]), the compiler turned
+  // them into loads from a constant table at a per-lane index: ten global loads,
+  // reissued after every row's LDS reads and waited for on the row's chain.
+  template <int DH>
+  __device__ __forceinline__ static void lane_const(int h, double* lk) {
     static_assert(DH >= 2, "eight schools: coordinates 0 and 1 on lane 0");
     constexpr double y[8] = {28., 8., -3., 7., -1., 1., 18., 12.};
     constexpr double is[8] = {1. / 15., 1. / 10., 1. / 16., 1. / 11.,
                               1. / 9.,  1. / 11., 1. / 10., 1. / 18.};
+#pragma unroll
+    for (int k = 0; k < DH; ++k) {
+      // theta_tilde j = h DH + k - 2: lane 0's k >= 2, every k of lane 1
+      const int j0 = k >= 2 ? k - 2 : 0, j1 = DH + k - 2 < 8 ? DH + k - 2 : 7;
+      double yj = h ? y[j1] : y[j0], isj = h ? is[j1] : is[j0];
+      asm("" : "+v"(yj), "+v"(isj));   // (opaque: kept in registers, not re-derived per row)
+      lk[k] = yj;
+      lk[DH + k] = isj;
+    }
+  }
+  template <int DMAX, int DH>
+  __device__ __forceinline__ static double row_half(const double* xh, double* gh, int h, int /*D*/,
+                                                    double x0, double x1, const double* lk) {
     const double mu = x0, u = x1, tau = exp(u);
     const double t5 = tau * 0.2, m5 = mu * 0.2;
     double lp = 0.0, gmu = 0.0, gu = 0.0;
@@ -632,10 +651,8 @@ struct EightSchools {
     }
 #pragma unroll
     for (int k = 0; k < DH; ++k) {
-      // theta_tilde j = h DH + k - 2: lane 0's k >= 2, every k of lane 1
       const bool th_on = h == 1 || k >= 2;
-      const int j0 = k >= 2 ? k - 2 : 0, j1 = DH + k - 2 < 8 ? DH + k - 2 : 7;
-      const double yj = h ? y[j1] : y[j0], isj = h ? is[j1] : is[j0];
+      const double yj = lk[k], isj = lk[DH + k];
       const double th = xh[k];
       const double r = (yj - mu - tau * th) * isj;
       const double rs = r * isj;
@@ -671,9 +688,12 @@ struct SepRow {
     return lp;
   }
   // Split rows: this lane's coordinates [h DH, h DH + DH) only (no cross terms)
+  template <int DH>
+  __device__ __forceinline__ static void lane_const(int /*h*/, double* /*lk*/) {}
   template <int DMAX, int DH>
   __device__ __forceinline__ static double row_half(const double* xh, double* gh, int h, int D,
-                                                    double /*x0*/, double /*x1*/) {
+                                                    double /*x0*/, double /*x1*/,
+                                                    const double* /*lk*/) {
     double lp = 0.0;
 #pragma unroll
     for (int k = 0; k < DH; ++k) {

@@ -1026,6 +1026,9 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
 #endif
 
   int slot = W > 0 ? (int)(a.step0 % W) : 0;  // window ring slot of step i (i % W)
+  // split rows: the target's per-lane constants, made once (Row::lane_const)
+  double lk[2 * DH] = {};
+  if constexpr (SPLIT) Row::template lane_const<DH>(tid & 1, lk);
   // One step.  RO = 0: every wave runs the whole step (host noise, chunked
   // draws); with overlapped draws the row waves (RO = 1) and the draw waves
   // (RO = 2) run their own copies of the step loop — same barriers, disjoint
@@ -1130,7 +1133,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
         gh[k] = 0.0;
       }
       const double x0 = e[0] * s_sg[0] + s_lam[0], x1 = e[1] * s_sg[1] + s_lam[1];
-      double lp = Row::template row_half<DMAX, DH>(xh, gh, h, D, x0, x1);
+      double lp = Row::template row_half<DMAX, DH>(xh, gh, h, D, x0, x1, lk);
       lp += dpp_f64<0xB1>(lp);   // the pair's total (the same sum in both lanes)
       const double lq = lqs;   // (+ sum_d log sigma_d, as row_of)
       if (a.pd) lp -= lq;
