@@ -1123,16 +1123,20 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
 
     // split rows: lane h of the pair (eh = its half of the noise, e = the whole
     // row for the shared coordinates 0 and 1); log p summed over the pair
+    // (mu, sigma of the lane's coordinates and of coordinates 0 / 1: read by the
+    // split-row block below before the row's noise, so the noise reads' wait covers
+    // them -- one LDS round trip per row instead of one per coordinate read under
+    // its own per-lane d < D test)
+    double mk[DH], sk[DH], m01[2], s01[2];
     auto row_half_of = [&](const double* eh, const double* e, double lqs, int h) {
       double xh[DH], gh[DH];
 #pragma unroll
       for (int k = 0; k < DH; ++k) {
         const int d = h * DH + k;
-        const double m = s_lam[d], sgd = s_sg[d];
-        xh[k] = d < D ? eh[k] * sgd + m : 0.0;
+        xh[k] = d < D ? eh[k] * sk[k] + mk[k] : 0.0;
         gh[k] = 0.0;
       }
-      const double x0 = e[0] * s_sg[0] + s_lam[0], x1 = e[1] * s_sg[1] + s_lam[1];
+      const double x0 = e[0] * s01[0] + m01[0], x1 = e[1] * s01[1] + m01[1];
       double lp = Row::template row_half<DMAX, DH>(xh, gh, h, D, x0, x1, lk);
       lp += dpp_f64<0xB1>(lp);   // the pair's total (the same sum in both lanes)
       const double lq = lqs;   // (+ sum_d log sigma_d, as row_of)
@@ -1179,6 +1183,18 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
         const double* buf = s_pf + (s % 3) * L.pf_slot;
         const unsigned base = (unsigned)(uintptr_t)((const lds_f64*)buf);
         const int h = tid & 1;
+        // this step's mu and sigma (clamped indices: every lane reads, no masked
+        // block), issued before the first row's noise reads and waited for with them
+#pragma unroll
+        for (int k = 0; k < DH; ++k) {
+          const int d = h * DH + k, dc = d < D ? d : 0;
+          mk[k] = s_lam[dc];
+          sk[k] = s_sg[dc];
+        }
+        m01[0] = s_lam[0];
+        m01[1] = s_lam[1];
+        s01[0] = s_sg[0];
+        s01[1] = s_sg[1];
         // pairs are active together (n is the same for both lanes): the DPP swaps
         // inside row_half_of see their partner
         for (int n = tid >> 1; n < N; n += RT >> 1) {
