@@ -226,7 +226,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
   const bool own_ok = live && (hasB || !(own & 1));
   const bool updater = rep && own_ok;
   double lam_own = pre.lam;
-  double s_own = exp(lam_own);
+  double s_own = exp_fast(lam_own);
   double muA = group_bcast<PPW, 0>(lam_own, grp), muB = group_bcast<PPW, 1>(lam_own, grp);
   double sA = group_bcast<PPW, 2>(s_own, grp), sB = group_bcast<PPW, 3>(s_own, grp);
 
@@ -402,7 +402,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
     }
     // lam - lr * g / sqrt(eps + accum)   (vb.py:374)
     lam_own = lam_own - (a.lr.at(i) * g_own) * rsqrt_pos(a.eps + q);
-    s_own = exp(lam_own);
+    s_own = exp_fast(lam_own);
     muA = group_bcast<PPW, 0>(lam_own, grp);
     muB = group_bcast<PPW, 1>(lam_own, grp);
     sA = group_bcast<PPW, 2>(s_own, grp);
@@ -941,7 +941,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
   for (int p = tid; p < P; p += NT) s_lam[p] = lam_g[p];
   if (!a.emit_grad)
     for (int q = tid; q < W * P; q += NT) s_ring[q] = ring_g[q];
-  for (int d = tid; d < D; d += NT) s_sg[d] = exp(lam_g[D + d]);
+  for (int d = tid; d < D; d += NT) s_sg[d] = exp_fast(lam_g[D + d]);
 
   const Rng rng{a.k0, a.k1, (uint32_t)(a.stream + (uint32_t)prob * a.stream_stride)};
   const double c0 = TFAM ? 0.0 : 0.5 * D * (1.0 + kLog2Pi);
@@ -1106,12 +1106,12 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
           return;
         }
         if (lw > mloc) {
-          const double f = (mloc == -INFINITY) ? 0.0 : exp(a.alpha * (mloc - lw));
+          const double f = (mloc == -INFINITY) ? 0.0 : exp_fast(a.alpha * (mloc - lw));
 #pragma unroll
           for (int k = 0; k <= 2 * DMAX; ++k) acc[k] *= f;
           mloc = lw;
         }
-        const double wgt = exp(a.alpha * (lw - mloc));
+        const double wgt = exp_fast(a.alpha * (lw - mloc));
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) {
           acc[d] += wgt * g[d];
@@ -1162,12 +1162,12 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
           return;
         }
         if (lw > mloc) {
-          const double f = (mloc == -INFINITY) ? 0.0 : exp(a.alpha * (mloc - lw));
+          const double f = (mloc == -INFINITY) ? 0.0 : exp_fast(a.alpha * (mloc - lw));
 #pragma unroll
           for (int k = 0; k < KH; ++k) acch[k] *= f;
           mloc = lw;
         }
-        const double wgt = exp(a.alpha * (lw - mloc));
+        const double wgt = exp_fast(a.alpha * (lw - mloc));
 #pragma unroll
         for (int k = 0; k < DH; ++k) {
           acch[k] += wgt * gh[k];
@@ -1332,7 +1332,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
         for (int q = 1; q < kBlockMaxRowWaves; ++q) M = q < RW ? fmax(M, mq[q]) : M;
       }
       if (rows) {
-        const double f = (mloc == -INFINITY) ? 0.0 : exp(a.alpha * (mloc - M));
+        const double f = (mloc == -INFINITY) ? 0.0 : exp_fast(a.alpha * (mloc - M));
         if constexpr (SPLIT) {
 #pragma unroll
           for (int k = 0; k < KH; ++k) acch[k] *= f;
@@ -1433,7 +1433,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
           if (i >= a.hist_start) a.hist[((long long)prob * a.n_hist + (i - a.hist_start)) * P + p] = nl;
         }
         s_lam[p] = nl;  // only thread p reads/writes s_lam[p] / s_sg[p - D] until the barrier
-        if (p >= D) s_sg[p - D] = exp(nl);
+        if (p >= D) s_sg[p - D] = exp_fast(nl);
       }
     }
     if (RO != 1 && tid == val_tid) {
@@ -1650,7 +1650,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
       }
       const double nl = __dsub_rn(s_lam[p], __dmul_rn(1e-6, gp) / sqrt(__dadd_rn(0.1, q)));
       s_lam[p] = nl;
-      if (p >= D) s_sg[p - D] = exp(nl);
+      if (p >= D) s_sg[p - D] = exp_fast(nl);
     }
     if (tid == (NT > 64 ? NT - 64 : 0)) {
       if (has_copy) sl = s_sl;
