@@ -437,26 +437,36 @@ __device__ __forceinline__ double stride4_sum(double k) {
   return k;
 }
 
+// max(a, b) as one v_max_f64: fmax's lowering first canonicalises each operand
+// (v_max_f64 x, x, x -- signalling-NaN quieting) and arithmetic never yields a
+// signalling NaN, so the canonicalisations only lengthen the wave reductions'
+// chains; quiet NaNs behave as in fmax (the other operand is returned)
+__device__ __forceinline__ double fmax_raw(double a, double b) {
+  double d;
+  asm("v_max_f64 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+
 __device__ __forceinline__ double swap_max16(double v) {
   const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
   const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
   const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  return fmax(__hiloint2double((int)b[0], (int)a[0]), __hiloint2double((int)b[1], (int)a[1]));
+  return fmax_raw(__hiloint2double((int)b[0], (int)a[0]), __hiloint2double((int)b[1], (int)a[1]));
 }
 
 __device__ __forceinline__ double swap_max32(double v) {
   const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
   const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
   const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  return fmax(__hiloint2double((int)b[0], (int)a[0]), __hiloint2double((int)b[1], (int)a[1]));
+  return fmax_raw(__hiloint2double((int)b[0], (int)a[0]), __hiloint2double((int)b[1], (int)a[1]));
 }
 
 // Wave-wide max with DPP + permlane swaps (every lane receives the maximum).
 __device__ __forceinline__ double wave_max_dpp(double v) {
-  v = fmax(v, dpp_f64<0xB1>(v));
-  v = fmax(v, dpp_f64<0x4E>(v));
-  v = fmax(v, dpp_f64<0x141>(v));
-  v = fmax(v, dpp_f64<0x140>(v));
+  v = fmax_raw(v, dpp_f64<0xB1>(v));
+  v = fmax_raw(v, dpp_f64<0x4E>(v));
+  v = fmax_raw(v, dpp_f64<0x141>(v));
+  v = fmax_raw(v, dpp_f64<0x140>(v));
   v = swap_max16(v);
   return swap_max32(v);
 }
@@ -657,26 +667,24 @@ struct EightSchools {
                                                     double x0, double x1, const double* lk) {
     const double mu = x0, u = x1, tau = exp_fast(u);
     const double t5 = tau * 0.2, m5 = mu * 0.2;
-    double lp = 0.0, gmu = 0.0, gu = 0.0;
-    if (h == 0) {
-      // (the prior terms sit on the rows' dependent chain of config 5's fit: the
-      // table-free log1p and a refined reciprocal instead of the library log1p and
-      // an IEEE division, ~1 ulp; log tau^2 = 2 u is far from overflow here: the
-      // library form takes the non-finite cases)
-      const double w = t5 * t5;
-      if (w < 0x1p+1000) {
-        const double d = 1.0 + w;
-        double r = __builtin_amdgcn_rcp(d);
-        r = fma(r, fma(-d, r, 1.0), r);
-        r = fma(r, fma(-d, r, 1.0), r);
-        lp = -0.5 * m5 * m5 - log1p_pos_fast(w) + u;
-        gu = -2.0 * w * r + 1.0;
-      } else {
-        lp = -0.5 * m5 * m5 - log1p(w) + u;
-        gu = -2.0 * w / (1.0 + w) + 1.0;
-      }
-      gmu = -m5 * 0.2;
-    }
+    // prior terms of mu and tau on lane 0, computed by both lanes without a branch
+    // (lane 1's discarded by the selects): as a lane-0 block they could not be
+    // interleaved with the theta terms below, which depend only on tau as well
+    // (the table-free log1p and a refined reciprocal instead of the library log1p
+    // and an IEEE division, ~1 ulp; also branch-free at the extremes: for w >= 2^1000
+    // the rounding correction of 1 + w is 0 and log_unit takes any normal argument,
+    // w = inf gives inf by the select and NaN stays NaN; the gradient
+    // -2 w / (1 + w) + 1 is NaN at w = inf, as the divided form is)
+    const double w = t5 * t5;
+    const double dw = 1.0 + w;
+    double rw = __builtin_amdgcn_rcp(dw);
+    rw = fma(rw, fma(-dw, rw, 1.0), rw);
+    rw = fma(rw, fma(-dw, rw, 1.0), rw);
+    const double l1 = w < INFINITY ? log1p_pos_fast(w) : w;
+    const double gu0 = -2.0 * w * rw + 1.0;
+    double lp = h == 0 ? -0.5 * m5 * m5 - l1 + u : 0.0;
+    double gmu = h == 0 ? -m5 * 0.2 : 0.0;
+    double gu = h == 0 ? gu0 : 0.0;
 #pragma unroll
     for (int k = 0; k < DH; ++k) {
       const bool th_on = h == 1 || k >= 2;

@@ -1329,7 +1329,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
         for (int q = 0; q < kBlockMaxRowWaves; ++q) mq[q] = s_max[q];
         M = mq[0];
 #pragma unroll
-        for (int q = 1; q < kBlockMaxRowWaves; ++q) M = q < RW ? fmax(M, mq[q]) : M;
+        for (int q = 1; q < kBlockMaxRowWaves; ++q) M = q < RW ? fmax_raw(M, mq[q]) : M;
       }
       if (rows) {
         const double f = (mloc == -INFINITY) ? 0.0 : exp_fast(a.alpha * (mloc - M));
