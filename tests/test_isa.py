@@ -73,7 +73,7 @@ def disasm_gemm(tmp_path_factory):
     return funcs
 
 
-PF_RE = re.compile(r'block_kernel<vbd::\w+, (true|false), true, (\d+), true, (?:true|false)>')
+PF_RE = re.compile(r'block_kernel<vbd::\w+, (true|false), true, (\d+), true, (?:true|false)(?:, \d+)?>')
 
 
 def test_copy_wave_row_reads_are_waited_before_any_other_instruction(disasm):

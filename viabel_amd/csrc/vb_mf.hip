@@ -170,7 +170,7 @@ struct SepPre {
   double lam = 0.0;
   double rg[PPW] = {};
 };
-template <int PPW, bool REGRING>
+template <int PPW, bool REGRING, bool ADV = false>
 __device__ __forceinline__ SepPre<PPW> sep_pre(const SepArgs& a, int wave) {
   constexpr int LPP = 64 / PPW, SL = LPP / 4;
   const int lane = threadIdx.x & 63, grp = lane / LPP, gl = lane & (LPP - 1);
@@ -183,7 +183,7 @@ __device__ __forceinline__ SepPre<PPW> sep_pre(const SepArgs& a, int wave) {
   SepPre<PPW> p;
   p.lam = own_ok ? a.lam[own_idx] : 0.0;
   if constexpr (REGRING) {
-    if (!a.emit_grad) {
+    if (ADV || !a.emit_grad) {
 #pragma unroll
       for (int j = 0; j < PPW; ++j) {
         const int sl = j * SL + sub;
@@ -194,7 +194,7 @@ __device__ __forceinline__ SepPre<PPW> sep_pre(const SepArgs& a, int wave) {
   return p;
 }
 
-template <class TGT, bool TFAM, bool HOST, int PPW, bool REGRING>
+template <class TGT, bool TFAM, bool HOST, int PPW, bool REGRING, bool ADV = false>
 __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, int wave,
                                          const double2* sct, const double2* ltab,
                                          const SepPre<PPW>& pre, unsigned long long t_entry = 0) {
@@ -209,6 +209,11 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
   const int w = wave * PPW + grp;     // column pair of this lane
   const bool live = w < a.n_pairs;    // trailing groups of the last wave may be empty
   const int D = a.D, N = a.N, W = a.W;
+  // ADV: the optimisation launches (vb_run_advance) -- no emitted gradient and the
+  // plain KLVI value -- as compile-time constants, so the step loop carries no branch,
+  // mask or scalar reload for the single-call forms (the headline's launches)
+  const int emit_grad = ADV ? 0 : a.emit_grad;
+  const int pdv = ADV ? 0 : a.pd;
   const long long P = 2LL * D;
   const int dA = 2 * w, dB = 2 * w + 1;
   const bool hasB = live && dB < D;
@@ -234,7 +239,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
   double rg[PPW];
 #pragma unroll
   for (int j = 0; j < PPW; ++j) rg[j] = 0.0;
-  if (!a.emit_grad) {
+  if (!emit_grad) {
     if constexpr (REGRING) {
 #pragma unroll
       for (int j = 0; j < PPW; ++j) rg[j] = pre.rg[j];
@@ -342,12 +347,12 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
       const int kr = kfull > k0 ? kfull : k0;
       if (gl + kr * LPP < N) sample(gl + kr * LPP, pdc);
     };
-    if (a.pd == 0) rows(std::integral_constant<int, 0>{});
-    else if (a.pd == 2) rows(std::integral_constant<int, 2>{});
+    if (pdv == 0) rows(std::integral_constant<int, 0>{});
+    else if (pdv == 2) rows(std::integral_constant<int, 2>{});
     else rows(std::integral_constant<int, 1>{});
     if constexpr (kQuad) {
       // the rows' log p: -1/2 sum x^2 plus the constant of each of the lane's rows
-      if (a.pd == 0) v = fma(hbw, fma(-0.5, qB, quad_c), fma(-0.5, qA, quad_c));
+      if (pdv == 0) v = fma(hbw, fma(-0.5, qB, quad_c), fma(-0.5, qA, quad_c));
     }
     const double S = reduce4<PPW>(lane, gA, gB, hA, hB);
     // d/dmu = -mean g ; d/dlog sigma = -(1 + sigma * mean(g * eps))
@@ -366,7 +371,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
       if (rep && live && st >= (s & ~3)) a.vpart[(long long)st * a.n_waves + w] = tot;
     }
 
-    if (a.emit_grad) {
+    if (emit_grad) {
       if (updater) a.grad[own_idx] = g_own;
       continue;
     }
@@ -441,7 +446,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
            t_loop, t_end, t_s0, t_s1, t_s2);
   }
 #endif
-  if (!a.emit_grad && own_ok) {
+  if (!emit_grad && own_ok) {
     if (rep) a.lam[own_idx] = lam_own;
     if constexpr (REGRING) {
 #pragma unroll
@@ -459,7 +464,7 @@ __device__ __forceinline__ void sep_body(const SepArgs& a, double* ring_base, in
 // Grid: blocks [0, a.blocks2) run PPW_BIG column pairs per wave, the remaining
 // blocks one pair per wave.  The split balances the work per SIMD with every
 // wave resident; it affects speed only.
-template <class TGT, bool TFAM, bool HOST, int PPW_BIG, bool REGRING>
+template <class TGT, bool TFAM, bool HOST, int PPW_BIG, bool REGRING, bool ADV = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(3)))
 void sep_kernel(SepArgs a) {
 #if defined(VB_SEP_PROF) || defined(VB_SEP_TS)
@@ -482,9 +487,9 @@ void sep_kernel(SepArgs a) {
   // (after it, as before round 5: 5.15-5.37 vs 5.14-5.35 us/step, launch pair 79.6
   // vs 78.1 us; profiles/r05/headline_prefetch_ab_d.log)
   if (big) {
-    if (wave * PPW_BIG < a.pairs2) pb = sep_pre<PPW_BIG, REGRING>(a, wave);
+    if (wave * PPW_BIG < a.pairs2) pb = sep_pre<PPW_BIG, REGRING, ADV>(a, wave);
   } else if (pair < a.n_pairs) {
-    p1 = sep_pre<1, REGRING>(a, pair);
+    p1 = sep_pre<1, REGRING, ADV>(a, pair);
   }
   if constexpr (!HOST) {
     load_bm_tables(s_sct, s_lt);
@@ -493,10 +498,10 @@ void sep_kernel(SepArgs a) {
   double* ring = REGRING ? nullptr : &s_ring[REGRING ? 0 : wid][0];
   if (big) {
     if (wave * PPW_BIG < a.pairs2)
-      sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING>(a, ring, wave, s_sct, s_lt, pb, t_entry);
+      sep_body<TGT, TFAM, HOST, PPW_BIG, REGRING, ADV>(a, ring, wave, s_sct, s_lt, pb, t_entry);
   } else {
     if (pair < a.n_pairs)
-      sep_body<TGT, TFAM, HOST, 1, REGRING>(a, ring, pair, s_sct, s_lt, p1, t_entry);
+      sep_body<TGT, TFAM, HOST, 1, REGRING, ADV>(a, ring, pair, s_sct, s_lt, p1, t_entry);
   }
 }
 
@@ -861,13 +866,22 @@ __host__ __device__ inline BlockLayout block_layout(int N, int D, bool host, boo
   return L;
 }
 
-template <class TGT, bool TFAM, bool HOST, int DMAX, bool PF = false, bool SPLIT = false>
+template <class TGT, bool TFAM, bool HOST, int DMAX, bool PF = false, bool SPLIT = false, int HOT = 0>
 // device-noise (HOST) instances launch <= 256 threads (<= 4 row waves, or <= 3 and the
 // copy wave): one wave per SIMD, so their registers may use the whole file instead of
 // spilling at the 256-VGPR cap a 512-thread bound implies (the DMAX = 16 instances).
 // Split-row instances (DMAX <= 10) launch up to 4 row waves + the copy wave.
 __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void block_kernel(BlockArgs a) {
   static_assert(!SPLIT || (HOST && PF && DMAX <= kBlockSplitMaxD), "split rows: copy-wave layout");
+  // HOT (split-row instances only): the objective / optimiser flags of the benchmark
+  // configurations as compile-time constants -- 1 KLVI + windowed adagrad, 2 CHIVI +
+  // windowed adagrad, no emitted gradient, no sampled log q -- so their runs carry no
+  // branch, mask or reload for the other modes (0: the flags as passed)
+  static_assert(HOT == 0 || SPLIT, "compile-time modes for the split-row instances");
+  const bool k_chivi = HOT == 2 ? true : (HOT == 1 ? false : (bool)a.chivi);
+  const bool k_pd = HOT ? false : (bool)a.pd;
+  const int k_opt = HOT ? 0 : a.opt;
+  const bool k_emit = HOT ? false : (bool)a.emit_grad;
   constexpr int K = 2 * DMAX + 2;   // G[DMAX], H[DMAX], V/S, spare
   constexpr int DH = (DMAX + 1) / 2, KH = 2 * DH + 1;   // split rows: per-lane half
   constexpr int WMAX = 64;
@@ -889,7 +903,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
   const int NT = blockDim.x;
   const int prob = blockIdx.x;
   const int D = a.D, N = a.N, W = a.W, P = a.P;
-  const bool need_lq = a.chivi || a.pd;
+  const bool need_lq = k_chivi || k_pd;
   const BlockLayout L = block_layout(N, D, HOST, need_lq, (HOST && PF) ? a.pf : 0);
   const int RW = L.rw, RT = 64 * RW, R = L.rec;
   const bool row_wave = wid < RW;
@@ -934,12 +948,12 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
   // adagrad window sums: the copy wave adds up the older W - 1 slots of every
   // parameter while the rows run (same order, oldest first), so the update adds
   // only the newest square (the same bits as the whole loop)
-  const bool qpre = kPF && a.opt == 0 && !a.emit_grad && W >= 1 && W <= kBlockQpreMaxW;
+  const bool qpre = kPF && k_opt == 0 && !k_emit && W >= 1 && W <= kBlockQpreMaxW;
   double* lam_g = a.lam + (long long)prob * P;
   double* ring_g = a.ring ? a.ring + (long long)prob * W * P : nullptr;
 
   for (int p = tid; p < P; p += NT) s_lam[p] = lam_g[p];
-  if (!a.emit_grad)
+  if (!k_emit)
     for (int q = tid; q < W * P; q += NT) s_ring[q] = ring_g[q];
   for (int d = tid; d < D; d += NT) s_sg[d] = exp_fast(lam_g[D + d]);
 
@@ -1081,8 +1095,8 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
       // log q(x; lam) + sum_d log sigma_d (mvn.logpdf / t.logpdf with all
       // constants, z = eps): the sigma term is added back in the value
       const double lq = lqs;
-      if (a.pd) lp -= lq;
-      if (!a.chivi) {
+      if (k_pd) lp -= lq;
+      if (!k_chivi) {
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) {
           acc[d] += g[d];
@@ -1140,9 +1154,9 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
       double lp = Row::template row_half<DMAX, DH>(xh, gh, h, D, x0, x1, lk);
       lp += dpp_f64<0xB1>(lp);   // the pair's total (the same sum in both lanes)
       const double lq = lqs;   // (+ sum_d log sigma_d, as row_of)
-      if (a.pd) lp -= lq;
+      if (k_pd) lp -= lq;
       const double own = h == 0 ? 1.0 : 0.0;   // the log p / weight slot: lane 0 only
-      if (!a.chivi) {
+      if (!k_chivi) {
 #pragma unroll
         for (int k = 0; k < DH; ++k) {
           acch[k] += gh[k];
@@ -1317,7 +1331,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
 
     VB_BT(0);
     double M = 0.0;
-    if (a.chivi) {
+    if (k_chivi) {
       if (rows) {
         const double wm = wave_max_dpp(mloc);
         if (lane == 0) s_max[wid] = wm;
@@ -1378,25 +1392,25 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
       const double c = colsum(mean ? p : DMAX + (p - D));
       const double sgp = s_sg[mean ? 0 : p - D];
       double gp;
-      if (!a.chivi) {
+      if (!k_chivi) {
         const double cd = c * inv_dN;
         gp = mean ? -cd : -(1.0 + sgp * cd);
       } else {
         const double Ssum = colsum(2 * DMAX);
         gp = (mean ? a.alpha * c : a.alpha * (sgp * c + Ssum)) * inv_dN;
       }
-      if (a.emit_grad) {
+      if (k_emit) {
         a.grad[(long long)prob * P + p] = gp;
       } else {
         double nl;
-        if (a.opt != 0) {
+        if (k_opt != 0) {
           // RMSProp-IA (vb.py:436-453) / Adam-IA (vb.py:606-617): state in
           // s_ring[0..P) (second moment) and s_ring[P..2P) (first moment); the
           // history keeps the PRE-update parameters of the last n_hist iterations.
           const double old = s_lam[p];
           if (i >= a.hist_start) a.hist[((long long)prob * a.n_hist + (i - a.hist_start)) * P + p] = old;
           const double g2 = __dmul_rn(gp, gp);
-          if (a.opt == 1) {
+          if (k_opt == 1) {
             const double sgs = i == 0 ? g2 : __dadd_rn(__dmul_rn(s_ring[p], 0.9), __dmul_rn(1.0 - 0.9, g2));
             s_ring[p] = sgs;
             nl = __dsub_rn(old, __dmul_rn(a.lr.at(i), gp) / sqrt(__dadd_rn(a.eps, sgs)));
@@ -1439,15 +1453,15 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
     if (RO != 1 && tid == val_tid) {
       double val;
       if constexpr (kPF) sl = s_sl;
-      if (!a.chivi) {
+      if (!k_chivi) {
         // entropy uses the pre-update lam: sum_d log sigma_d (the sampled log q of
         // klvi_pd lacks it: -(mean (log p - log q)) = -(st / N + sl))
         const double st = colsum(2 * DMAX);
-        val = a.pd ? -(st / dN + sl) : -(c0 + sl + st / dN);
+        val = k_pd ? -(st / dN + sl) : -(c0 + sl + st / dN);
       } else {
         val = log(colsum(2 * DMAX) / dN) / a.alpha + (M + sl);
       }
-      a.values[(long long)prob * a.n_iters + (a.emit_grad ? 0 : i)] = val;
+      a.values[(long long)prob * a.n_iters + (k_emit ? 0 : i)] = val;
     }
     if constexpr (!HOST) {
       // the draw waves' last item round of step s + 1 runs here, beside the
@@ -1480,7 +1494,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
     // barrier: the slots it reads were written by earlier steps' updates (before
     // their end barriers), and the update of step s reads s_qold after the
     // reduction barrier.
-    const int nbar = a.chivi ? 3 : 2;
+    const int nbar = k_chivi ? 3 : 2;
     int cslot = slot;
     for (int s = 0; s < a.n_steps; ++s) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1533,13 +1547,13 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
 #ifdef VB_BLOCK_TS
   if (prob == 0 && tid == 0 && a.n_steps > 0)
     printf("BLOCKTS D=%d N=%d NT=%d RW=%d chivi=%d steps=%d cyc/step=%.0f | rows %.0f max+bar %.0f rs %.0f bar %.0f upd %.0f bar %.0f\n",
-           D, N, NT, RW, a.chivi ? 1 : 0, a.n_steps, (double)(clock64() - tb0) / a.n_steps,
+           D, N, NT, RW, k_chivi ? 1 : 0, a.n_steps, (double)(clock64() - tb0) / a.n_steps,
            (double)bt[0] / a.n_steps, (double)bt[1] / a.n_steps, (double)bt[2] / a.n_steps,
            (double)bt[3] / a.n_steps, (double)bt[4] / a.n_steps, (double)bt[5] / a.n_steps);
 #endif
 #undef VB_BT
 
-  if (!a.emit_grad) {
+  if (!k_emit) {
     for (int p = tid; p < P; p += NT) lam_g[p] = s_lam[p];
     for (int q = tid; q < W * P; q += NT) ring_g[q] = s_ring[q];
   }
@@ -2288,8 +2302,14 @@ static void sep_split(SepArgs& a) {
 
 template <class TGT, bool TFAM, bool HOST, bool REG>
 static void sep_launch(const SepArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 4, REG>), dim3(a.blocks2 + a.blocks1), dim3(256),
-                     0, s, a);
+  // the optimisation launches (no emitted gradient, plain KLVI value) take the
+  // instance with those flags compiled in (sep_kernel's ADV)
+  if (!a.emit_grad && a.pd == 0)
+    hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 4, REG, true>), dim3(a.blocks2 + a.blocks1),
+                       dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((sep_kernel<TGT, TFAM, HOST, 4, REG>), dim3(a.blocks2 + a.blocks1), dim3(256),
+                       0, s, a);
 }
 
 template <class TGT>
@@ -2337,10 +2357,20 @@ static hipError_t block_dispatch_dm(int fam, bool host, const BlockArgs& a, int 
   const bool pf = host && L.pf;
   if constexpr (DM <= kBlockSplitMaxD) {
     if (host && L.split) {
-      if (fam == 1)
-        hipLaunchKernelGGL((block_kernel<TGT, true, true, DM, true, true>), grid, block, 0, s, a);
-      else
-        hipLaunchKernelGGL((block_kernel<TGT, false, true, DM, true, true>), grid, block, 0, s, a);
+      // the benchmark modes with their flags compiled in (block_kernel's HOT)
+      const int hot = (!a.emit_grad && a.opt == 0 && !a.pd) ? (a.chivi ? 2 : 1) : 0;
+#define VB_SPLIT_LAUNCH(F, H) \
+  hipLaunchKernelGGL((block_kernel<TGT, F, true, DM, true, true, H>), grid, block, 0, s, a)
+      if (fam == 1) {
+        if (hot == 1) VB_SPLIT_LAUNCH(true, 1);
+        else if (hot == 2) VB_SPLIT_LAUNCH(true, 2);
+        else VB_SPLIT_LAUNCH(true, 0);
+      } else {
+        if (hot == 1) VB_SPLIT_LAUNCH(false, 1);
+        else if (hot == 2) VB_SPLIT_LAUNCH(false, 2);
+        else VB_SPLIT_LAUNCH(false, 0);
+      }
+#undef VB_SPLIT_LAUNCH
       return hipGetLastError();
     }
   }
