@@ -7,4 +7,4 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 VIABEL_AMD_LIB=$PWD/viabel_amd/libviabel_amd_ts.so timeout -k 10 120 python -u scripts/block_phase_cfg12.py \
   > gpurun_out/block_ts.log 2>&1 || { tail -20 gpurun_out/block_ts.log; exit 1; }
-grep -E "==|BLOCKTS" gpurun_out/block_ts.log | head -40
+grep -E "==|BLOCKTS|COPYTS" gpurun_out/block_ts.log | head -60

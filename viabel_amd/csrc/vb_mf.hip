@@ -1496,35 +1496,102 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
     // reduction barrier.
     const int nbar = k_chivi ? 3 : 2;
     int cslot = slot;
+#ifdef VB_BLOCK_TS
+    // the copy wave's own marks (lane 0 of problem 0): prefetch landed, prefetch
+    // issued, window sums done, log-sigma sum + LDS drained, first barrier left
+    unsigned long long ct[5] = {0, 0, 0, 0, 0}, tc = clock64();
+#define VB_CT(k) do { const unsigned long long t_ = clock64(); ct[k] += t_ - tc; tc = t_; } while (0)
+#else
+#define VB_CT(k) do {} while (0)
+#endif
     for (int s = 0; s < a.n_steps; ++s) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      VB_CT(0);
       if (s + 2 < a.n_steps) pf_issue(s + 2);
-      if (qpre && lane < P) {
-        const long long i = a.step0 + s;
-        const int cnt = (i + 1 < W) ? (int)(i + 1) : W;
-        const int oldest = (cnt < W || cslot + 1 == W) ? 0 : cslot + 1;
-        double q = 0.0;
-        for (int k = 0; k + 1 < cnt; ++k) {
-          int Lk = oldest + k;
-          if (Lk >= W) Lk -= W;
-          const double t = s_ring[Lk * P + lane];
-          q = __dadd_rn(q, __dmul_rn(t, t));
+      VB_CT(1);
+      // the window sums (s_qold) and sum_d log sigma_d (s_sl) of step s: both are first
+      // read after the step's reduction barrier (CHIVI form, below)
+      auto presums = [&]() __attribute__((always_inline)) {
+        if (qpre && lane < P) {
+          const long long i = a.step0 + s;
+          const int cnt = (i + 1 < W) ? (int)(i + 1) : W;
+          const int oldest = (cnt < W || cslot + 1 == W) ? 0 : cslot + 1;
+          double q = 0.0;
+          for (int k = 0; k + 1 < cnt; ++k) {
+            int Lk = oldest + k;
+            if (Lk >= W) Lk -= W;
+            const double t = s_ring[Lk * P + lane];
+            q = __dadd_rn(q, __dmul_rn(t, t));
+          }
+          s_qold[lane] = q;
         }
-        s_qold[lane] = q;
-      }
-      cslot = cslot + 1 == W ? 0 : cslot + 1;
-      if (lane == 0) {   // sum_d log sigma_d for the value (same order as the rows' loop)
-        double sl = 0.0;
+        VB_CT(2);
+        cslot = cslot + 1 == W ? 0 : cslot + 1;
+        if (lane == 0) {   // sum_d log sigma_d for the value (same order as the rows' loop)
+          double sl = 0.0;
+  #pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            const double l = s_lam[D + d];
+            sl += d < D ? l : 0.0;
+          }
+          s_sl = sl;
+        }
+      };
+      if (k_chivi) {
+        // CHIVI: the sums run after the block-max barrier, beside the rows' rescale and
+        // reduce-scatter, instead of holding that barrier (the copy wave arrived last
+        // there: profiles/r05/copy_wave_ts.log); s_lam is still the pre-update lambda
+        // until the reduction barrier.  (KLVI keeps them before its first barrier, the
+        // reduction one, in a separate copy of the code: sharing one lambda changed the
+        // KLVI instances' code and cost config 1 3 %.)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        VB_CT(3);
+        __builtin_amdgcn_s_barrier();   // the block-max barrier
+        VB_CT(4);
+        presums();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      } else {
+        if (qpre && lane < P) {
+          const long long i = a.step0 + s;
+          const int cnt = (i + 1 < W) ? (int)(i + 1) : W;
+          const int oldest = (cnt < W || cslot + 1 == W) ? 0 : cslot + 1;
+          double q = 0.0;
+          for (int k = 0; k + 1 < cnt; ++k) {
+            int Lk = oldest + k;
+            if (Lk >= W) Lk -= W;
+            const double t = s_ring[Lk * P + lane];
+            q = __dadd_rn(q, __dmul_rn(t, t));
+          }
+          s_qold[lane] = q;
+        }
+        VB_CT(2);
+        cslot = cslot + 1 == W ? 0 : cslot + 1;
+        if (lane == 0) {   // sum_d log sigma_d for the value (same order as the rows' loop)
+          double sl = 0.0;
 #pragma unroll
-        for (int d = 0; d < DMAX; ++d) {
-          const double l = s_lam[D + d];
-          sl += d < D ? l : 0.0;
+          for (int d = 0; d < DMAX; ++d) {
+            const double l = s_lam[D + d];
+            sl += d < D ? l : 0.0;
+          }
+          s_sl = sl;
         }
-        s_sl = sl;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        VB_CT(3);
+        __builtin_amdgcn_s_barrier();   // the reduction barrier
+        VB_CT(4);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      for (int b = 0; b < nbar; ++b) __builtin_amdgcn_s_barrier();
+      for (int b = 1; b < nbar; ++b) __builtin_amdgcn_s_barrier();
+#ifdef VB_BLOCK_TS
+      tc = clock64();   // (the step's later barriers not counted)
+#endif
     }
+#ifdef VB_BLOCK_TS
+    if (prob == 0 && lane == 0 && a.n_steps > 0)
+      printf("COPYTS steps=%d | vmcnt wait %.0f issue %.0f window sums %.0f log-sigma sum + drain %.0f first barrier wait %.0f\n",
+             a.n_steps, (double)ct[0] / a.n_steps, (double)ct[1] / a.n_steps, (double)ct[2] / a.n_steps,
+             (double)ct[3] / a.n_steps, (double)ct[4] / a.n_steps);
+#endif
+#undef VB_CT
   } else if (split) {
     if constexpr (!HOST && !TFAM) {
       if (row_wave) {
