@@ -895,6 +895,8 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
   __shared__ double s_e[HOST ? 1 : kBlockDrawLds + DMAX];  // + slack for the row loads
   __shared__ __attribute__((aligned(16))) double s_pf[HOST && PF ? kBlockPfLds + kBlockDMax : 1];
   __shared__ double s_qold[HOST && PF ? 2 * DMAX : 1];   // window sums without the newest slot
+  // KLVI (qnext): the window sums of step s without its two newest slots, by step parity
+  __shared__ double s_qpre[2][HOST && PF ? 2 * DMAX : 1];
   __shared__ double s_sl;   // copy-wave layout: sum_d log sigma_d of the step's lam
   if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
 
@@ -949,6 +951,11 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
   // parameter while the rows run (same order, oldest first), so the update adds
   // only the newest square (the same bits as the whole loop)
   const bool qpre = kPF && k_opt == 0 && !k_emit && W >= 1 && W <= kBlockQpreMaxW;
+  // KLVI: the copy wave sums step s + 1's window (but its newest slot) after step s's
+  // reduction barrier, beside the update, instead of before that barrier, which it held
+  // (profiles/r05/copy_wave_ts.log); the update adds the previous gradient's square
+  // (gprev) and its own -- the same additions in the same order
+  const bool qnext = qpre && !k_chivi && W >= 2;
   double* lam_g = a.lam + (long long)prob * P;
   double* ring_g = a.ring ? a.ring + (long long)prob * W * P : nullptr;
 
@@ -1040,6 +1047,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
 #endif
 
   int slot = W > 0 ? (int)(a.step0 % W) : 0;  // window ring slot of step i (i % W)
+  double gprev = 0.0;   // (qnext) the update thread's gradient of the previous step
   // split rows: the target's per-lane constants, made once (Row::lane_const)
   double lk[2 * DH] = {};
   if constexpr (SPLIT) Row::template lane_const<DH>(tid & 1, lk);
@@ -1429,7 +1437,11 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
           s_ring[slot * P + p] = gp;
           double q = 0.0;
           if (qpre) {
-            q = __dadd_rn(s_qold[p], __dmul_rn(gp, gp));
+            if (qnext && s > 0)
+              q = __dadd_rn(__dadd_rn(s_qpre[s & 1][p], __dmul_rn(gprev, gprev)), __dmul_rn(gp, gp));
+            else
+              q = __dadd_rn(s_qold[p], __dmul_rn(gp, gp));
+            gprev = gp;
           } else {
             const int cnt = (i + 1 < W) ? (int)(i + 1) : W;
             const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;  // (i + 1) % W
@@ -1551,7 +1563,7 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
         presums();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       } else {
-        if (qpre && lane < P) {
+        if (qpre && lane < P && !(qnext && s > 0)) {
           const long long i = a.step0 + s;
           const int cnt = (i + 1 < W) ? (int)(i + 1) : W;
           const int oldest = (cnt < W || cslot + 1 == W) ? 0 : cslot + 1;
@@ -1579,6 +1591,24 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
         VB_CT(3);
         __builtin_amdgcn_s_barrier();   // the reduction barrier
         VB_CT(4);
+        if (qnext && lane < P && s + 1 < a.n_steps) {
+          // step s + 1's older window slots but the newest (step s's, written by the
+          // update running now), oldest first; cslot is already step s + 1's slot.  The
+          // slots read were written by step s - 1's update or earlier; step s's update
+          // writes the slot of step s + 1 - W, which is not among them.
+          const long long i1 = a.step0 + s + 1;
+          const int cnt = (i1 + 1 < W) ? (int)(i1 + 1) : W;
+          const int oldest = (cnt < W || cslot + 1 == W) ? 0 : cslot + 1;
+          double q = 0.0;
+          for (int k = 0; k + 2 < cnt; ++k) {
+            int Lk = oldest + k;
+            if (Lk >= W) Lk -= W;
+            const double t = s_ring[Lk * P + lane];
+            q = __dadd_rn(q, __dmul_rn(t, t));
+          }
+          s_qpre[(s + 1) & 1][lane] = q;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
       }
       for (int b = 1; b < nbar; ++b) __builtin_amdgcn_s_barrier();
 #ifdef VB_BLOCK_TS
@@ -1656,20 +1686,26 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
   for (int d = tid; d < D; d += NT) s_sg[d] = 1.0;
   __syncthreads();
   int slot = 0;
-  double val = 0.0;
+  double val = 0.0, gprev = 0.0;
+  const double inv_dN = 1.0 / dN;
   for (int s = 0; s < n_steps; ++s) {
     double sl = 0.0;
-    if (copy || !has_copy) {
+    if (!has_copy) {
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) sl += d < D ? s_lam[D + d] : 0.0;
     }
-    if (copy) {
+    // (block_kernel's copy wave: KLVI sums the whole window before the reduction
+    // barrier only at a launch's first step and the next step's window but its newest
+    // slot after it (qnext); CHIVI sums after the block-max barrier)
+    auto copy_sums = [&](bool whole) {
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) sl += d < D ? s_lam[D + d] : 0.0;
       if (lane == 0) s_sl = sl;
       if (qpre && lane < P) {
         const int cnt = (s + 1 < W) ? s + 1 : W;
         const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;
         double q = 0.0;
-        for (int k = 0; k + 1 < cnt; ++k) {
+        for (int k = 0; k + (whole ? 1 : 2) < cnt; ++k) {
           int Lk = oldest + k;
           if (Lk >= W) Lk -= W;
           const double v = s_ring[Lk * P + lane];
@@ -1677,7 +1713,8 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
         }
         s_qold[lane] = q;
       }
-    }
+    };
+    if (copy && !chivi && s == 0) copy_sums(true);
     // accumulators: a cheap function of the last update (one LDS read and K adds; a
     // per-k read of s_lam[k % P] spent an integer division per accumulator and made
     // the floor grow with K by ~0.06 us per accumulator)
@@ -1692,6 +1729,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
         if (lane == 0) s_max[wid] = wm;
       }
       __syncthreads();
+      if (copy) copy_sums(true);
       double mq[kBlockMaxRowWaves];
 #pragma unroll
       for (int q = 0; q < kBlockMaxRowWaves; ++q) mq[q] = s_max[q];
@@ -1701,6 +1739,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
     }
     if (row_wave) wave_reduce_scatter<K>(acc, s_red[wid]);
     __syncthreads();
+    if (copy && !chivi) copy_sums(false);
     auto colsum = [&](int k) {   // as block_kernel: each reader sums its column
       double tq[kBlockMaxRowWaves];
 #pragma unroll
@@ -1713,12 +1752,14 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
     if (tid < P) {
       const int p = tid;
       const bool mean = p < D;
-      const double cd = colsum(mean ? p : DMAX + (p - D)) / dN;
+      const double cd = colsum(mean ? p : DMAX + (p - D)) * inv_dN;
       const double gp = mean ? -cd : -(1.0 + s_sg[mean ? 0 : p - D] * cd);
       s_ring[slot * P + p] = gp;
       double q = 0.0;
       if (qpre) {
-        q = __dadd_rn(s_qold[p], __dmul_rn(gp, gp));
+        q = (!chivi && s > 0) ? __dadd_rn(__dadd_rn(s_qold[p], __dmul_rn(gprev, gprev)), __dmul_rn(gp, gp))
+                              : __dadd_rn(s_qold[p], __dmul_rn(gp, gp));
+        gprev = gp;
       } else {
         const int cnt = (s + 1 < W) ? s + 1 : W;
         const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;
@@ -1729,7 +1770,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
           q = __dadd_rn(q, __dmul_rn(v, v));
         }
       }
-      const double nl = __dsub_rn(s_lam[p], __dmul_rn(1e-6, gp) / sqrt(__dadd_rn(0.1, q)));
+      const double nl = __dsub_rn(s_lam[p], __dmul_rn(1e-6, gp) * rsqrt_pos(__dadd_rn(0.1, q)));
       s_lam[p] = nl;
       if (p >= D) s_sg[p - D] = exp_fast(nl);
     }
