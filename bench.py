@@ -764,11 +764,17 @@ def main():
     # one GPU per rank (LOCAL_RANK mod the visible devices, as restarts.bind_local_device);
     # collectives over nccl (= RCCL) whenever every local rank has a GPU of its own;
     # more local ranks than GPUs (a rehearsal of the N > 1 path on a one-GPU box,
-    # scripts/gpu_rehearse_ranks.sh) use gloo, since RCCL refuses two ranks on one GPU
+    # scripts/gpu_rehearse_ranks.sh) use gloo, since RCCL refuses two ranks on one GPU.
+    # A launcher that does not export LOCAL_WORLD_SIZE gets nccl (the production
+    # case: one rank per GPU); VIABEL_AMD_BENCH_BACKEND overrides the choice.
     global COLL_CPU
     n_dev = max(1, torch.cuda.device_count())
-    local_world = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
-    backend = 'nccl' if local_world <= n_dev else 'gloo'
+    lws = os.environ.get('LOCAL_WORLD_SIZE')
+    backend = 'nccl' if lws is None or int(lws) <= n_dev else 'gloo'
+    backend = os.environ.get('VIABEL_AMD_BENCH_BACKEND', backend)
+    if backend not in ('nccl', 'gloo'):
+        raise ValueError('VIABEL_AMD_BENCH_BACKEND must be nccl or gloo')
+    local_world = int(lws) if lws is not None else world
     local_dev = local % n_dev
     if world > 1:
         import torch.distributed as dist
@@ -887,8 +893,3 @@ if __name__ == '__main__':
         os.environ.setdefault(k, '1')
     os.environ.setdefault('VIABEL_AMD_PROGRESS', '0')     # no progress bars in the legs
     main()
-    # the library's runs, contexts and streams (the CU-masked pre-draw ones included)
-    # are released while the HIP runtime is alive: under rocprofv3 the process's
-    # static teardown has crashed with them still open after a complete run
-    from viabel_amd import _native
-    _native.release_all()

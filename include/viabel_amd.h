@@ -26,6 +26,8 @@
  *                          viabel/vb.py:392-712 (the RMSProp-IA / Adam-IA updates)
  *   vb_rhat                viabel/functions.py:8-65 (compute_R_hat and its windowed /
  *                          halfway drivers)
+ *   vb_rhat_stats / vb_rhat_combine  viabel/functions.py:8-31 split at the chain axis,
+ *                          for the chains of viabel/vb.py:417-421 sharded over ranks
  *   vb_iterate_average     viabel/functions.py:68-77 (stochastic_iterate_averaging)
  *   vb_adagrad_update      viabel/vb.py:364-374 (one adagrad step for a foreign objective)
  *   vb_adagrad_update_scaled  viabel/vb.py:364-374 with has_log_norm (grad_scale, :371-373)
@@ -289,6 +291,19 @@ int vb_ia_update(vb_ctx* ctx, int32_t optimizer, int64_t P, double* lam, const d
 int vb_rhat(vb_ctx* ctx, const double* chains, int64_t n_chains, int64_t n_iters, int64_t P,
             int64_t n_jobs, const int64_t* job_start, const int64_t* job_len,
             double* var_hat_out, double* rhat_out);
+/* The two stages of vb_rhat, for chains held by different processes
+ * (viabel/vb.py:417-421's chain loop sharded over ranks, then
+ * viabel/functions.py:8-52 on the union).  vb_rhat_stats: per segment j,
+ * half-chain i (= 2 chain + half) and parameter p, the half-chain mean and
+ * centred sum of squares, mean_out / ss_out [n_jobs][2 n_chains][P].
+ * vb_rhat_combine: R-hat of n_halves half-chains from those statistics
+ * (n_halves = 2 x the chains of all ranks, in chain order; job_len the segment
+ * lengths); the same bits as vb_rhat on the gathered chains. */
+int vb_rhat_stats(vb_ctx* ctx, const double* chains, int64_t n_chains, int64_t n_iters, int64_t P,
+                  int64_t n_jobs, const int64_t* job_start, const int64_t* job_len,
+                  double* mean_out, double* ss_out);
+int vb_rhat_combine(vb_ctx* ctx, const double* mean, const double* ss, int64_t n_halves, int64_t P,
+                    int64_t n_jobs, const int64_t* job_len, double* var_hat_out, double* rhat_out);
 /* stochastic_iterate_averaging: out [n - start][cols] = cumulative means of
  * x[start:, 0:cols] (row stride ld). */
 int vb_iterate_average(vb_ctx* ctx, const double* x, int64_t n, int64_t ld, int64_t cols,

@@ -40,10 +40,12 @@ def philox(ctr, key):
 
 
 def noise(seed, stream, step, n, dim, family='gauss', df=0.0):
-    """Standardized draws eps[n, dim] of one step (N(0,1) or t(df))."""
+    """Standardized draws eps[n, dim] of one step: N(0,1) ('gauss'), t(df) as
+    N / sqrt(Gamma) ('t', the estimators' draws) or by Bailey's polar method
+    ('t_polar', the log-weight draws of the t family)."""
     out = np.empty((n, dim))
     _lib().vbo_fill(seed, stream & 0xFFFFFF, step & 0xFFFFFFFF, n, dim,
-                    1 if family == 't' else 0, float(df),
+                    {'gauss': 0, 't': 1, 't_polar': 2}[family], float(df),
                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
     return out
 

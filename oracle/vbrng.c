@@ -15,6 +15,16 @@
  *  - t draw: sqrt(df/2) * gauss / sqrt(gamma(df/2)), the structure of numpy's
  *    legacy standard_t; gamma by Marsaglia & Tsang (2000), proposals from
  *    purposes 1..64 with 32-bit uniforms.
+ *  - polar t draw (family 2; the log-weight draws of the t family): Bailey,
+ *    "Polar generation of random variates with the t-distribution", Math. Comp.
+ *    62 (1994) 779-781.  Row n's candidates come from ONE stream of blocks,
+ *    attempt k = 0, 1, ... at counter (k, n, step, stream | 65 << 24), two
+ *    candidates per block, (x, y) words then (z, w) words: u, v = ((int32) word
+ *    + 1/2) 2^-31 in (-1, 1), W = fma(u, u, v v); W < 1 is accepted and becomes
+ *    the row's next variate T = u sqrt(df (W^(-2/df) - 1) / W), computed as
+ *    u sqrt(df expm1(-(2/df) log W) / W).  At most D + 64 attempts; a variate
+ *    still missing then is 0 (never observed: 2D + 128 candidates at acceptance
+ *    pi/4 leave fewer than D accepted with probability < 1e-30).
  */
 #include <math.h>
 #include <stdint.h>
@@ -93,10 +103,36 @@ static void gamma2(uint64_t seed, uint32_t stream, uint32_t pair, uint32_t n, ui
   }
 }
 
-/* standardized draws eps[n][D] for one step: family 0 = N(0,1), 1 = t(df) */
+#define VBO_POLAR_PURPOSE 65u
+
+static double polar_uniform(uint32_t w) { return ((double)(int32_t)w + 0.5) * 0x1p-31; }
+
+/* row n of polar t draws (see the header) into out[0..D) */
+static void polar_t_row(uint64_t seed, uint32_t stream, uint32_t n, uint32_t step, int64_t D,
+                        double df, double* out) {
+  int64_t cnt = 0;
+  for (int64_t i = 0; i < D; ++i) out[i] = 0.0;
+  for (uint32_t k = 0; cnt < D && (int64_t)k < D + 64; ++k) {
+    blk w = draw(seed, stream, k, n, step, VBO_POLAR_PURPOSE);
+    for (int c = 0; c < 2 && cnt < D; ++c) {
+      double u = polar_uniform(w.v[2 * c]), v = polar_uniform(w.v[2 * c + 1]);
+      double W = fma(u, u, v * v);
+      if (!(W < 1.0)) continue;
+      double e = expm1((-2.0 / df) * log(W));
+      out[cnt++] = u * sqrt(df * e / W);
+    }
+  }
+}
+
+/* standardized draws eps[n][D] for one step: family 0 = N(0,1), 1 = t(df),
+ * 2 = polar t(df) (the log-weight draws) */
 void vbo_fill(uint64_t seed, uint32_t stream, uint32_t step, int64_t nrows, int64_t D, int family,
               double df, double* eps) {
   int64_t npairs = (D + 1) / 2;
+  if (family == 2) {
+    for (int64_t r = 0; r < nrows; ++r) polar_t_row(seed, stream, (uint32_t)r, step, D, df, eps + r * D);
+    return;
+  }
   for (int64_t r = 0; r < nrows; ++r) {
     for (int64_t j = 0; j < npairs; ++j) {
       double z0, z1;

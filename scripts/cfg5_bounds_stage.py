@@ -26,7 +26,3 @@ def main():
 
 if __name__ == '__main__':
     main()
-    # release the library's objects while the HIP runtime is alive (under
-    # rocprofv3 this run once crashed in the process's static teardown)
-    from viabel_amd import _native
-    _native.release_all()

@@ -136,6 +136,10 @@ _SIGNATURES = {
                         ctypes.c_int),
     'vb_rhat': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                  ctypes.c_int64, c_int64_p, c_int64_p, c_double_p, c_double_p], ctypes.c_int),
+    'vb_rhat_stats': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                       ctypes.c_int64, c_int64_p, c_int64_p, c_double_p, c_double_p], ctypes.c_int),
+    'vb_rhat_combine': ([ctypes.c_void_p, c_double_p, c_double_p, ctypes.c_int64, ctypes.c_int64,
+                         ctypes.c_int64, c_int64_p, c_double_p, c_double_p], ctypes.c_int),
     'vb_iterate_average': ([ctypes.c_void_p, c_double_p, ctypes.c_int64, ctypes.c_int64,
                             ctypes.c_int64, ctypes.c_int64, c_double_p], ctypes.c_int),
 }
@@ -225,20 +229,13 @@ class Context:
         self.handle = None
 
 
-# At interpreter exit native objects are released by process teardown, not by
-# finalizers: a finalizer running after the HIP / rocBLAS runtimes' own static
-# destructors would call into torn-down libraries.
+# At interpreter exit every context is destroyed while the HIP runtime is alive
+# (release_all, registered with atexit below); native objects still referenced
+# then are left to process teardown: their finalizers run after the HIP / rocBLAS
+# runtimes' own static destructors may have, so they skip the native release.
+# The library also releases what live contexts hold from its own exit handler
+# (vb_capi.hip release_live_contexts) for callers that never destroy them.
 _SHUTDOWN = [False]
-
-
-@atexit.register
-def _mark_shutdown():
-    for c in list(_ctx.values()):
-        try:
-            c.synchronize()
-        except Exception:
-            pass
-    _SHUTDOWN[0] = True
 
 
 def shutting_down():
@@ -246,25 +243,30 @@ def shutting_down():
 
 
 def release_all():
-    """At the end of a program: collect the objects no longer referenced (their
-    native release runs first), then synchronize and destroy every context (its
-    streams, the CU-masked pre-draw streams included) while the HIP runtime is
-    still alive.  The library is not used afterwards (later finalizers skip their
-    native release).  Under a profiler, the process's teardown has crashed with
-    such streams still alive after a complete run."""
+    """Collect the objects no longer referenced (their native release runs first),
+    then synchronize and destroy every context (its stream, the CU-masked pre-draw
+    streams and the full-rank workspace) while the HIP runtime is still alive.
+    The library is not used afterwards (later finalizers skip their native
+    release).  Runs at interpreter exit; a program may call it earlier.  Round 5:
+    with CU-masked streams still alive at exit, the process's teardown crashed
+    under rocprofv3."""
     import gc
     gc.collect()
     for d, c in list(_ctx.items()):
         try:
             c.synchronize()
+        except Exception:
+            pass
+        try:
             if c.handle and _lib is not None:
                 _lib.vb_ctx_destroy(c.handle)
         finally:
             c.handle = None
-            del _ctx[d]
-    # native objects still referenced are left to process teardown (their finalizers
-    # must not call into a destroyed context)
+            _ctx.pop(d, None)
     _SHUTDOWN[0] = True
+
+
+atexit.register(release_all)
 
 
 _ctx = {}

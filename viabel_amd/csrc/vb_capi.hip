@@ -15,7 +15,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -100,6 +102,30 @@ struct DevBuf {
   double* d() const { return static_cast<double*>(p); }
 };
 
+// Pinned host memory (hipHostMalloc), grown on demand, freed with its owner.
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int reserve(size_t bytes) {
+    if (bytes <= cap) return VB_OK;
+    release();
+    hipError_t e = hipHostMalloc(&p, bytes);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+      return fail(VB_ENOMEM, "hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    }
+    cap = bytes;
+    return VB_OK;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  ~PinnedBuf() { release(); }
+};
+
 }  // namespace
 
 int vbk::vb_set_error(int code, const char* fmt, ...) {
@@ -123,14 +149,67 @@ struct vb_ctx {
   int pd_ready = -1;
   hipStream_t pd_stream = nullptr, blk_stream = nullptr;
   hipEvent_t pd_ev[6] = {};
-  ~vb_ctx() {
+  PinnedBuf psis_flags;  // the PSIS fast select's per-column flags, read by the host
+  // the resources the context created besides its stream: the full-rank workspace
+  // (rocBLAS / rocSOLVER handles, buffers), the CU-masked pre-draw streams and their
+  // events.  Run by vb_ctx_destroy and, for contexts still alive at exit, by the
+  // library's own exit handler (release_live_contexts) before the HIP runtime tears
+  // itself down.  Idempotent; the context stays usable (they are made again on use).
+  void release_side() {
+    if (pd_stream) (void)hipStreamSynchronize(pd_stream);
+    if (blk_stream) (void)hipStreamSynchronize(blk_stream);
     vbk::fr_work_destroy(fr);
-    for (hipEvent_t& e : pd_ev)
+    fr = nullptr;
+    for (hipEvent_t& e : pd_ev) {
       if (e) (void)hipEventDestroy(e);
+      e = nullptr;
+    }
     if (pd_stream) (void)hipStreamDestroy(pd_stream);
     if (blk_stream) (void)hipStreamDestroy(blk_stream);
+    pd_stream = blk_stream = nullptr;
+    pd_ready = -1;
+    psis_flags.release();
   }
+  ~vb_ctx() { release_side(); }
 };
+
+namespace {
+
+// Contexts alive now.  A process that exits with contexts it never destroyed (a
+// Python program whose objects are still referenced, a C program without
+// vb_ctx_destroy) would otherwise leave their CU-masked streams and rocBLAS
+// handles to the process's static teardown, after the HIP runtime's: under
+// rocprofv3 that order crashed at exit (round 5).  The handler is registered with
+// std::atexit after the first context exists, i.e. after the HIP runtime has
+// initialised, so it runs before the runtime's own exit-time teardown.
+std::mutex g_ctx_mu;
+std::set<vb_ctx*>* g_live = nullptr;
+
+void release_live_contexts() {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  if (!g_live) return;
+  for (vb_ctx* c : *g_live) {
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->release_side();
+  }
+}
+
+void register_ctx(vb_ctx* c) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  if (!g_live) {
+    g_live = new std::set<vb_ctx*>();  // never freed: read by the exit handler
+    std::atexit(release_live_contexts);
+  }
+  g_live->insert(c);
+}
+
+void unregister_ctx(vb_ctx* c) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  if (g_live) g_live->erase(c);
+}
+
+}  // namespace
 
 namespace {
 
@@ -551,14 +630,17 @@ int vb_ctx_create(int device, void* hip_stream, vb_ctx** out) {
     }
     c->own_stream = true;
   }
+  register_ctx(c);
   *out = c;
   return VB_OK;
 }
 
 int vb_ctx_destroy(vb_ctx* c) {
   if (!c) return VB_OK;
+  unregister_ctx(c);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  c->release_side();
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return VB_OK;
@@ -1718,6 +1800,7 @@ static int psislw_impl(vb_ctx* c, const double* lw, int64_t n, int64_t m, long l
   VB_TRY(dti.stage(c, 4, reinterpret_cast<long long*>(tail_idx_out),
                    tail_idx_out ? (size_t)tail_cap * m : 0));
   VB_TRY(c->slot[6].reserve(sizeof(unsigned) * (size_t)group));   // fast-select flags
+  VB_TRY(c->psis_flags.reserve(sizeof(unsigned) * (size_t)group));  // their host copy
   VB_TRY(dnt.stage(c, 5, reinterpret_cast<long long*>(n_tail_out), n_tail_out ? (size_t)m : 0));
   for (int64_t c0 = 0; c0 < m; c0 += group) {
     const int g = (int)std::min<int64_t>(group, m - c0);
@@ -1725,7 +1808,8 @@ static int psislw_impl(vb_ctx* c, const double* lw, int64_t n, int64_t m, long l
                              Mt, c->slot[3].p,
                              dk.d + c0, dti.d ? dti.d + (size_t)c0 * tail_cap : nullptr,
                              (long long)tail_cap, dnt.d ? dnt.d + c0 : nullptr, c->stream,
-                             static_cast<unsigned*>(c->slot[6].p)));
+                             static_cast<unsigned*>(c->slot[6].p),
+                             static_cast<unsigned*>(c->psis_flags.p)));
   }
   VB_TRY(dout.finish(c));
   VB_TRY(dk.finish(c));
@@ -1807,6 +1891,32 @@ int vb_gpinv(vb_ctx* c, const double* p, int64_t n, double k, double sigma, doub
   return sync(c);
 }
 
+// R-hat segments: job_len even, >= 2, inside [0, n_iters)
+static int check_rhat_jobs(int64_t n_iters, int64_t n_jobs, const int64_t* job_start,
+                           const int64_t* job_len) {
+  for (int64_t j = 0; j < n_jobs; ++j) {
+    if (job_len[j] < 2 || job_len[j] % 2 || (job_start && (job_start[j] < 0 ||
+                                                           job_start[j] + job_len[j] > n_iters)))
+      return fail(VB_EINVAL, "R-hat segment %lld: [%lld, +%lld) invalid for %lld iterations",
+                  (long long)j, job_start ? (long long)job_start[j] : 0LL, (long long)job_len[j],
+                  (long long)n_iters);
+  }
+  return VB_OK;
+}
+
+// the segments' starts and lengths in device memory (slot 1): [start | len]
+static int rhat_jobs_dev(vb_ctx* c, int64_t n_jobs, const int64_t* job_start,
+                         const int64_t* job_len, long long** dj) {
+  VB_TRY(c->slot[1].reserve(sizeof(long long) * 2 * n_jobs));
+  *dj = static_cast<long long*>(c->slot[1].p);
+  if (job_start)
+    VB_HIP(hipMemcpyAsync(*dj, job_start, sizeof(long long) * n_jobs, hipMemcpyHostToDevice,
+                          c->stream));
+  VB_HIP(hipMemcpyAsync(*dj + n_jobs, job_len, sizeof(long long) * n_jobs, hipMemcpyHostToDevice,
+                        c->stream));
+  return VB_OK;
+}
+
 int vb_rhat(vb_ctx* c, const double* chains, int64_t n_chains, int64_t n_iters, int64_t P,
             int64_t n_jobs, const int64_t* job_start, const int64_t* job_len, double* var_hat_out,
             double* rhat_out) {
@@ -1814,23 +1924,70 @@ int vb_rhat(vb_ctx* c, const double* chains, int64_t n_chains, int64_t n_iters, 
   if (!chains || !job_start || !job_len || !rhat_out) return fail(VB_EINVAL, "null argument");
   if (n_chains < 1 || n_iters < 0 || P < 1 || n_jobs < 0) return fail(VB_EINVAL, "invalid sizes");
   if (n_jobs == 0) return VB_OK;
-  for (int64_t j = 0; j < n_jobs; ++j) {
-    if (job_len[j] < 2 || job_len[j] % 2 || job_start[j] < 0 || job_start[j] + job_len[j] > n_iters)
-      return fail(VB_EINVAL, "R-hat segment %lld: [%lld, +%lld) invalid for %lld iterations",
-                  (long long)j, (long long)job_start[j], (long long)job_len[j], (long long)n_iters);
-  }
+  VB_TRY(check_rhat_jobs(n_iters, n_jobs, job_start, job_len));
   In dc;
   VB_TRY(dc.stage(c, 0, chains, (size_t)n_chains * n_iters * P));
-  VB_TRY(c->slot[1].reserve(sizeof(long long) * 2 * n_jobs));
-  long long* dj = static_cast<long long*>(c->slot[1].p);
-  VB_HIP(hipMemcpyAsync(dj, job_start, sizeof(long long) * n_jobs, hipMemcpyHostToDevice, c->stream));
-  VB_HIP(hipMemcpyAsync(dj + n_jobs, job_len, sizeof(long long) * n_jobs, hipMemcpyHostToDevice,
-                        c->stream));
+  long long* dj;
+  VB_TRY(rhat_jobs_dev(c, n_jobs, job_start, job_len, &dj));
   Out dv, dr;
   VB_TRY(dv.stage(c, 2, var_hat_out, var_hat_out ? (size_t)n_jobs * P : 0));
   VB_TRY(dr.stage(c, 3, rhat_out, (size_t)n_jobs * P));
-  VB_HIP(vbk::launch_rhat(dc.d, n_chains, n_iters, P, n_jobs, dj, dj + n_jobs, dv.d, dr.d,
-                          c->stream));
+  // the same two stages as the rank-sharded path (vb_rhat_stats on each rank's
+  // chains, one gather, vb_rhat_combine), so both give the same bits
+  const size_t ns = (size_t)n_jobs * 2 * n_chains * P;
+  VB_TRY(c->slot[4].reserve(sizeof(double) * 2 * ns));
+  double* st = c->slot[4].d();
+  VB_HIP(vbk::launch_rhat_stats(dc.d, n_chains, n_iters, P, n_jobs, dj, dj + n_jobs, st, st + ns,
+                                c->stream));
+  VB_HIP(vbk::launch_rhat_combine(st, st + ns, 2 * n_chains, P, n_jobs, dj + n_jobs, dv.d, dr.d,
+                                  c->stream));
+  VB_TRY(dv.finish(c));
+  VB_TRY(dr.finish(c));
+  return sync(c);
+}
+
+int vb_rhat_stats(vb_ctx* c, const double* chains, int64_t n_chains, int64_t n_iters, int64_t P,
+                  int64_t n_jobs, const int64_t* job_start, const int64_t* job_len,
+                  double* mean_out, double* ss_out) {
+  VB_TRY(check_ctx(c));
+  if (!chains || !job_start || !job_len || !mean_out || !ss_out)
+    return fail(VB_EINVAL, "null argument");
+  if (n_chains < 1 || n_iters < 0 || P < 1 || n_jobs < 0) return fail(VB_EINVAL, "invalid sizes");
+  if (n_jobs == 0) return VB_OK;
+  VB_TRY(check_rhat_jobs(n_iters, n_jobs, job_start, job_len));
+  In dc;
+  VB_TRY(dc.stage(c, 0, chains, (size_t)n_chains * n_iters * P));
+  long long* dj;
+  VB_TRY(rhat_jobs_dev(c, n_jobs, job_start, job_len, &dj));
+  const size_t ns = (size_t)n_jobs * 2 * n_chains * P;
+  Out dm, dss;
+  VB_TRY(dm.stage(c, 2, mean_out, ns));
+  VB_TRY(dss.stage(c, 3, ss_out, ns));
+  VB_HIP(vbk::launch_rhat_stats(dc.d, n_chains, n_iters, P, n_jobs, dj, dj + n_jobs, dm.d, dss.d,
+                                c->stream));
+  VB_TRY(dm.finish(c));
+  VB_TRY(dss.finish(c));
+  return sync(c);
+}
+
+int vb_rhat_combine(vb_ctx* c, const double* mean, const double* ss, int64_t n_halves, int64_t P,
+                    int64_t n_jobs, const int64_t* job_len, double* var_hat_out, double* rhat_out) {
+  VB_TRY(check_ctx(c));
+  if (!mean || !ss || !job_len || !rhat_out) return fail(VB_EINVAL, "null argument");
+  if (n_halves < 2 || n_halves % 2 || P < 1 || n_jobs < 0) return fail(VB_EINVAL, "invalid sizes");
+  if (n_jobs == 0) return VB_OK;
+  VB_TRY(check_rhat_jobs(0, n_jobs, nullptr, job_len));
+  const size_t ns = (size_t)n_jobs * n_halves * P;
+  In dm, dss;
+  VB_TRY(dm.stage(c, 0, mean, ns));
+  VB_TRY(dss.stage(c, 4, ss, ns));
+  long long* dj;
+  VB_TRY(rhat_jobs_dev(c, n_jobs, nullptr, job_len, &dj));
+  Out dv, dr;
+  VB_TRY(dv.stage(c, 2, var_hat_out, var_hat_out ? (size_t)n_jobs * P : 0));
+  VB_TRY(dr.stage(c, 3, rhat_out, (size_t)n_jobs * P));
+  VB_HIP(vbk::launch_rhat_combine(dm.d, dss.d, n_halves, P, n_jobs, dj + n_jobs, dv.d, dr.d,
+                                  c->stream));
   VB_TRY(dv.finish(c));
   VB_TRY(dr.finish(c));
   return sync(c);

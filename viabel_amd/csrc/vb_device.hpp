@@ -133,6 +133,30 @@ __device__ __forceinline__ double exp_fast(double x) {
   return x != x ? x : res;
 }
 
+// expm1(x) for finite x >= 0, ~1 ulp: exp_fast's reduction x = k ln2 + r and its
+// polynomial, expm1(r) = r + r^2 q(r) (no cancellation near 0), then
+// 2^k (1 + expm1(r)) - 1 = 2^k expm1(r) + (2^k - 1) in one fma (2^k - 1 exact
+// for the k the callers reach, x <= 709)
+__device__ __forceinline__ double expm1_pos(double x) {
+  const double xc = fmin(x, 709.0);
+  const double k = rint(xc * 1.4426950408889634);
+  double r = fma(-k, 6.93147180369123816490e-01, xc);
+  r = fma(-k, 1.90821492927058770002e-10, r);
+  double q = 2.5105102509207056e-08;
+  q = hfma(q, r, 2.7620092546932737e-07);
+  q = hfma(q, r, 2.755725563278083e-06);
+  q = hfma(q, r, 2.4801521277219366e-05);
+  q = hfma(q, r, 0.00019841269874702037);
+  q = hfma(q, r, 0.0013888888917237376);
+  q = hfma(q, r, 0.008333333333326141);
+  q = hfma(q, r, 0.041666666666624025);
+  q = hfma(q, r, 0.1666666666666667);
+  q = hfma(q, r, 0.5000000000000001);
+  const double p = fma(r * r, q, r);
+  const double t = ldexp(1.0, (int)k);
+  return fma(t, p, t - 1.0);
+}
+
 // log1p(w) for w >= 0 finite, without tables: log(1 + w) by log_unit (any positive
 // normal argument) plus the rounding correction of 1 + w; ~1 ulp, ~35
 // instructions against the library's double-double ~100
@@ -378,6 +402,42 @@ __device__ __forceinline__ void gamma_pair(const Rng& rng, uint32_t pair, uint32
       }
     }
   }
+}
+
+// ---- polar t draws (the t family's log-weight draws) ------------------------
+// Bailey's polar method (Math. Comp. 62 (1994) 779-781; oracle/vbrng.c restates
+// it): row n's candidates come from one stream of Philox blocks, attempt k at
+// counter (k, n, step, stream | kPolarPurpose << 24), two candidates per block;
+// u, v = ((int32) word + 1/2) 2^-31, W = u^2 + v^2, W < 1 accepted as the row's
+// next variate T = u sqrt(df expm1(-(2/df) log W) / W).  One transcendental set per
+// accepted variate instead of a Box-Muller normal and Marsaglia-Tsang gamma
+// attempts (each a Box-Muller normal and two logs).  Attempts are capped at D + 64
+// (a variate still missing is 0; P < 1e-30).  Log q's log1p(T^2 / df) takes
+// T^2 / df = (u^2 / W) expm1(.) from the same terms (no division by df, no rounded T).
+constexpr uint32_t kPolarPurpose = 65u;
+
+__device__ __forceinline__ double polar_uniform(uint32_t w) {
+  return fma((double)(int32_t)w, 0x1p-31, 0x1p-32);
+}
+
+__device__ __forceinline__ double polar_w(uint32_t a, uint32_t b) {
+  const double u = polar_uniform(a), v = polar_uniform(b);
+  return fma(u, u, v * v);
+}
+
+// T of an accepted candidate (raw words a, b) and l1 = log1p(T^2 / df);
+// c2 = -2 / df (formed on the host as the oracle does)
+__device__ __forceinline__ double polar_t(uint32_t a, uint32_t b, double df, double c2,
+                                          const double2* ltab, double& l1) {
+  const double u = polar_uniform(a), v = polar_uniform(b);
+  const double W = fma(u, u, v * v);
+  const double em1 = expm1_pos(c2 * log_u01_tab(W, ltab));
+  double rw = __builtin_amdgcn_rcp(W);
+  rw = fma(rw, fma(-W, rw, 1.0), rw);
+  rw = fma(rw, fma(-W, rw, 1.0), rw);
+  const double c = em1 * rw;
+  l1 = log1p_pos_tab(u * u * c, ltab);       // T^2 / df = (u^2 / W) expm1
+  return u * sqrt_pos(df * c);
 }
 
 // ---- wave-level helpers (wave64) -------------------------------------------

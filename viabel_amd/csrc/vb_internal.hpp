@@ -96,6 +96,11 @@ hipError_t launch_row_mean(const double* hist, long long rows, long long P, long
                            double* out, hipStream_t s);
 
 // elementwise family helpers
+// polar t samples of a mean-field t family (the log-weight draws, vbrng.c family 2)
+// and their log q per row
+hipError_t launch_sample_polar(int D, long long m, const double* lam, double df, double t_const,
+                               uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* x,
+                               double* lq, hipStream_t s);
 hipError_t launch_sample(int fam, int D, long long n, const double* lam, double t_scale,
                          double shape, const double* noise, uint32_t k0, uint32_t k1,
                          uint32_t stream, uint32_t step, double* x, hipStream_t s);
@@ -132,9 +137,12 @@ hipError_t launch_ia_update(int opt, long long P, double* lam, const double* g, 
 // R-hat (functions.py:8-31) of chains [nc][n][P] (row stride P) over n_jobs
 // iteration segments [start, start + len) (len even): out [n_jobs][P] (var_hat
 // in var_out when non-null).
-hipError_t launch_rhat(const double* chains, long long nc, long long n, long long P,
-                       long long n_jobs, const long long* start, const long long* len,
-                       double* var_out, double* rhat_out, hipStream_t s);
+hipError_t launch_rhat_stats(const double* chains, long long nc, long long n, long long P,
+                             long long n_jobs, const long long* start, const long long* len,
+                             double* mean_out, double* ss_out, hipStream_t s);
+hipError_t launch_rhat_combine(const double* mean, const double* ss, long long nc2, long long P,
+                               long long n_jobs, const long long* len, double* var_out,
+                               double* rhat_out, hipStream_t s);
 // cumulative means (functions.py:68-77) of x[start:, cols] with row stride ld
 hipError_t launch_iterate_average(const double* x, long long n, long long ld, long long cols,
                                   long long start, double* out, hipStream_t s);
@@ -164,7 +172,8 @@ size_t psis_col_stride(long long tail_cap);      // scratch bytes per column of 
 hipError_t psis_columns(const double* lw, double* out, long long n, int m, long long rs,
                         long long cs, long long Mt, void* scratch, double* k_dev,
                         long long* tail_idx_dev, long long tail_cap, long long* n_tail_dev,
-                        hipStream_t s, unsigned* flag_dev = nullptr);
+                        hipStream_t s, unsigned* flag_dev = nullptr,
+                        unsigned* flag_host = nullptr);
 hipError_t psis_gpdfit(const double* x, long long n, void* scratch, double* out4,
                        double* ks_out, double* w_out, hipStream_t s);
 hipError_t psis_gpinv(const double* p, long long n, double k, double sigma, double* out,

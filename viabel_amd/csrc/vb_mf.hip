@@ -1672,7 +1672,9 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
   __shared__ double s_ring[64 * 2 * DMAX];
   __shared__ double s_red[kBlockMaxRowWaves][K];
   __shared__ double s_max[kBlockMaxRowWaves];
-  __shared__ double s_qold[2 * DMAX];
+  // window pre-sums, parity-indexed as block_kernel's s_qpre: KLVI's copy wave
+  // writes step s + 1's while the update threads read step s's
+  __shared__ double s_qpre[2][2 * DMAX];
   __shared__ double s_sl;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int NT = blockDim.x, P = 2 * D, RW = NT_rows / 64;
@@ -1684,37 +1686,36 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
   for (int p = tid; p < P; p += NT) s_lam[p] = 0.01 * p;
   for (int q = tid; q < W * P; q += NT) s_ring[q] = 0.0;
   for (int d = tid; d < D; d += NT) s_sg[d] = 1.0;
+  for (int p = tid; p < 2 * 2 * DMAX; p += NT) (&s_qpre[0][0])[p] = 0.0;
   __syncthreads();
   int slot = 0;
   double val = 0.0, gprev = 0.0;
   const double inv_dN = 1.0 / dN;
+  // ring slots of steps [first, first + n), oldest first, squared and summed into
+  // buf (the copy wave, lanes < P)
+  auto window_sum = [&](int first, int n, double* buf) {
+    if (qpre && lane < P) {
+      double q = 0.0;
+      int L = first % W;
+      for (int k = 0; k < n; ++k) {
+        const double v = s_ring[L * P + lane];
+        q = __dadd_rn(q, __dmul_rn(v, v));
+        L = L + 1 == W ? 0 : L + 1;
+      }
+      buf[lane] = q;
+    }
+  };
   for (int s = 0; s < n_steps; ++s) {
     double sl = 0.0;
-    if (!has_copy) {
+    if (!has_copy || copy) {
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) sl += d < D ? s_lam[D + d] : 0.0;
     }
-    // (block_kernel's copy wave: KLVI sums the whole window before the reduction
-    // barrier only at a launch's first step and the next step's window but its newest
-    // slot after it (qnext); CHIVI sums after the block-max barrier)
-    auto copy_sums = [&](bool whole) {
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) sl += d < D ? s_lam[D + d] : 0.0;
-      if (lane == 0) s_sl = sl;
-      if (qpre && lane < P) {
-        const int cnt = (s + 1 < W) ? s + 1 : W;
-        const int oldest = (cnt < W || slot + 1 == W) ? 0 : slot + 1;
-        double q = 0.0;
-        for (int k = 0; k + (whole ? 1 : 2) < cnt; ++k) {
-          int Lk = oldest + k;
-          if (Lk >= W) Lk -= W;
-          const double v = s_ring[Lk * P + lane];
-          q = __dadd_rn(q, __dmul_rn(v, v));
-        }
-        s_qold[lane] = q;
-      }
-    };
-    if (copy && !chivi && s == 0) copy_sums(true);
+    // (block_kernel's copy wave: sum_d log sigma_d before the reduction barrier;
+    // CHIVI sums the step's window but its newest slot after the block-max barrier,
+    // KLVI the NEXT step's window but its two newest slots after the reduction
+    // barrier, beside the update -- qnext)
+    if (copy && lane == 0) s_sl = sl;
     // accumulators: a cheap function of the last update (one LDS read and K adds; a
     // per-k read of s_lam[k % P] spent an integer division per accumulator and made
     // the floor grow with K by ~0.06 us per accumulator)
@@ -1729,7 +1730,10 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
         if (lane == 0) s_max[wid] = wm;
       }
       __syncthreads();
-      if (copy) copy_sums(true);
+      if (copy) {
+        const int cnt = s + 1 < W ? s + 1 : W;
+        window_sum(s + 1 - cnt, cnt - 1, s_qpre[s & 1]);
+      }
       double mq[kBlockMaxRowWaves];
 #pragma unroll
       for (int q = 0; q < kBlockMaxRowWaves; ++q) mq[q] = s_max[q];
@@ -1739,7 +1743,11 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
     }
     if (row_wave) wave_reduce_scatter<K>(acc, s_red[wid]);
     __syncthreads();
-    if (copy && !chivi) copy_sums(false);
+    if (copy && !chivi) {
+      // step s + 1's window (min(s + 2, W) slots) without steps s and s + 1
+      const int cnt1 = s + 2 < W ? s + 2 : W;
+      window_sum(s + 2 - cnt1, cnt1 - 2, s_qpre[(s + 1) & 1]);
+    }
     auto colsum = [&](int k) {   // as block_kernel: each reader sums its column
       double tq[kBlockMaxRowWaves];
 #pragma unroll
@@ -1757,8 +1765,9 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
       s_ring[slot * P + p] = gp;
       double q = 0.0;
       if (qpre) {
-        q = (!chivi && s > 0) ? __dadd_rn(__dadd_rn(s_qold[p], __dmul_rn(gprev, gprev)), __dmul_rn(gp, gp))
-                              : __dadd_rn(s_qold[p], __dmul_rn(gp, gp));
+        const double qo = s_qpre[s & 1][p];
+        q = (!chivi && s > 0) ? __dadd_rn(__dadd_rn(qo, __dmul_rn(gprev, gprev)), __dmul_rn(gp, gp))
+                              : __dadd_rn(qo, __dmul_rn(gp, gp));
         gprev = gp;
       } else {
         const int cnt = (s + 1 < W) ? s + 1 : W;
@@ -2212,77 +2221,117 @@ __global__ __launch_bounds__(256) void logw_sep_kernel(int D, long long m, const
   if (lane == 0) lw[r] = lp - lq;
 }
 
-// VB_LOGW_PAIR_LOOPS: the per-pair gamma loops of draw_pair instead (A/B build)
-__device__ __forceinline__ constexpr bool logw_gamma_row() {
-#ifdef VB_LOGW_PAIR_LOOPS
-  return false;
-#else
-  return true;
-#endif
+// Separable targets, t family, Philox: the polar t draws need the row's candidates
+// in stream order, so one thread walks a row (the wave-per-row logw_sep_kernel
+// splits a row's pairs over lanes); each accepted candidate is transformed, scaled
+// and evaluated (target and log q terms) as it is accepted.  lam rows stay in L2.
+template <class TGT>
+__global__ __launch_bounds__(256) void logw_sep_polar_kernel(int D, long long m, const double* lam,
+                                                             double df, double t_const, Rng rng,
+                                                             uint32_t step, uint32_t stride,
+                                                             double* lw, double* xs) {
+  __shared__ double2 s_sct[kSinCosN];
+  __shared__ double2 s_lt[kLogN + kLogU01N];
+  load_bm_tables(s_sct, s_lt);
+  __syncthreads();
+  const int q = blockIdx.y;
+  lam += (long long)q * 2 * D;
+  lw += (long long)q * m;
+  if (xs) xs += (long long)q * m * D;
+  rng.stream += (uint32_t)q * stride;
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= m) return;
+  const double c2 = -2.0 / df, hdf1 = 0.5 * (df + 1.0);
+  double lp = 0.0, lq = 0.0;
+  int cnt = 0;
+  const uint32_t kmax = (uint32_t)D + 64u;
+  auto take = [&](uint32_t a, uint32_t b) {
+    double l1;
+    const double T = polar_t(a, b, df, c2, s_lt, l1);
+    const double mu = lam[cnt], ls = lam[D + cnt];
+    const double x = T * exp(ls) + mu;
+    double g;
+    lp += TGT::lp1(x, g);
+    lq += t_const - l1 * hdf1 - ls;
+    if (xs) xs[r * D + cnt] = x;
+    ++cnt;
+  };
+  for (uint32_t k = 0; cnt < D && k < kmax; ++k) {
+    const u4 w = rng.draw(k, (uint32_t)r, step, kPolarPurpose);
+    if (polar_w(w.x, w.y) < 1.0) take(w.x, w.y);
+    if (cnt < D && polar_w(w.z, w.w) < 1.0) take(w.z, w.w);
+  }
+  // (never taken in practice) variates still missing are 0: x = mu
+  for (; cnt < D; ++cnt) {
+    const double mu = lam[cnt], ls = lam[D + cnt];
+    double g;
+    lp += TGT::lp1(mu, g);
+    lq += t_const - ls;
+    if (xs) xs[r * D + cnt] = mu;
+  }
+  lw[r] = lp - lq;
 }
 
-// The gamma variates of a row's t draws, every pair's Marsaglia-Tsang attempts in
-// ONE loop per thread (draw_pair runs one loop per pair; a wave repeats a pair's
-// loop while any lane still rejects, ~1.4 passes per pair at shape 20): the
-// thread walks its pairs in order, attempt k of pair j from Philox purpose 1 + k
-// as in gamma_pair, so the accepted values are bit for bit gamma_pair's.  The
-// loop ends when every lane has finished all its pairs.  g[2 j + c] -> sg (LDS,
-// [DMAX][256] per block).
-template <int DMAX>
-__device__ __forceinline__ void gamma_row(const Rng& rng, long long r, int npairs, uint32_t step,
-                                          double shape, double* sg, const double2* sct,
-                                          const double2* ltab) {
-  const double d = shape - 1.0 / 3.0;
-  const double c = 1.0 / sqrt(9.0 * d);
+// Polar t samples x [m][D] of rows of a mean-field t family and their log q (the
+// materialised log-weight path: host-callback or non-separable wide targets), one
+// thread per row as logw_sep_polar_kernel.
+__global__ __launch_bounds__(256) void sample_polar_kernel(int D, long long m, const double* lam,
+                                                           double df, double t_const, Rng rng,
+                                                           uint32_t step, double* x, double* lq_out) {
+  __shared__ double2 s_sct[kSinCosN];
+  __shared__ double2 s_lt[kLogN + kLogU01N];
+  load_bm_tables(s_sct, s_lt);
+  __syncthreads();
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= m) return;
+  const double c2 = -2.0 / df, hdf1 = 0.5 * (df + 1.0);
+  double lq = 0.0;
+  int cnt = 0;
+  const uint32_t kmax = (uint32_t)D + 64u;
+  auto take = [&](uint32_t a, uint32_t b) {
+    double l1;
+    const double T = polar_t(a, b, df, c2, s_lt, l1);
+    const double ls = lam[D + cnt];
+    x[r * D + cnt] = T * exp(ls) + lam[cnt];
+    lq += t_const - l1 * hdf1 - ls;
+    ++cnt;
+  };
+  for (uint32_t k = 0; cnt < D && k < kmax; ++k) {
+    const u4 w = rng.draw(k, (uint32_t)r, step, kPolarPurpose);
+    if (polar_w(w.x, w.y) < 1.0) take(w.x, w.y);
+    if (cnt < D && polar_w(w.z, w.w) < 1.0) take(w.z, w.w);
+  }
+  for (; cnt < D; ++cnt) {
+    x[r * D + cnt] = lam[cnt];
+    lq += t_const - lam[D + cnt];
+  }
+  lq_out[r] = lq;
+}
+
+// The polar t candidates of row r (see polar_t, vb_device.hpp): thread t walks the
+// row's attempt stream, storing each accepted candidate's raw words in its next slot
+// (LDS, slots[i * 256 + t], i < DMAX); the loop ends when every lane has D
+// variates (or D + 64 attempts).  Returns the number of variates stored.  The
+// transcendentals run afterwards, once per variate, outside the divergent loop.
+__device__ __forceinline__ int polar_row(const Rng& rng, long long r, int D, uint32_t step,
+                                         uint2* slots) {
   const int t = threadIdx.x;
-  int j = 0;
-  uint32_t k = 0;
-  bool da = false, db = false;
-  double ga = d, gb = d;
-  while (j < npairs) {
-    const u4 w = rng.draw((uint32_t)j, (uint32_t)r, step, 1u + k);
-    const double u1 = ((double)w.x + 0.5) * 0x1p-32;
-    const double u2 = (double)w.y * 0x1p-32;
-    double sn, cs;
-    const double rr = sqrt_pos(-2.0 * log_u01_tab(u1, ltab));
-    sincospi_tab(2.0 * u2, sn, cs, sct);
-    const double za = rr * cs, zb = rr * sn;
-    const double ua = ((double)w.z + 0.5) * 0x1p-32;
-    const double ub = ((double)w.w + 0.5) * 0x1p-32;
-    if (!da) {
-      double v = 1.0 + c * za;
-      if (v > 0.0) {
-        v = v * v * v;
-        const double lu = log_u01_tab(ua, ltab);
-        const double lv = (v >= 0x1p-1022 && v < 0x1p+1023) ? log_unit_tab(v, ltab) : log(v);
-        if (lu < 0.5 * za * za + d - d * v + d * lv) {
-          ga = d * v;
-          da = true;
-        }
-      }
+  int cnt = 0;
+  const uint32_t kmax = (uint32_t)D + 64u;
+  for (uint32_t k = 0; cnt < D && k < kmax; ++k) {
+    const u4 w = rng.draw(k, (uint32_t)r, step, kPolarPurpose);
+    const bool aa = polar_w(w.x, w.y) < 1.0;
+    const bool ab = polar_w(w.z, w.w) < 1.0;
+    if (aa) {
+      slots[cnt * 256 + t] = make_uint2(w.x, w.y);
+      ++cnt;
     }
-    if (!db) {
-      double v = 1.0 + c * zb;
-      if (v > 0.0) {
-        v = v * v * v;
-        const double lu = log_u01_tab(ub, ltab);
-        const double lv = (v >= 0x1p-1022 && v < 0x1p+1023) ? log_unit_tab(v, ltab) : log(v);
-        if (lu < 0.5 * zb * zb + d - d * v + d * lv) {
-          gb = d * v;
-          db = true;
-        }
-      }
-    }
-    ++k;
-    if ((da && db) || k >= 64u) {
-      sg[(2 * j) * 256 + t] = ga;
-      sg[(2 * j + 1) * 256 + t] = gb;
-      ++j;
-      k = 0;
-      da = db = false;
-      ga = gb = d;
+    if (ab && cnt < D) {
+      slots[cnt * 256 + t] = make_uint2(w.z, w.w);
+      ++cnt;
     }
   }
+  return cnt;
 }
 
 // any target with D <= DMAX: one thread per draw
@@ -2294,9 +2343,9 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
                                                        double* xs) {
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
-  __shared__ double s_mu[DMAX], s_ls[DMAX], s_sg[DMAX], s_isg[DMAX];
-  // t family, Philox: the row's gamma variates (gamma_row), [DMAX][256]
-  __shared__ double s_gam[(TFAM && !HOST) ? DMAX * 256 : 1];
+  __shared__ double s_mu[DMAX], s_ls[DMAX], s_sg[DMAX];
+  // t family, Philox: the row's accepted polar candidates (polar_row), [DMAX][256]
+  __shared__ uint2 s_pol[(TFAM && !HOST) ? DMAX * 256 : 1];
   // row q of a batched launch (vb_log_weights_rows): its own lambda, output
   // row, noise rows and Philox stream (stream + q * stride)
   const int q = blockIdx.y;
@@ -2312,7 +2361,6 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
     s_mu[threadIdx.x] = lam[threadIdx.x];
     s_ls[threadIdx.x] = ls;
     s_sg[threadIdx.x] = exp(ls);
-    s_isg[threadIdx.x] = exp(-ls);
   }
   if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
   __syncthreads();
@@ -2320,48 +2368,46 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
   if (r >= m) return;
   double x[DMAX], g[DMAX];
   double lq = 0.0;
-  const double inv_df = 1.0 / df;
   if constexpr (TFAM && !HOST) {
-    if (logw_gamma_row())
-      gamma_row<DMAX>(rng, r, (D + 1) / 2, step, shape, s_gam, s_sct, s_lt);
-  }
+    // polar t draws (the log-weight draws of the t family, vbrng.c family 2):
+    // log q = t_const - (df + 1)/2 log1p(T^2 / df) - log sigma at the draw itself
+    // (x = mu + sigma T rounded moves it by ~1e-16 relative)
+    const int cnt = polar_row(rng, r, D, step, s_pol);
+    const double c2 = -2.0 / df, hdf1 = 0.5 * (df + 1.0);
 #pragma unroll
-  for (int j = 0; j < (DMAX + 1) / 2; ++j) {
-    double e0 = 0.0, e1 = 0.0;
-    if (2 * j < D) {
-      if constexpr (TFAM && !HOST) {
-        if (logw_gamma_row()) {   // the numerators here, the gammas from gamma_row
-          normal_pair_tab(rng.draw((uint32_t)j, (uint32_t)r, step, 0u), e0, e1, s_sct, s_lt);
-          // t = sqrt(df / 2) z / sqrt(G) with a refined rsqrt (as the block kernel's
-          // draw items), not sqrt + divide
-          e0 = t_scale * e0 * rsqrt_pos(s_gam[(2 * j) * 256 + threadIdx.x]);
-          e1 = t_scale * e1 * rsqrt_pos(s_gam[(2 * j + 1) * 256 + threadIdx.x]);
-        } else {
-          draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e0, e1, s_sct, s_lt);
-        }
-      } else {
-        draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e0, e1, s_sct, s_lt);
-      }
-    }
-    const double e[2] = {e0, e1};
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int d = 2 * j + c;
-      if (d >= DMAX) continue;
+    for (int d = 0; d < DMAX; ++d) {
       x[d] = 0.0;
       g[d] = 0.0;
       if (d < D) {
-        const double mu = s_mu[d], sg = s_sg[d];
-        x[d] = e[c] * sg + mu;
-        if constexpr (TFAM && !HOST) {
-          // log q with 1 / sigma and 1 / df multiplications (the Philox t path, whose
-          // draws are already ~1 ulp from the C oracle's)
-          const double z = (x[d] - mu) * s_isg[d];
-          lq += t_const - log1p_pos_tab(z * z * inv_df, s_lt) * (0.5 * (df + 1.0)) - s_ls[d];
-        } else {
-          lq += logq1s<TFAM, HOST>(x[d], mu, s_ls[d], sg, df, t_const, s_lt);
-        }
+        const uint2 wd = s_pol[d * 256 + threadIdx.x];
+        double l1;
+        double T = polar_t(wd.x, wd.y, df, c2, s_lt, l1);
+        T = d < cnt ? T : 0.0;
+        l1 = d < cnt ? l1 : 0.0;
+        x[d] = T * s_sg[d] + s_mu[d];
+        lq += t_const - l1 * hdf1 - s_ls[d];
         if (xs) xs[r * D + d] = x[d];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < (DMAX + 1) / 2; ++j) {
+      double e0 = 0.0, e1 = 0.0;
+      if (2 * j < D)
+        draw_pair<TFAM, HOST>(rng, noise, D, r, j, step, t_scale, shape, e0, e1, s_sct, s_lt);
+      const double e[2] = {e0, e1};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int d = 2 * j + c;
+        if (d >= DMAX) continue;
+        x[d] = 0.0;
+        g[d] = 0.0;
+        if (d < D) {
+          const double mu = s_mu[d], sg = s_sg[d];
+          x[d] = e[c] * sg + mu;
+          lq += logq1s<TFAM, HOST>(x[d], mu, s_ls[d], sg, df, t_const, s_lt);
+          if (xs) xs[r * D + d] = x[d];
+        }
       }
     }
   }
@@ -2581,6 +2627,16 @@ hipError_t launch_sample(int fam, int D, long long n, const double* lam, double 
   else
     hipLaunchKernelGGL((sample_kernel<false, false>), grid, block, 0, s, D, n, lam, t_scale,
                        shape, noise, rng, step, x);
+  return hipGetLastError();
+}
+
+hipError_t launch_sample_polar(int D, long long m, const double* lam, double df, double t_const,
+                               uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* x,
+                               double* lq, hipStream_t s) {
+  if (m == 0) return hipSuccess;
+  const Rng rng{k0, k1, stream};
+  hipLaunchKernelGGL(sample_polar_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, D, m,
+                     lam, df, t_const, rng, step, x, lq);
   return hipGetLastError();
 }
 
@@ -2812,7 +2868,14 @@ template <class TGT, bool TFAM, bool HOST>
 static void logw_launch(int D, long long m, const double* lam, double t_scale, double shape,
                         double df, double t_const, const double* noise, Rng rng, uint32_t step,
                         int rows, uint32_t stride, double* lw, double* xs, hipStream_t s) {
-  if constexpr (TGT::kSeparable) {
+  if constexpr (TGT::kSeparable && TFAM && !HOST) {
+    if (D > kBlockDMax) {
+      hipLaunchKernelGGL((logw_sep_polar_kernel<TGT>),
+                         dim3((unsigned)((m + 255) / 256), (unsigned)rows), dim3(256), 0, s, D, m,
+                         lam, df, t_const, rng, step, stride, lw, xs);
+      return;
+    }
+  } else if constexpr (TGT::kSeparable) {
     if (D > kBlockDMax) {
       hipLaunchKernelGGL((logw_sep_kernel<TGT, TFAM, HOST>),
                          dim3((unsigned)((m + 3) / 4), (unsigned)rows), dim3(256), 0, s, D, m,

@@ -1023,7 +1023,7 @@ size_t psis_col_stride(long long tail_cap) {
 hipError_t psis_columns(const double* lw, double* out, long long n, int m, long long rs,
                         long long cs, long long Mt, void* scratch, double* k_dev,
                         long long* tail_idx_dev, long long tail_cap, long long* n_tail_dev,
-                        hipStream_t s, unsigned* flag_dev) {
+                        hipStream_t s, unsigned* flag_dev, unsigned* flag_host) {
   const long long cap = Mt < 1 ? 1 : Mt;   // the tail holds at most M_t draws
   const long long sb = (long long)psis_col_stride(cap);
   PsisScratch S = carve(scratch, cap);
@@ -1032,7 +1032,7 @@ hipError_t psis_columns(const double* lw, double* out, long long n, int m, long 
   // fast path (see the header): 1 + 2 in two histogram passes; the host reads the
   // per-column flags (one wait) and takes the radix path when any column's
   // candidates exceed one workgroup's sort
-  bool fast = flag_dev && psis_fast_select_enabled() && cap <= kTailMax && n < (1LL << 31);
+  bool fast = flag_dev && flag_host && psis_fast_select_enabled() && cap <= kTailMax && n < (1LL << 31);
   if (fast) {
     hipLaunchKernelGGL(sel_init_kernel, dim3(1, m), dim3(256), 0, s, S.ps, S.hist, n - Mt - 1, sb);
     hipLaunchKernelGGL(sel_hist1_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.part, S.hist,
@@ -1042,18 +1042,8 @@ hipError_t psis_columns(const double* lw, double* out, long long n, int m, long 
     hipLaunchKernelGGL(sel_hist2_kernel, dim3(g, m), dim3(256), 0, s, lw, n, rs, cs, S.ps, S.hist,
                        sb);
     hipLaunchKernelGGL(sel_pick_kernel, dim3(1, m), dim3(256), 0, s, S.hist, S.ps, 2, flag_dev, sb);
-    // the flags land in a pinned buffer of the calling thread (grown on demand,
-    // kept for the life of the thread: released by the driver at process exit)
-    static thread_local unsigned* fl = nullptr;
-    static thread_local int fl_cap = 0;
-    if (m > fl_cap) {
-      if (fl) (void)hipHostFree(fl);
-      fl = nullptr;
-      fl_cap = 0;
-      const hipError_t ea = hipHostMalloc(reinterpret_cast<void**>(&fl), sizeof(unsigned) * m);
-      if (ea != hipSuccess) return ea;
-      fl_cap = m;
-    }
+    // the flags land in the caller's pinned buffer (the context's, >= m entries)
+    unsigned* fl = flag_host;
     hipError_t e = hipMemcpyAsync(fl, flag_dev, sizeof(unsigned) * m, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;

@@ -9,44 +9,61 @@ using namespace vbd;
 
 namespace {
 
-// One thread per (job, parameter).  compute_R_hat on chains[:, s:s+len, :]:
-// the segment is split into halves (psi = 2 nc half-chains of h = len/2 draws),
-// two-pass means / variances as numpy does, then
-//   B = h sum_j (mean_j - mean)^2 / (2nc - 1),  W = mean_j s_j^2 + 1e-8,
-//   var_hat = (h - 1) / h + B / (h W),  R-hat = sqrt(var_hat).
-__global__ __launch_bounds__(256) void rhat_kernel(const double* chains, long long nc, long long n,
-                                                   long long P, const long long* start,
-                                                   const long long* len, double* var_out,
-                                                   double* rhat_out) {
+// compute_R_hat on chains[:, s:s+len, :] (functions.py:8-31) in two stages, so
+// that chains held by different ranks combine to the same bits as one process:
+//   rhat_stats_kernel    one thread per (job, half-chain j, parameter): the
+//                        half-chain mean m_j = (sum of its h = len/2 draws) / h and
+//                        the centred sum of squares ss_j = sum (x - m_j)^2 (numpy's
+//                        two-pass np.mean / squared deviations);
+//   rhat_combine_kernel  one thread per (job, parameter), half-chains in order:
+//                        grand = sum_j m_j / (2 nc), s_j^2 = ss_j / (h - 1),
+//                        B = h sum_j (m_j - grand)^2 / (2 nc - 1),
+//                        W = nanmean_j s_j^2 + 1e-8,
+//                        var_hat = (h - 1) / h + B / (h W), R-hat = sqrt(var_hat).
+// Half-chain j of chain c is j = 2c + h (np.reshape of [nc][2h][P] into
+// [2nc][h][P]); stats are [job][2 nc][P].
+__global__ __launch_bounds__(256) void rhat_stats_kernel(const double* chains, long long n,
+                                                         long long P, const long long* start,
+                                                         const long long* len, double* mean_out,
+                                                         double* ss_out) {
+  const long long job = blockIdx.y, j = blockIdx.z, nc2 = gridDim.z;
+  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const long long h = len[job] / 2;
+  const double* x = chains + ((j >> 1) * n + start[job] + (j & 1) * h) * P + p;
+  double m = 0.0;
+  for (long long t = 0; t < h; ++t) m += x[t * P];
+  m /= (double)h;
+  double ss = 0.0;
+  for (long long t = 0; t < h; ++t) {
+    const double d = x[t * P] - m;
+    ss += d * d;
+  }
+  const long long o = (job * nc2 + j) * P + p;
+  mean_out[o] = m;
+  ss_out[o] = ss;
+}
+
+__global__ __launch_bounds__(256) void rhat_combine_kernel(const double* mean, const double* ss,
+                                                           long long nc2, long long P,
+                                                           const long long* len, double* var_out,
+                                                           double* rhat_out) {
   const long long job = blockIdx.y;
   const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
   if (p >= P) return;
-  const long long s0 = start[job], h = len[job] / 2;
-  const long long nc2 = 2 * nc;
-  double sum_means = 0.0, sum_var = 0.0;
-  long long n_var = 0;
-  // pass 1: grand mean of the half-chain means
-  for (long long j = 0; j < nc2; ++j) {
-    const double* x = chains + ((j >> 1) * n + s0 + (j & 1) * h) * P + p;
-    double m = 0.0;
-    for (long long t = 0; t < h; ++t) m += x[t * P];
-    sum_means += m / (double)h;
-  }
+  const long long h = len[job] / 2;
+  const double* mj = mean + job * nc2 * P + p;
+  const double* sj = ss + job * nc2 * P + p;
+  double sum_means = 0.0;
+  for (long long j = 0; j < nc2; ++j) sum_means += mj[j * P];
   const double grand = sum_means / (double)nc2;
-  double B = 0.0;
+  double B = 0.0, sum_var = 0.0;
+  long long n_var = 0;
   for (long long j = 0; j < nc2; ++j) {
-    const double* x = chains + ((j >> 1) * n + s0 + (j & 1) * h) * P + p;
-    double m = 0.0;
-    for (long long t = 0; t < h; ++t) m += x[t * P];
-    m /= (double)h;
-    double ss = 0.0;
-    for (long long t = 0; t < h; ++t) {
-      const double d = x[t * P] - m;
-      ss += d * d;
-    }
-    const double sj = ss / (double)(h - 1);
-    if (!isnan(sj)) {  // np.nanmean over the half-chain variances
-      sum_var += sj;
+    const double m = mj[j * P];
+    const double v = sj[j * P] / (double)(h - 1);
+    if (!isnan(v)) {  // np.nanmean over the half-chain variances
+      sum_var += v;
       ++n_var;
     }
     B += (m - grand) * (m - grand);
@@ -73,12 +90,22 @@ __global__ __launch_bounds__(256) void iterate_average_kernel(const double* x, l
 
 }  // namespace
 
-hipError_t launch_rhat(const double* chains, long long nc, long long n, long long P,
-                       long long n_jobs, const long long* start, const long long* len,
-                       double* var_out, double* rhat_out, hipStream_t s) {
+hipError_t launch_rhat_stats(const double* chains, long long nc, long long n, long long P,
+                             long long n_jobs, const long long* start, const long long* len,
+                             double* mean_out, double* ss_out, hipStream_t s) {
+  if (n_jobs <= 0 || P <= 0 || nc <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rhat_stats_kernel,
+                     dim3((unsigned)((P + 255) / 256), (unsigned)n_jobs, (unsigned)(2 * nc)),
+                     dim3(256), 0, s, chains, n, P, start, len, mean_out, ss_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rhat_combine(const double* mean, const double* ss, long long nc2, long long P,
+                               long long n_jobs, const long long* len, double* var_out,
+                               double* rhat_out, hipStream_t s) {
   if (n_jobs <= 0 || P <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rhat_kernel, dim3((unsigned)((P + 255) / 256), (unsigned)n_jobs), dim3(256), 0,
-                     s, chains, nc, n, P, start, len, var_out, rhat_out);
+  hipLaunchKernelGGL(rhat_combine_kernel, dim3((unsigned)((P + 255) / 256), (unsigned)n_jobs),
+                     dim3(256), 0, s, mean, ss, nc2, P, len, var_out, rhat_out);
   return hipGetLastError();
 }
 

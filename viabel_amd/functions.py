@@ -19,6 +19,7 @@ import numpy as np
 from . import _native as nat
 
 __all__ = ['compute_R_hat', 'compute_R_hat_adaptive_numpy', 'compute_R_hat_halfway',
+           'adaptive_segments', 'halfway_segments', 'rhat_stats', 'rhat_combine',
            'stochastic_iterate_averaging', 'safe_root', 'flat_to_triang', 'triang_to_flat',
            'compute_posterior_moments']
 
@@ -64,30 +65,74 @@ def compute_R_hat(chains, warmup=500):
     return var[0], out[0]
 
 
+def adaptive_segments(n_chains, n_iters, K, window_size=100):
+    """(start, length) of every window of compute_R_hat_adaptive_numpy, with the
+    reference's reshape errors (functions.py:44-52)."""
+    n_windows = n_iters // window_size
+    if n_windows * window_size != n_iters:
+        raise ValueError('cannot reshape array of size %d into shape (%d,%d,%d,newaxis)'
+                         % (n_chains * n_iters * K, n_chains, n_windows, window_size))
+    if window_size % 2 == 1:
+        _segment(n_chains, window_size, K, 0)
+    return [(i * window_size, window_size) for i in range(n_windows)]
+
+
+def halfway_segments(n_chains, n_iters, K, interval=100, start=1000):
+    """(start, length) of every sub-chain of compute_R_hat_halfway
+    (functions.py:54-65)."""
+    segs = []
+    for i in range(n_iters // interval):
+        sub_n = min(start + (i + 1) * interval, n_iters)
+        segs.append(_segment(n_chains, sub_n, K, sub_n // 2))
+    return segs
+
+
 def compute_R_hat_adaptive_numpy(chains, window_size=100):
     """R-hat of consecutive windows of `window_size` iterations: (n_windows, K)."""
     c = _chains(chains)
     nc, n, K = c.shape
-    n_windows = n // window_size
-    if n_windows * window_size != n:
-        raise ValueError('cannot reshape array of size %d into shape (%d,%d,%d,newaxis)'
-                         % (c.size, nc, n_windows, window_size))
-    if window_size % 2 == 1:
-        _segment(nc, window_size, K, 0)
-    return _rhat_batch(c, [(i * window_size, window_size) for i in range(n_windows)])[1]
+    return _rhat_batch(c, adaptive_segments(nc, n, K, window_size))[1]
 
 
 def compute_R_hat_halfway(chains, interval=100, start=1000):
     """R-hat of chains[:, :start + (i+1) interval] after discarding its first half."""
     c = _chains(chains)
     nc, n, K = c.shape
-    segs = []
-    for i in range(n // interval):
-        sub_n = min(start + (i + 1) * interval, n)
-        segs.append(_segment(nc, sub_n, K, sub_n // 2))
+    segs = halfway_segments(nc, n, K, interval, start)
     if not segs:
         return np.zeros((0,))
     return _rhat_batch(c, segs)[1]
+
+
+def rhat_stats(chains, segs):
+    """First stage of R-hat for chains held by one rank: per segment, half-chain
+    (2 c + half) and parameter, the half-chain mean and centred sum of squares,
+    each [n_segs][2 n_chains][K] (vb_rhat_stats)."""
+    c = _chains(chains)
+    nc, n, K = c.shape
+    starts = np.array([s for s, _ in segs], dtype=np.int64)
+    lens = np.array([m for _, m in segs], dtype=np.int64)
+    mean = np.empty((len(segs), 2 * nc, K))
+    ss = np.empty((len(segs), 2 * nc, K))
+    nat.check(nat.lib().vb_rhat_stats(nat.context().handle, nat.dptr(c), nc, n, K, len(segs),
+                                      nat.i64ptr(starts), nat.i64ptr(lens), nat.dptr(mean),
+                                      nat.dptr(ss)))
+    return mean, ss
+
+
+def rhat_combine(mean, ss, lens, return_var=False):
+    """Second stage: R-hat [n_segs][K] of the half-chains of all ranks
+    (mean / ss [n_segs][n_halves][K] in chain order, vb_rhat_combine); the same
+    bits as compute_R_hat on the gathered chains."""
+    mean = nat.as_f64(mean)
+    ss = nat.as_f64(ss)
+    J, H, K = mean.shape
+    lens = np.ascontiguousarray(lens, dtype=np.int64)
+    out = np.empty((J, K))
+    var = np.empty((J, K)) if return_var else None
+    nat.check(nat.lib().vb_rhat_combine(nat.context().handle, nat.dptr(mean), nat.dptr(ss), H, K, J,
+                                        nat.i64ptr(lens), nat.dptr(var), nat.dptr(out)))
+    return (var, out) if return_var else out
 
 
 def stochastic_iterate_averaging(estimate, start):

@@ -248,3 +248,146 @@ def run_restarts(family_factory, target, n_restarts, n_iters, n_samples=100, n_b
     if not dist_on:
         return np.asarray(local)[np.argsort(np.asarray(local)[:, 0])]
     return gather_records(local, n_restarts, width, group)
+
+
+# ---------------------------------------------------------------------------
+# RMSProp-IA / Adam-IA chains with R-hat, sharded over ranks (vb.py:392-712)
+
+class DeviceIAOps:
+    """run_ia_chains' per-rank work on the device: the rank's chains in one
+    launch chain (one workgroup per chain, chain o on Philox stream
+    family.stream + o whatever the sharding), the first R-hat stage
+    (vb_rhat_stats), the combine (vb_rhat_combine) and the cumulative means
+    (vb_iterate_average).  Tests substitute other ops to run the sharding and
+    the collective without a GPU."""
+
+    @staticmethod
+    def chains(opt, obj, inits, ids, world, n_iters, window, learning_rate, epsilon,
+               learning_rate_end):
+        from . import vb
+        fam = obj.family
+        run = vb.DeviceRun(obj, n_iters, inits, window, learning_rate, epsilon,
+                           learning_rate_end, optimizer=opt)
+        run.advance_philox(n_iters, fam.seed, fam.stream + ids[0], fam.step, stream_stride=world)
+        lam, hist, vals, _ = run.result()
+        return lam, hist, vals
+
+    @staticmethod
+    def stats(hist, segs):
+        from . import functions
+        return functions.rhat_stats(hist, segs)
+
+    @staticmethod
+    def combine(mean, ss, lens):
+        from . import functions
+        return functions.rhat_combine(mean, ss, lens)
+
+    @staticmethod
+    def average(x, start):
+        from . import functions
+        return functions.stochastic_iterate_averaging(x, start)[0]
+
+
+def run_ia_chains(opt, n_iters, objective_and_grad, init_param, K, has_log_norm=False,
+                  window=500, learning_rate=.01, epsilon=1e-6, rhat_window=500, n_optimisers=1,
+                  r_mean_threshold=1.15, r_sigma_threshold=1.20, tail_avg_iters=2000,
+                  learning_rate_end=None, perturb_scale=0.5, avg_grad_norm=False, group=None,
+                  gather_histories=False, ops=None):
+    """rmsprop_IA_optimize_with_rhat / adam_IA_optimize_with_rhat (vb.py:392-712,
+    `opt` = OPT_RMSPROP_IA / OPT_ADAM_IA) with the n_optimisers chains of the
+    reference's loop (vb.py:417-421) dealt to the ranks of `group`: chain o on
+    rank o % world.  Each rank runs its chains, then reduces each to the
+    statistics split-chain R-hat needs (per window / halfway segment, half-chain
+    and parameter: the half-chain mean and centred sum of squares,
+    functions.rhat_stats).  ONE all_gather of fixed-size per-chain records
+    (chain id, final parameters, value history, those statistics) gives every
+    rank all chains' statistics; the R-hat combine (functions.py:8-31's B / W
+    algebra) then runs on them in chain order, so r_hat_mean / r_hat_sigma (and
+    the halfway ones) and the averaging starts equal the one-process run's bit
+    for bit.  Returns the one-process tuple (final parameters of the last chain,
+    history chains, averaged means, averaged sigmas, values of all chains, log
+    norms, log); history chains and averages are this rank's chains (ids in
+    log['chain_ids']) unless gather_histories=True, which all-gathers the
+    histories as well (a second collective of n_optimisers x history x P).
+
+    The objective must be a native Philox-noise objective: chain o's noise is
+    then its own stream.  (The numpy-stream path draws the chains one after
+    another from shared generators, vb.py:419 / the family stream, and a
+    caller's objective runs where the caller's code runs: neither shards.)"""
+    from . import vb, functions
+    if ops is None:
+        if not isinstance(objective_and_grad, vb.NativeObjective) or \
+                objective_and_grad.family.rng != 'philox':
+            raise ValueError("sharded IA chains need a native objective with rng='philox' "
+                             "(chain o draws from its own Philox stream)")
+        if has_log_norm:
+            raise ValueError('not enough values to unpack (expected 3, got 2)')
+        if avg_grad_norm:
+            raise ValueError('avg_grad_norm runs the host-side update path, which is not sharded')
+        ops = DeviceIAOps
+    if learning_rate <= 0:
+        raise ValueError('learning rate must be positive')
+    if learning_rate_end is not None and learning_rate <= learning_rate_end:
+        raise ValueError('initial learning rate must be greater than final learning rate')
+    try:
+        import torch.distributed as dist
+        dist_on = dist.is_available() and dist.is_initialized()
+    except ImportError:
+        dist_on = False
+    rank, world = (dist.get_rank(group), dist.get_world_size(group)) if dist_on else (0, 1)
+    n_iters = int(n_iters)
+    init_param = np.asarray(init_param, dtype=float)
+    P = init_param.size
+    inits = vb._ia_inits(init_param, n_optimisers, perturb_scale)
+    n_hist = min(n_iters, 100 * int(window))              # vb.py:465-466
+    segs_w = functions.adaptive_segments(n_optimisers, n_hist, P, rhat_window)
+    segs_h = functions.halfway_segments(n_optimisers, n_hist, P, 100, 200)
+    segs = segs_w + segs_h
+    J = len(segs)
+    if ops is DeviceIAOps and dist_on:
+        bind_local_device(rank)
+    ids = shard(n_optimisers, rank, world)
+    width = 1 + P + n_iters + 4 * J * P
+    local = np.zeros((len(ids), width))
+    hist = np.zeros((0, n_hist, P))
+    if ids:
+        lam, hist, vals = ops.chains(opt, objective_and_grad, np.stack([inits[o] for o in ids]),
+                                     ids, world, n_iters, int(window), learning_rate, epsilon,
+                                     learning_rate_end)
+        hist = np.asarray(hist)
+        mean, ss = ops.stats(hist, segs)                  # [J][2 n_local][P]
+        nl = len(ids)
+        per_chain = lambda a: np.asarray(a).reshape(J, nl, 2, P).transpose(1, 0, 2, 3).reshape(nl, -1)
+        local = np.concatenate([np.asarray(ids, dtype=float)[:, None], np.asarray(lam),
+                                np.asarray(vals), per_chain(mean), per_chain(ss)], axis=1)
+    if ops is DeviceIAOps:
+        objective_and_grad.family.step += n_iters        # as the one-process run leaves it
+    table = gather_records(local, n_optimisers, width, group) if dist_on else local
+    o1, o2 = 1 + P, 1 + P + n_iters
+    o3 = o2 + 2 * J * P
+    to_halves = lambda a: a.reshape(n_optimisers, J, 2, P).transpose(1, 0, 2, 3).reshape(
+        J, 2 * n_optimisers, P)
+    lens = np.array([m for _, m in segs], dtype=np.int64)
+    rhats = ops.combine(np.ascontiguousarray(to_halves(table[:, o2:o3])),
+                        np.ascontiguousarray(to_halves(table[:, o3:])), lens)
+    rw = rhats[:len(segs_w)]
+    rh = rhats[len(segs_w):] if segs_h else np.zeros((0,))
+    rm, rs = rw[:, :K], rw[:, K:]
+    start_m, start_s = vb._ia_avg_starts(rm, rs, n_iters, rhat_window, r_mean_threshold,
+                                         r_sigma_threshold, tail_avg_iters)
+    chain_ids = list(ids)
+    if gather_histories:
+        hrec = np.concatenate([np.asarray(ids, dtype=float)[:, None], hist.reshape(len(ids), -1)],
+                              axis=1) if ids else np.zeros((0, 1 + n_hist * P))
+        htab = gather_records(hrec, n_optimisers, 1 + n_hist * P, group) if dist_on else hrec
+        hist = htab[:, 1:].reshape(n_optimisers, n_hist, P)
+        chain_ids = list(range(n_optimisers))
+    means = [ops.average(np.ascontiguousarray(hist[j, :, :K]), start_m) for j in range(len(chain_ids))]
+    sigmas = [ops.average(np.ascontiguousarray(hist[j, :, K:]), start_s)
+              for j in range(len(chain_ids))]
+    values = table[:, o1:o2].reshape(-1)
+    log = {'start_avg_mean_iters': start_m, 'start_avg_sigma_iters': start_s,
+           'r_hat_mean': rm, 'r_hat_sigma': rs,
+           'r_hat_mean_halfway': rh[:, :K], 'r_hat_sigma_halfway': rh[:, K:],
+           'chain_ids': chain_ids}
+    return (table[-1, 1:1 + P].copy(), hist, means, sigmas, values, np.zeros(len(values)), log)

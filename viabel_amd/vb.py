@@ -729,14 +729,9 @@ def _ia_host_chains(opt, n_iters, objective_and_grad, init_param, has_log_norm, 
     return lams, hists, np.array(values), np.array(log_norms, dtype=float)
 
 
-def _ia_finish(lams, hists, values, log_norms, n_iters, K, rhat_window, r_mean_threshold,
-               r_sigma_threshold, tail_avg_iters, n_optimisers):
-    """R-hat windows and iterate averaging of the chains (vb.py:486-553)."""
-    from . import functions
-    chains = np.stack(hists, axis=0)
-    rhats = functions.compute_R_hat_adaptive_numpy(chains, window_size=rhat_window)
-    rhats_halfway = functions.compute_R_hat_halfway(chains, interval=100, start=200)
-    rm, rs = rhats[:, :K], rhats[:, K:]
+def _ia_avg_starts(rm, rs, n_iters, rhat_window, r_mean_threshold, r_sigma_threshold,
+                   tail_avg_iters):
+    """First window pair whose R-hats are all below the thresholds (vb.py:495-512)."""
     start_m = start_s = n_iters - tail_avg_iters
     for ee in range(rm.shape[0] - 1):
         if (rm[ee] < r_mean_threshold).all() and (rm[ee + 1] < r_mean_threshold).all():
@@ -746,6 +741,33 @@ def _ia_finish(lams, hists, values, log_norms, n_iters, K, rhat_window, r_mean_t
         if (rs[ee] < r_sigma_threshold).all() and (rs[ee + 1] < r_sigma_threshold).all():
             start_s = ee * rhat_window
             break
+    return start_m, start_s
+
+
+def _ia_inits(init_param, n_optimisers, perturb_scale):
+    """Chain o's start: init_param for o = 0, else init_param + randn * (o + 1) *
+    perturb_scale after np.random.seed(o) (vb.py:418-421 / 583-586); the global
+    RNG is left where the reference leaves it."""
+    inits = []
+    for o in range(n_optimisers):
+        np.random.seed(seed=o)
+        if o == 0:
+            inits.append(init_param.copy())
+        else:
+            inits.append(init_param + np.random.randn(len(init_param)) * (o + 1) * perturb_scale)
+    return inits
+
+
+def _ia_finish(lams, hists, values, log_norms, n_iters, K, rhat_window, r_mean_threshold,
+               r_sigma_threshold, tail_avg_iters, n_optimisers):
+    """R-hat windows and iterate averaging of the chains (vb.py:486-553)."""
+    from . import functions
+    chains = np.stack(hists, axis=0)
+    rhats = functions.compute_R_hat_adaptive_numpy(chains, window_size=rhat_window)
+    rhats_halfway = functions.compute_R_hat_halfway(chains, interval=100, start=200)
+    rm, rs = rhats[:, :K], rhats[:, K:]
+    start_m, start_s = _ia_avg_starts(rm, rs, n_iters, rhat_window, r_mean_threshold,
+                                      r_sigma_threshold, tail_avg_iters)
     means, sigmas = [], []
     for o in range(n_optimisers):
         means.append(functions.stochastic_iterate_averaging(chains[o, :, :K], start_m)[0])
@@ -761,14 +783,31 @@ def rmsprop_IA_optimize_with_rhat(n_iters, objective_and_grad, init_param, K,
                                   epsilon=.000001, rhat_window=500, averaging=True,
                                   n_optimisers=1, r_mean_threshold=1.15, r_sigma_threshold=1.20,
                                   tail_avg_iters=2000, avg_grad_norm=False,
-                                  learning_rate_end=None):
+                                  learning_rate_end=None, sharded=False, group=None,
+                                  gather_histories=False):
     """vb.py:392-553: RMSProp (decay .9) chains, windowed / halfway R-hat, and
     iterate averaging from the first pair of windows whose R-hat is below the
     thresholds.  Returns (final param of the last chain, history chains
     [n_optimisers, n_hist, P], averaged means per chain, averaged sigmas per
     chain, values, log norms, log dict).  The updates run on the device
     (vb_run, optimizer RMSPROP_IA); R-hat and averaging too (vb_rhat,
-    vb_iterate_average)."""
+    vb_iterate_average).
+
+    sharded=True (a Philox-noise native objective under torch.distributed): the
+    chains are dealt to the ranks of `group` (restarts.run_ia_chains: chain o on
+    rank o % world, one gather of per-chain R-hat statistics); the R-hat
+    diagnostics and averaging starts equal the one-process run's.  The returned
+    histories and averages are then this rank's chains unless gather_histories."""
+    if sharded:
+        from . import restarts
+        return restarts.run_ia_chains(
+            nat.OPT_RMSPROP_IA, n_iters, objective_and_grad, init_param, K,
+            has_log_norm=has_log_norm, window=window, learning_rate=learning_rate,
+            epsilon=epsilon, rhat_window=rhat_window, n_optimisers=n_optimisers,
+            r_mean_threshold=r_mean_threshold, r_sigma_threshold=r_sigma_threshold,
+            tail_avg_iters=tail_avg_iters, learning_rate_end=learning_rate_end,
+            perturb_scale=0.5, avg_grad_norm=avg_grad_norm, group=group,
+            gather_histories=gather_histories)
     return _ia_optimize(nat.OPT_RMSPROP_IA, n_iters, objective_and_grad, init_param, K,
                         has_log_norm, window, learning_rate, epsilon, rhat_window, n_optimisers,
                         r_mean_threshold, r_sigma_threshold, tail_avg_iters, learning_rate_end,
@@ -779,9 +818,21 @@ def adam_IA_optimize_with_rhat(n_iters, objective_and_grad, init_param, K,
                                has_log_norm=False, window=500, learning_rate=.01,
                                epsilon=.000001, rhat_window=500, averaging=True, n_optimisers=1,
                                r_mean_threshold=1.15, r_sigma_threshold=1.20,
-                               tail_avg_iters=2000, learning_rate_end=None):
+                               tail_avg_iters=2000, learning_rate_end=None, sharded=False,
+                               group=None, gather_histories=False):
     """vb.py:556-712: Adam (beta1 .9, beta2 .999, bias correction with i + 2)
-    chains; same diagnostics and return value as rmsprop_IA_optimize_with_rhat."""
+    chains; same diagnostics, return value and sharding as
+    rmsprop_IA_optimize_with_rhat."""
+    if sharded:
+        from . import restarts
+        return restarts.run_ia_chains(
+            nat.OPT_ADAM_IA, n_iters, objective_and_grad, init_param, K,
+            has_log_norm=has_log_norm, window=window, learning_rate=learning_rate,
+            epsilon=epsilon, rhat_window=rhat_window, n_optimisers=n_optimisers,
+            r_mean_threshold=r_mean_threshold, r_sigma_threshold=r_sigma_threshold,
+            tail_avg_iters=tail_avg_iters, learning_rate_end=learning_rate_end,
+            perturb_scale=0.2, avg_grad_norm=False, group=group,
+            gather_histories=gather_histories)
     return _ia_optimize(nat.OPT_ADAM_IA, n_iters, objective_and_grad, init_param, K,
                         has_log_norm, window, learning_rate, epsilon, rhat_window, n_optimisers,
                         r_mean_threshold, r_sigma_threshold, tail_avg_iters, learning_rate_end,
