@@ -310,6 +310,11 @@ int vb_iterate_average(vb_ctx* ctx, const double* x, int64_t n, int64_t ld, int6
                        int64_t start, double* out);
 
 /* ---- log weights for bounds / PSIS (experiments.py:60-63) ------------ */
+/* Philox noise: the mean-field t family's draws here are Bailey's trigonometric
+ * t variates (one Philox block per column pair, no rejection; oracle/vbrng.c
+ * family 2), not the estimators' normal / gamma construction -- the same t(df)
+ * distribution (the Philox mode is a statistical contract).
+ * Host noise (the reference's numpy streams) is used as given. */
 int vb_log_weights(vb_ctx* ctx, const vb_family* fam, const vb_target* tgt,
                    const double* lam, int64_t m, const vb_noise* noise,
                    double* lw_out, double* samples_out /* nullable, [m, D] */);

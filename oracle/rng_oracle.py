@@ -41,11 +41,11 @@ def philox(ctr, key):
 
 def noise(seed, stream, step, n, dim, family='gauss', df=0.0):
     """Standardized draws eps[n, dim] of one step: N(0,1) ('gauss'), t(df) as
-    N / sqrt(Gamma) ('t', the estimators' draws) or by Bailey's polar method
-    ('t_polar', the log-weight draws of the t family)."""
+    N / sqrt(Gamma) ('t', the estimators' draws) or by Bailey's trigonometric
+    method ('t_bailey', the log-weight draws of the t family)."""
     out = np.empty((n, dim))
     _lib().vbo_fill(seed, stream & 0xFFFFFF, step & 0xFFFFFFFF, n, dim,
-                    {'gauss': 0, 't': 1, 't_polar': 2}[family], float(df),
+                    {'gauss': 0, 't': 1, 't_bailey': 2}[family], float(df),
                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
     return out
 

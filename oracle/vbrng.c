@@ -15,16 +15,13 @@
  *  - t draw: sqrt(df/2) * gauss / sqrt(gamma(df/2)), the structure of numpy's
  *    legacy standard_t; gamma by Marsaglia & Tsang (2000), proposals from
  *    purposes 1..64 with 32-bit uniforms.
- *  - polar t draw (family 2; the log-weight draws of the t family): Bailey,
+ *  - Bailey t draw (family 2; the log-weight draws of the t family): Bailey,
  *    "Polar generation of random variates with the t-distribution", Math. Comp.
- *    62 (1994) 779-781.  Row n's candidates come from ONE stream of blocks,
- *    attempt k = 0, 1, ... at counter (k, n, step, stream | 65 << 24), two
- *    candidates per block, (x, y) words then (z, w) words: u, v = ((int32) word
- *    + 1/2) 2^-31 in (-1, 1), W = fma(u, u, v v); W < 1 is accepted and becomes
- *    the row's next variate T = u sqrt(df (W^(-2/df) - 1) / W), computed as
- *    u sqrt(df expm1(-(2/df) log W) / W).  At most D + 64 attempts; a variate
- *    still missing then is 0 (never observed: 2D + 128 candidates at acceptance
- *    pi/4 leave fewer than D accepted with probability < 1e-30).
+ *    62 (1994) 779-781: T = cos(2 pi U2) sqrt(df (U1^(-2/df) - 1)) for U1, U2 iid
+ *    U(0, 1).  Column pair j of row n from the block at counter (j, n, step,
+ *    stream | 65 << 24): variate 2j from words (x, z), 2j + 1 from (y, w); of each
+ *    (lo, hi), U1 = (a + 1/2) 2^-40 with a = lo | (hi & 0xff) << 32 and
+ *    U2 = (hi >> 8) 2^-24; T = cos(2 pi U2) sqrt(df expm1(-(2/df) log U1)).
  */
 #include <math.h>
 #include <stdint.h>
@@ -103,34 +100,35 @@ static void gamma2(uint64_t seed, uint32_t stream, uint32_t pair, uint32_t n, ui
   }
 }
 
-#define VBO_POLAR_PURPOSE 65u
+#define VBO_BAILEY_PURPOSE 65u
 
-static double polar_uniform(uint32_t w) { return ((double)(int32_t)w + 0.5) * 0x1p-31; }
-
-/* row n of polar t draws (see the header) into out[0..D) */
-static void polar_t_row(uint64_t seed, uint32_t stream, uint32_t n, uint32_t step, int64_t D,
-                        double df, double* out) {
-  int64_t cnt = 0;
-  for (int64_t i = 0; i < D; ++i) out[i] = 0.0;
-  for (uint32_t k = 0; cnt < D && (int64_t)k < D + 64; ++k) {
-    blk w = draw(seed, stream, k, n, step, VBO_POLAR_PURPOSE);
-    for (int c = 0; c < 2 && cnt < D; ++c) {
-      double u = polar_uniform(w.v[2 * c]), v = polar_uniform(w.v[2 * c + 1]);
-      double W = fma(u, u, v * v);
-      if (!(W < 1.0)) continue;
-      double e = expm1((-2.0 / df) * log(W));
-      out[cnt++] = u * sqrt(df * e / W);
-    }
+/* Bailey t variates of column pair j of row n (see the header) */
+static void bailey_pair(uint64_t seed, uint32_t stream, uint32_t j, uint32_t n, uint32_t step,
+                        double df, double* t0, double* t1) {
+  blk w = draw(seed, stream, j, n, step, VBO_BAILEY_PURPOSE);
+  double* out[2] = {t0, t1};
+  for (int c = 0; c < 2; ++c) {
+    uint32_t lo = w.v[c], hi = w.v[2 + c];
+    double a = (double)((((uint64_t)(hi & 0xffu)) << 32) | lo);
+    double u1 = (a + 0.5) * 0x1p-40;
+    double u2 = (double)(hi >> 8) * 0x1p-24;
+    *out[c] = cos(2.0 * M_PI * u2) * sqrt(df * expm1((-2.0 / df) * log(u1)));
   }
 }
 
 /* standardized draws eps[n][D] for one step: family 0 = N(0,1), 1 = t(df),
- * 2 = polar t(df) (the log-weight draws) */
+ * 2 = Bailey t(df) (the log-weight draws) */
 void vbo_fill(uint64_t seed, uint32_t stream, uint32_t step, int64_t nrows, int64_t D, int family,
               double df, double* eps) {
   int64_t npairs = (D + 1) / 2;
   if (family == 2) {
-    for (int64_t r = 0; r < nrows; ++r) polar_t_row(seed, stream, (uint32_t)r, step, D, df, eps + r * D);
+    for (int64_t r = 0; r < nrows; ++r)
+      for (int64_t j = 0; j < npairs; ++j) {
+        double t0, t1;
+        bailey_pair(seed, stream, (uint32_t)j, (uint32_t)r, step, df, &t0, &t1);
+        eps[r * D + 2 * j] = t0;
+        if (2 * j + 1 < D) eps[r * D + 2 * j + 1] = t1;
+      }
     return;
   }
   for (int64_t r = 0; r < nrows; ++r) {

@@ -222,7 +222,7 @@ def _cfg5_oracle_record(r, init, n_iters, N, M):
         return vb_oracle.klvi_value_grad(fam, 'eight_schools_ncp', lam, N, eps=eps)
     opt, _, vals, _ = vb_oracle.adagrad_optimize(n_iters, f, init, learning_rate=.01,
                                                  learning_rate_end=.001)
-    eps = rng_oracle.noise(0, (1 << 20) + r, 0, M, D, 't_polar', 40.0)
+    eps = rng_oracle.noise(0, (1 << 20) + r, 0, M, D, 't_bailey', 40.0)
     _, lw = vb_oracle.log_weights(fam, 'eight_schools_ncp', opt, M, eps=eps)
     with warnings.catch_warnings():
         warnings.simplefilter('ignore')

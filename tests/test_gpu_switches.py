@@ -14,6 +14,8 @@ each side runs in a child process; the child writes its run's result
   of the largest entry over a short trajectory.
 * VIABEL_AMD_HOST_TRACE=1 (host timestamps of the column-pair launch path on
   stderr): the same bits, and the trace lines are there.
+* VIABEL_AMD_DIV_TWO_PASS=0 (divergence statistics in numpy's three passes at every
+  size): equal to the two-pass Welford / Chan form to rounding.
 (VIABEL_AMD_PREDRAW, _BLOCK_SPLIT, _PREDRAW_OVERLAP, _GEMM_EPI_EXACT,
 _PSIS_FAST_SELECT and _FR_NS_START have their own tests in test_gpu_vb.py,
 test_gpu_configs.py, test_gpu_fullrank.py and test_gpu_bounds_psis.py.)
@@ -116,3 +118,40 @@ def test_host_trace_is_bitwise_default_and_prints(tmp_path):
     for k in ('lam', 'hist', 'vals'):
         np.testing.assert_array_equal(out[k], ref[k])
     assert 'sep advance' in err, err[-2000:]
+
+
+_DIV_CHILD = '''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from viabel_amd import bounds
+rs = np.random.RandomState(17)
+lw = np.stack([rs.standard_t(5.0, 300_000) * 0.7 - 3.0, rs.randn(300_000) * 2.0 + 1.0])
+np.save(sys.argv[2], bounds.divergence_rows(lw))
+'''
+
+
+def test_div_two_pass_switch(tmp_path):
+    """VIABEL_AMD_DIV_TWO_PASS=0 (the three-pass divergence statistics at every
+    size) against the default two-pass Welford / Chan form at n = 3e5: equal to
+    rounding (1e-12 relative), and both equal to the oracle's divergence_bound
+    statistics (bounds.py:142-192, numpy's definitions) to 1e-12."""
+    from oracle import bounds_oracle
+    out = {}
+    for tag, env in (('two', {}), ('three', {'VIABEL_AMD_DIV_TWO_PASS': '0'})):
+        path = str(tmp_path / ('%s.npy' % tag))
+        subprocess.check_call([sys.executable, '-c', _DIV_CHILD, ROOT, path],
+                              env=dict(os.environ, **env), timeout=300)
+        out[tag] = np.load(path)
+    np.testing.assert_allclose(out['two'], out['three'], rtol=1e-12, atol=1e-14)
+    rs = np.random.RandomState(17)
+    lw = np.stack([rs.standard_t(5.0, 300_000) * 0.7 - 3.0, rs.randn(300_000) * 2.0 + 1.0])
+    import warnings
+    for j in range(2):
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            d, lnb = bounds_oracle.divergence_bound(lw[j], return_log_norm_bound=True)
+        np.testing.assert_allclose(out['two'][j, :2], [d, lnb], rtol=1e-12)
+        r = np.exp(2 * (lw[j] - lw[j].max()))
+        np.testing.assert_allclose(out['two'][j, 2:7],
+                                   [r.mean(), r.std() / np.sqrt(r.size), lw[j].mean(),
+                                    lw[j].std() / np.sqrt(lw[j].size), lw[j].max()], rtol=1e-12)

@@ -35,18 +35,18 @@ def test_t_draws_match_student_t():
 
 
 @pytest.mark.parametrize('df', [3.0, 8.0, 40.0])
-def test_polar_t_draws_match_student_t(df):
-    """Bailey's polar t (the log-weight draws of the t family, vbrng.c family 2):
-    KS against scipy's t, the variance, and no correlation between a row's
-    consecutive variates (different accepted points are independent)."""
-    z = rng_oracle.noise(seed=5, stream=1, step=2, n=40000, dim=6, family='t_polar', df=df)
+def test_bailey_t_draws_match_student_t(df):
+    """Bailey's trigonometric t (the log-weight draws of the t family, vbrng.c
+    family 2): KS against scipy's t, the variance, and no correlation between a
+    row's consecutive variates (a pair's two variates use disjoint words)."""
+    z = rng_oracle.noise(seed=5, stream=1, step=2, n=40000, dim=6, family='t_bailey', df=df)
     assert stats.kstest(z.ravel(), 't', args=(df,)).pvalue > 1e-3
     if df > 4:
         assert abs(z.var() / (df / (df - 2)) - 1) < 0.03
     r = np.corrcoef(z[:, :-1].ravel(), z[:, 1:].ravel())[0, 1]
     assert abs(r) < 0.01
-    # the row stream does not depend on D: a row's first variates are the same
-    z3 = rng_oracle.noise(seed=5, stream=1, step=2, n=50, dim=3, family='t_polar', df=df)
+    # counter addressing by column pair: a row's first variates do not depend on D
+    z3 = rng_oracle.noise(seed=5, stream=1, step=2, n=50, dim=3, family='t_bailey', df=df)
     np.testing.assert_array_equal(z3, z[:50, :3])
 
 

@@ -27,7 +27,7 @@ def oracle_compute(ids, inits):
             return vb_oracle.klvi_value_grad(fam, 'eight_schools_ncp', lam, N_SAMPLES, eps=eps)
         opt, hist, vals, _ = vb_oracle.adagrad_optimize(N_ITERS, f, init, learning_rate=.01,
                                                         learning_rate_end=.001)
-        eps = rng_oracle.noise(0, (1 << 20) + r, 0, 2000, D, 't_polar', 40.0)
+        eps = rng_oracle.noise(0, (1 << 20) + r, 0, 2000, D, 't_bailey', 40.0)
         _, lw = vb_oracle.log_weights(fam, 'eight_schools_ncp', opt, 2000, eps=eps)
         with warnings.catch_warnings():
             warnings.simplefilter('ignore')

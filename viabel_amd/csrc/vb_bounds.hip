@@ -9,6 +9,9 @@
 // block combines them in block order), so results are bitwise reproducible
 // run to run.  Passes follow numpy's two-pass definitions (np.std centres on
 // the mean first) rather than one-pass power sums, which cancel badly.
+#include <algorithm>
+#include <cstdlib>
+
 #include "vb_device.hpp"
 #include "vb_internal.hpp"
 
@@ -19,8 +22,9 @@ namespace vbk {
 namespace {
 
 constexpr int kRedBlocks = 1024;
-// divergence scratch per log-weight row: partials [2 kRedBlocks], sc [4], m2 [2] (+ pad)
-constexpr long long kDivStride = 2 * kRedBlocks + 8;
+// divergence scratch per log-weight row: partials [4 kRedBlocks] (two-pass form;
+// the three-pass form uses 2 per block), sc [4], m2 [2] (+ pad)
+constexpr long long kDivStride = 4 * kRedBlocks + 8;
 
 __device__ __forceinline__ double block_sum1(double v, double* red) {
   v = wave_sum(v);
@@ -41,6 +45,18 @@ __device__ __forceinline__ double block_max1(double v, double* red) {
 }
 
 __global__ void set_scalar_kernel(double* p, double v) { *p = v; }
+
+// VIABEL_AMD_DIV_TWO_PASS=0: the three-pass divergence statistics (numpy's two-pass
+// definitions) at every size instead of the two-pass Welford / Chan form from
+// kDivTwoPassMinN log weights on (A/B and parity switch; the two agree to rounding)
+constexpr long long kDivTwoPassMinN = 1LL << 16;
+bool div_two_pass_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("VIABEL_AMD_DIV_TWO_PASS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 int red_grid(long long n) {
   long long g = (n + 2047) / 2048;
@@ -171,6 +187,182 @@ __global__ __launch_bounds__(256) void lw_rdev_kernel(const double* lw, long lon
   if (threadIdx.x == 0) {
     part[2 * blockIdx.x] = q;
     part[2 * blockIdx.x + 1] = 0.0;
+  }
+}
+
+// ---- two passes over the log weights (bounds_divergence_rows, n >= 2^16) -------
+// Every statistic divergence_bound needs (bounds.py:142-192) from TWO reads of lw
+// instead of three: pass A the max M and Welford (count, mean, M2) of lw; pass B
+// Welford of r = exp(alpha (lw - M)).  Thread states merge with Chan et al.'s
+// pairwise formula (Am. Stat. 37 (1983) 242-247) in a fixed order (a shuffle-down
+// tree in each wave, waves in order, blocks in order), so the results are bitwise
+// reproducible; against numpy's two-pass np.mean / np.std they differ by rounding
+// (as any reduction order at these sizes does).  Each thread streams kDivPer log
+// weights (four loads in flight), so the merges are a small part of the pass.
+struct Welf {
+  double n, mean, m2;
+};
+
+__device__ __forceinline__ void welf_add(Welf& a, double v) {
+  a.n += 1.0;
+  double inv = __builtin_amdgcn_rcp(a.n);          // 1 / count, refined (~1 ulp)
+  inv = fma(inv, fma(-a.n, inv, 1.0), inv);
+  inv = fma(inv, fma(-a.n, inv, 1.0), inv);
+  const double d = v - a.mean;
+  a.mean = fma(d, inv, a.mean);
+  a.m2 = fma(d, v - a.mean, a.m2);
+}
+
+__device__ __forceinline__ Welf welf_merge(const Welf& a, const Welf& b) {
+  if (b.n == 0.0) return a;
+  if (a.n == 0.0) return b;
+  Welf o;
+  o.n = a.n + b.n;
+  const double wb = b.n / o.n;
+  const double d = b.mean - a.mean;
+  o.mean = fma(d, wb, a.mean);
+  o.m2 = fma(d * d, a.n * wb, a.m2 + b.m2);
+  return o;
+}
+
+__device__ __forceinline__ Welf welf_shfl_down(const Welf& a, int off) {
+  return Welf{__shfl_down(a.n, off, 64), __shfl_down(a.mean, off, 64), __shfl_down(a.m2, off, 64)};
+}
+
+constexpr int kDivPer = 32;   // log weights per thread per pass
+int div2_grid(long long n) {
+  long long g = (n + 256LL * kDivPer - 1) / (256LL * kDivPer);
+  return (int)std::max(1LL, std::min<long long>(g, kRedBlocks));
+}
+
+// the block's Welford state (+ max) in a fixed order; lane 0 of wave 0 returns it
+template <bool MAX>
+__device__ __forceinline__ Welf welf_block(Welf a, double& m, Welf* red, double* redm) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    a = welf_merge(a, welf_shfl_down(a, off));
+    if (MAX) m = fmax(m, __shfl_down(m, off, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = a;
+    if (MAX) redm[threadIdx.x >> 6] = m;
+  }
+  __syncthreads();
+  if (MAX) m = fmax(fmax(redm[0], redm[1]), fmax(redm[2], redm[3]));
+  return welf_merge(welf_merge(red[0], red[1]), welf_merge(red[2], red[3]));
+}
+
+// grid-stride loads of this thread's log weights, four in flight
+template <class F>
+__device__ __forceinline__ void div_stream(const double* lw, long long n, F&& f) {
+  const long long st = (long long)gridDim.x * 256;
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * st < n; i += 4 * st) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = lw[i + u * st];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) f(v[u]);
+  }
+  for (; i < n; i += st) f(lw[i]);
+}
+
+// pass A: partials [4 b .. 4 b + 3] = (max, n, mean, M2) of lw
+__global__ __launch_bounds__(256) void lw_div_a_kernel(const double* lw, long long n, double* part,
+                                                       long long ld) {
+  __shared__ Welf red[4];
+  __shared__ double redm[4];
+  lw += (long long)blockIdx.y * ld;
+  part += (long long)blockIdx.y * kDivStride;
+  Welf a{0.0, 0.0, 0.0};
+  double m = -INFINITY;
+  div_stream(lw, n, [&](double v) {
+    m = fmax(m, v);
+    welf_add(a, v);
+  });
+  const Welf b = welf_block<true>(a, m, red, redm);
+  if (threadIdx.x == 0) {
+    double* o = part + 4 * blockIdx.x;
+    o[0] = m;
+    o[1] = b.n;
+    o[2] = b.mean;
+    o[3] = b.m2;
+  }
+}
+
+// merge pass A's block states in block order: sc[0] = max, sc[1] = mean, sc[2] = M2
+__global__ __launch_bounds__(64) void div_a_final(const double* part, int nb, double* sc) {
+  part += (long long)blockIdx.y * kDivStride;
+  sc += (long long)blockIdx.y * kDivStride;
+  Welf a{0.0, 0.0, 0.0};
+  double m = -INFINITY;
+  for (int b = threadIdx.x; b < nb; b += 64) {
+    const double* q = part + 4 * b;
+    m = fmax(m, q[0]);
+    a = welf_merge(a, Welf{q[1], q[2], q[3]});
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    a = welf_merge(a, welf_shfl_down(a, off));
+    m = fmax(m, __shfl_down(m, off, 64));
+  }
+  if (threadIdx.x == 0) {
+    sc[0] = m;
+    sc[1] = a.mean;
+    sc[2] = a.m2;
+  }
+}
+
+// pass B: partials [3 b ..] = Welford (n, mean, M2) of r = exp(alpha (lw - max))
+__global__ __launch_bounds__(256) void lw_div_b_kernel(const double* lw, long long n, double alpha,
+                                                       const double* sc, double* part,
+                                                       long long ld) {
+  __shared__ Welf red[4];
+  lw += (long long)blockIdx.y * ld;
+  sc += (long long)blockIdx.y * kDivStride;
+  part += (long long)blockIdx.y * kDivStride;
+  const double mx = sc[0];
+  Welf a{0.0, 0.0, 0.0};
+  div_stream(lw, n, [&](double v) { welf_add(a, exp_fast(alpha * (v - mx))); });
+  double unused = 0.0;
+  const Welf b = welf_block<false>(a, unused, red, nullptr);
+  if (threadIdx.x == 0) {
+    double* o = part + 3 * blockIdx.x;
+    o[0] = b.n;
+    o[1] = b.mean;
+    o[2] = b.m2;
+  }
+}
+
+// merge pass B's block states; out7 as divergence_final
+__global__ __launch_bounds__(64) void div_b_final(const double* part, int nb, long long n,
+                                                  double alpha, int has_elbo, double elbo,
+                                                  const double* sc, double* out7) {
+  part += (long long)blockIdx.y * kDivStride;
+  sc += (long long)blockIdx.y * kDivStride;
+  out7 += (long long)blockIdx.y * 7;
+  Welf a{0.0, 0.0, 0.0};
+  for (int b = threadIdx.x; b < nb; b += 64) {
+    const double* q = part + 3 * b;
+    a = welf_merge(a, Welf{q[0], q[1], q[2]});
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) a = welf_merge(a, welf_shfl_down(a, off));
+  if (threadIdx.x == 0) {
+    const double sq = sqrt((double)n);
+    const double mean_r = a.mean;
+    const double se_r = sqrt(a.m2 / (double)n) / sq;
+    const double cubo = log(mean_r) / alpha + sc[0];
+    const double mean_lw = sc[1];
+    const double se_lw = has_elbo ? NAN : sqrt(sc[2] / (double)n) / sq;
+    const double lnb = has_elbo ? elbo : mean_lw;
+    out7[0] = alpha / (alpha - 1.0) * (cubo - lnb);
+    out7[1] = lnb;
+    out7[2] = mean_r;
+    out7[3] = se_r;
+    out7[4] = mean_lw;
+    out7[5] = se_lw;
+    out7[6] = sc[0];
   }
 }
 
@@ -371,8 +563,21 @@ hipError_t bounds_divergence_rows(const double* lw, long long rows, long long n,
   const int g = red_grid(n);
   const unsigned R = (unsigned)rows;
   double* part = scratch;
-  double* sc = scratch + 2 * kRedBlocks;
+  double* sc = scratch + 4 * kRedBlocks;   // after the largest (two-pass) partials
   double* m2 = sc + 4;
+  // below 2^16 log weights the exact three-pass form (numpy's definitions, whose
+  // bits it reproduces on small inputs -- the Monte Carlo warning texts print them);
+  // above, no reduction order reproduces numpy's pairwise sums bit for bit anyway,
+  // and the two-pass Welford form reads the 8 B per log weight twice, not three times
+  if (div_two_pass_enabled() && n >= kDivTwoPassMinN) {
+    const int g2 = div2_grid(n);
+    hipLaunchKernelGGL(lw_div_a_kernel, dim3(g2, R), dim3(256), 0, s, lw, n, part, ld);
+    hipLaunchKernelGGL(div_a_final, dim3(1, R), dim3(64), 0, s, part, g2, sc);
+    hipLaunchKernelGGL(lw_div_b_kernel, dim3(g2, R), dim3(256), 0, s, lw, n, alpha, sc, part, ld);
+    hipLaunchKernelGGL(div_b_final, dim3(1, R), dim3(64), 0, s, part, g2, n, alpha, has_elbo, elbo,
+                       sc, out7);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(lw_max_sum_kernel, dim3(g, R), dim3(256), 0, s, lw, n, part, ld);
   hipLaunchKernelGGL(lw_max_sum_final, dim3(1, R), dim3(256), 0, s, part, g, n, sc);
   hipLaunchKernelGGL(lw_rescaled_kernel, dim3(g, R), dim3(256), 0, s, lw, n, alpha, sc, part, ld);

@@ -133,12 +133,13 @@ __device__ __forceinline__ double exp_fast(double x) {
   return x != x ? x : res;
 }
 
-// expm1(x) for finite x >= 0, ~1 ulp: exp_fast's reduction x = k ln2 + r and its
+// expm1(x) for 0 <= x <= 700, ~1 ulp: exp_fast's reduction x = k ln2 + r and its
 // polynomial, expm1(r) = r + r^2 q(r) (no cancellation near 0), then
-// 2^k (1 + expm1(r)) - 1 = 2^k expm1(r) + (2^k - 1) in one fma (2^k - 1 exact
-// for the k the callers reach, x <= 709)
+// 2^k (1 + expm1(r)) - 1 = 2^k expm1(r) + (2^k - 1) in one fma (2^k - 1 exact for
+// k <= 53; larger k round it as 2^k, well within an ulp of the result).  The
+// Bailey draws pass -(2/df) log U1 <= 57 / df.
 __device__ __forceinline__ double expm1_pos(double x) {
-  const double xc = fmin(x, 709.0);
+  const double xc = x;
   const double k = rint(xc * 1.4426950408889634);
   double r = fma(-k, 6.93147180369123816490e-01, xc);
   r = fma(-k, 1.90821492927058770002e-10, r);
@@ -224,7 +225,7 @@ __device__ __forceinline__ double log_unit_tab(double u, const double2* ltab) {
   e = lo ? e - 1 : e;
   // exact: m in [0.5, 2); the clamp only matters for 0 / inf / NaN arguments,
   // which callers route to the general log (memory safety)
-  const int i = min(max((int)rint(fma(m, 64.0, -64.0)), kLogLo), kLogLo + kLogN - 1);
+  const int i = min(max((int)rint(hfma(m, 64.0, -64.0)), kLogLo), kLogLo + kLogN - 1);
   const double2 t = ltab[i - kLogLo];
   const double r = fma(m, t.x, -1.0);
   double p = 0.1111111111111111;                 // 1/9
@@ -291,6 +292,26 @@ __device__ __forceinline__ void sincospi_tab(double x, double& sn, double& cs,
   const double ct = fma(t2, pc, 1.0);               // cos(theta)
   sn = fma(t.x, ct, t.y * st);
   cs = fma(t.y, ct, -(t.x * st));
+}
+
+// cos(pi x) for x = b 2^-23 (b < 2^24, so x in [0, 2)), from the integer b: table
+// point q = round(b / 2^16) (= rint(128 x) up to the tie direction; either point
+// keeps |r| <= 1/256) and the exact residual r = (b - q 2^16) 2^-23, as
+// sincospi_tab otherwise
+__device__ __forceinline__ double cospi_tab_u24(uint32_t b, const double2* sct) {
+  const uint32_t q = (b + 0x8000u) >> 16;
+  const double r = (double)(int)(b - (q << 16)) * 0x1p-23;
+  const double2 t = sct[q];
+  const double th = fma(r, 3.141592653589793, r * 1.2246467991473532e-16);
+  const double t2 = th * th;
+  double ps = hfma(t2, -0.0001984126984126984, 0.008333333333333333);
+  ps = hfma(ps, t2, -0.16666666666666666);
+  const double st = fma(th * t2, ps, th);
+  double pc = hfma(t2, 2.48015873015873e-05, -0.001388888888888889);
+  pc = hfma(pc, t2, 0.041666666666666664);
+  pc = hfma(pc, t2, -0.5);
+  const double ct = fma(t2, pc, 1.0);
+  return fma(t.y, ct, -(t.x * st));
 }
 
 // Two standard normals (Box-Muller) with the table transcendentals.
@@ -404,40 +425,31 @@ __device__ __forceinline__ void gamma_pair(const Rng& rng, uint32_t pair, uint32
   }
 }
 
-// ---- polar t draws (the t family's log-weight draws) ------------------------
-// Bailey's polar method (Math. Comp. 62 (1994) 779-781; oracle/vbrng.c restates
-// it): row n's candidates come from one stream of Philox blocks, attempt k at
-// counter (k, n, step, stream | kPolarPurpose << 24), two candidates per block;
-// u, v = ((int32) word + 1/2) 2^-31, W = u^2 + v^2, W < 1 accepted as the row's
-// next variate T = u sqrt(df expm1(-(2/df) log W) / W).  One transcendental set per
-// accepted variate instead of a Box-Muller normal and Marsaglia-Tsang gamma
-// attempts (each a Box-Muller normal and two logs).  Attempts are capped at D + 64
-// (a variate still missing is 0; P < 1e-30).  Log q's log1p(T^2 / df) takes
-// T^2 / df = (u^2 / W) expm1(.) from the same terms (no division by df, no rounded T).
-constexpr uint32_t kPolarPurpose = 65u;
+// ---- Bailey t draws (the t family's log-weight draws) -----------------------
+// Bailey, "Polar generation of random variates with the t-distribution", Math.
+// Comp. 62 (1994) 779-781: for U1, U2 iid U(0, 1),
+//   T = cos(2 pi U2) sqrt(df (U1^(-2/df) - 1))  ~  t(df)
+// (the polar method's radius W = U1 and angle drawn directly: no rejection, no
+// divergent loop).  One Philox block per column pair j of row n, counter (j, n,
+// step, stream | kBaileyPurpose << 24): variate 2 j from words (x, z), 2 j + 1
+// from (y, w); of each (lo, hi) pair U1 = (a + 1/2) 2^-40 with a = lo | (hi & 0xff)
+// << 32, and U2 = (hi >> 8) 2^-24 (|T| reaches sqrt(df (2^(82/df) - 1)): 11.2 at
+// df = 40, past the t(40) quantile of 1 - 1e-13).  Per variate one log, one exp,
+// one sin / cos pair, a square root and log q's log1p(T^2 / df) = log1p(cos^2
+// (U1^(-2/df) - 1)) -- a Box-Muller normal and Marsaglia-Tsang gamma attempts (each
+// a normal and two logs) before.  oracle/vbrng.c (family 2) restates it with libm.
+constexpr uint32_t kBaileyPurpose = 65u;
 
-__device__ __forceinline__ double polar_uniform(uint32_t w) {
-  return fma((double)(int32_t)w, 0x1p-31, 0x1p-32);
-}
-
-__device__ __forceinline__ double polar_w(uint32_t a, uint32_t b) {
-  const double u = polar_uniform(a), v = polar_uniform(b);
-  return fma(u, u, v * v);
-}
-
-// T of an accepted candidate (raw words a, b) and l1 = log1p(T^2 / df);
-// c2 = -2 / df (formed on the host as the oracle does)
-__device__ __forceinline__ double polar_t(uint32_t a, uint32_t b, double df, double c2,
-                                          const double2* ltab, double& l1) {
-  const double u = polar_uniform(a), v = polar_uniform(b);
-  const double W = fma(u, u, v * v);
-  const double em1 = expm1_pos(c2 * log_u01_tab(W, ltab));
-  double rw = __builtin_amdgcn_rcp(W);
-  rw = fma(rw, fma(-W, rw, 1.0), rw);
-  rw = fma(rw, fma(-W, rw, 1.0), rw);
-  const double c = em1 * rw;
-  l1 = log1p_pos_tab(u * u * c, ltab);       // T^2 / df = (u^2 / W) expm1
-  return u * sqrt_pos(df * c);
+// T of words (lo, hi) and l1 = log1p(T^2 / df); c2 = -2 / df (formed on the host
+// as the oracle forms it)
+__device__ __forceinline__ double bailey_t(uint32_t lo, uint32_t hi, double df, double c2,
+                                           const double2* sct, const double2* ltab, double& l1) {
+  const double a = hfma((double)(hi & 0xffu), 0x1p32, (double)lo);  // exact, 40 bits
+  const double u1 = hfma(a, 0x1p-40, 0x1p-41);                        // (a + 1/2) 2^-40
+  const double em1 = expm1_pos(c2 * log_u01_tab(u1, ltab));           // U1^(-2/df) - 1
+  const double cs = cospi_tab_u24(hi >> 8, sct);                      // cos(2 pi U2)
+  l1 = log1p_pos_tab(cs * cs * em1, ltab);
+  return cs * sqrt_pos(df * em1);
 }
 
 // ---- wave-level helpers (wave64) -------------------------------------------

@@ -2423,16 +2423,14 @@ int mf_wide_log_weights(FrWork* W, const MfSpec& f, const double* lam, long long
   if (int rc = reserve_n(W, D, m)) return rc;
   double* x = xs ? xs : W->X.d();
   if (f.fam == 1 && !host_eps) {
-    // the t family's Philox log-weight draws are polar t rows (as logw_row_kernel),
-    // their log q formed with them
-    FR_HIP(launch_sample_polar(D, m, lam, f.df, f.t_const, k0, k1, stream, step, x, W->zz.d(), st));
+    // the t family's Philox log-weight draws are Bailey pairs (as logw_row_kernel)
+    FR_HIP(launch_sample_bailey(D, m, lam, f.df, k0, k1, stream, step, x, st));
   } else {
     FR_HIP(launch_sample(f.fam, D, m, lam, f.t_scale, f.shape, host_eps, k0, k1, stream, step, x,
                          st));
   }
   if (int rc = eval_target(W, f.tgt, f.host, D, m, x, W->logp.d(), nullptr, st)) return rc;
-  if (!(f.fam == 1 && !host_eps))
-    FR_HIP(launch_family_logdensity(f.fam, D, m, lam, f.df, f.t_const, x, W->zz.d(), st));
+  FR_HIP(launch_family_logdensity(f.fam, D, m, lam, f.df, f.t_const, x, W->zz.d(), st));
   hipLaunchKernelGGL(sub_kernel, dim3(blocks(m)), dim3(256), 0, st, m, W->logp.d(), W->zz.d(), lw);
   FR_HIP(hipGetLastError());
   return 0;

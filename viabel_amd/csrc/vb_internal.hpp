@@ -96,11 +96,10 @@ hipError_t launch_row_mean(const double* hist, long long rows, long long P, long
                            double* out, hipStream_t s);
 
 // elementwise family helpers
-// polar t samples of a mean-field t family (the log-weight draws, vbrng.c family 2)
-// and their log q per row
-hipError_t launch_sample_polar(int D, long long m, const double* lam, double df, double t_const,
-                               uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* x,
-                               double* lq, hipStream_t s);
+// Bailey t samples of a mean-field t family (the log-weight draws, vbrng.c family 2)
+hipError_t launch_sample_bailey(int D, long long m, const double* lam, double df, uint32_t k0,
+                                uint32_t k1, uint32_t stream, uint32_t step, double* x,
+                                hipStream_t s);
 hipError_t launch_sample(int fam, int D, long long n, const double* lam, double t_scale,
                          double shape, const double* noise, uint32_t k0, uint32_t k1,
                          uint32_t stream, uint32_t step, double* x, hipStream_t s);

@@ -2136,14 +2136,18 @@ __device__ __forceinline__ void draw_pair(const Rng& rng, const double* noise, i
   if constexpr (HOST) {
     eA = noise[r * D + dA];
     eB = dB < D ? noise[r * D + dB] : 0.0;
+  } else if constexpr (TFAM) {
+    // the log-weight draws of the t family: Bailey pairs (bailey_t); shape and
+    // t_scale belong to the estimators' normal / gamma draws
+    (void)t_scale;
+    (void)shape;
+    const u4 w = rng.draw((uint32_t)j, (uint32_t)r, step, kBaileyPurpose);
+    const double df = 2.0 * shape, c2 = -2.0 / df;
+    double l1;
+    eA = bailey_t(w.x, w.z, df, c2, sct, lt, l1);
+    eB = bailey_t(w.y, w.w, df, c2, sct, lt, l1);
   } else {
     normal_pair_tab(rng.draw((uint32_t)j, (uint32_t)r, step, 0u), eA, eB, sct, lt);
-    if constexpr (TFAM) {
-      double ga, gb;
-      gamma_pair<true>(rng, (uint32_t)j, (uint32_t)r, step, shape, ga, gb, sct, lt);
-      eA = t_scale * eA / sqrt(ga);
-      eB = t_scale * eB / sqrt(gb);
-    }
   }
 }
 
@@ -2221,119 +2225,6 @@ __global__ __launch_bounds__(256) void logw_sep_kernel(int D, long long m, const
   if (lane == 0) lw[r] = lp - lq;
 }
 
-// Separable targets, t family, Philox: the polar t draws need the row's candidates
-// in stream order, so one thread walks a row (the wave-per-row logw_sep_kernel
-// splits a row's pairs over lanes); each accepted candidate is transformed, scaled
-// and evaluated (target and log q terms) as it is accepted.  lam rows stay in L2.
-template <class TGT>
-__global__ __launch_bounds__(256) void logw_sep_polar_kernel(int D, long long m, const double* lam,
-                                                             double df, double t_const, Rng rng,
-                                                             uint32_t step, uint32_t stride,
-                                                             double* lw, double* xs) {
-  __shared__ double2 s_sct[kSinCosN];
-  __shared__ double2 s_lt[kLogN + kLogU01N];
-  load_bm_tables(s_sct, s_lt);
-  __syncthreads();
-  const int q = blockIdx.y;
-  lam += (long long)q * 2 * D;
-  lw += (long long)q * m;
-  if (xs) xs += (long long)q * m * D;
-  rng.stream += (uint32_t)q * stride;
-  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (r >= m) return;
-  const double c2 = -2.0 / df, hdf1 = 0.5 * (df + 1.0);
-  double lp = 0.0, lq = 0.0;
-  int cnt = 0;
-  const uint32_t kmax = (uint32_t)D + 64u;
-  auto take = [&](uint32_t a, uint32_t b) {
-    double l1;
-    const double T = polar_t(a, b, df, c2, s_lt, l1);
-    const double mu = lam[cnt], ls = lam[D + cnt];
-    const double x = T * exp(ls) + mu;
-    double g;
-    lp += TGT::lp1(x, g);
-    lq += t_const - l1 * hdf1 - ls;
-    if (xs) xs[r * D + cnt] = x;
-    ++cnt;
-  };
-  for (uint32_t k = 0; cnt < D && k < kmax; ++k) {
-    const u4 w = rng.draw(k, (uint32_t)r, step, kPolarPurpose);
-    if (polar_w(w.x, w.y) < 1.0) take(w.x, w.y);
-    if (cnt < D && polar_w(w.z, w.w) < 1.0) take(w.z, w.w);
-  }
-  // (never taken in practice) variates still missing are 0: x = mu
-  for (; cnt < D; ++cnt) {
-    const double mu = lam[cnt], ls = lam[D + cnt];
-    double g;
-    lp += TGT::lp1(mu, g);
-    lq += t_const - ls;
-    if (xs) xs[r * D + cnt] = mu;
-  }
-  lw[r] = lp - lq;
-}
-
-// Polar t samples x [m][D] of rows of a mean-field t family and their log q (the
-// materialised log-weight path: host-callback or non-separable wide targets), one
-// thread per row as logw_sep_polar_kernel.
-__global__ __launch_bounds__(256) void sample_polar_kernel(int D, long long m, const double* lam,
-                                                           double df, double t_const, Rng rng,
-                                                           uint32_t step, double* x, double* lq_out) {
-  __shared__ double2 s_sct[kSinCosN];
-  __shared__ double2 s_lt[kLogN + kLogU01N];
-  load_bm_tables(s_sct, s_lt);
-  __syncthreads();
-  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (r >= m) return;
-  const double c2 = -2.0 / df, hdf1 = 0.5 * (df + 1.0);
-  double lq = 0.0;
-  int cnt = 0;
-  const uint32_t kmax = (uint32_t)D + 64u;
-  auto take = [&](uint32_t a, uint32_t b) {
-    double l1;
-    const double T = polar_t(a, b, df, c2, s_lt, l1);
-    const double ls = lam[D + cnt];
-    x[r * D + cnt] = T * exp(ls) + lam[cnt];
-    lq += t_const - l1 * hdf1 - ls;
-    ++cnt;
-  };
-  for (uint32_t k = 0; cnt < D && k < kmax; ++k) {
-    const u4 w = rng.draw(k, (uint32_t)r, step, kPolarPurpose);
-    if (polar_w(w.x, w.y) < 1.0) take(w.x, w.y);
-    if (cnt < D && polar_w(w.z, w.w) < 1.0) take(w.z, w.w);
-  }
-  for (; cnt < D; ++cnt) {
-    x[r * D + cnt] = lam[cnt];
-    lq += t_const - lam[D + cnt];
-  }
-  lq_out[r] = lq;
-}
-
-// The polar t candidates of row r (see polar_t, vb_device.hpp): thread t walks the
-// row's attempt stream, storing each accepted candidate's raw words in its next slot
-// (LDS, slots[i * 256 + t], i < DMAX); the loop ends when every lane has D
-// variates (or D + 64 attempts).  Returns the number of variates stored.  The
-// transcendentals run afterwards, once per variate, outside the divergent loop.
-__device__ __forceinline__ int polar_row(const Rng& rng, long long r, int D, uint32_t step,
-                                         uint2* slots) {
-  const int t = threadIdx.x;
-  int cnt = 0;
-  const uint32_t kmax = (uint32_t)D + 64u;
-  for (uint32_t k = 0; cnt < D && k < kmax; ++k) {
-    const u4 w = rng.draw(k, (uint32_t)r, step, kPolarPurpose);
-    const bool aa = polar_w(w.x, w.y) < 1.0;
-    const bool ab = polar_w(w.z, w.w) < 1.0;
-    if (aa) {
-      slots[cnt * 256 + t] = make_uint2(w.x, w.y);
-      ++cnt;
-    }
-    if (ab && cnt < D) {
-      slots[cnt * 256 + t] = make_uint2(w.z, w.w);
-      ++cnt;
-    }
-  }
-  return cnt;
-}
-
 // any target with D <= DMAX: one thread per draw
 template <class TGT, bool TFAM, bool HOST, int DMAX>
 __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const double* lam,
@@ -2344,8 +2235,8 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
   __shared__ double s_mu[DMAX], s_ls[DMAX], s_sg[DMAX];
-  // t family, Philox: the row's accepted polar candidates (polar_row), [DMAX][256]
-  __shared__ uint2 s_pol[(TFAM && !HOST) ? DMAX * 256 : 1];
+  // t family, Philox: the row's samples x, [DMAX][256] (see below)
+  __shared__ double s_x[(TFAM && !HOST) ? DMAX * 256 : 1];
   // row q of a batched launch (vb_log_weights_rows): its own lambda, output
   // row, noise rows and Philox stream (stream + q * stride)
   const int q = blockIdx.y;
@@ -2369,25 +2260,36 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
   double x[DMAX], g[DMAX];
   double lq = 0.0;
   if constexpr (TFAM && !HOST) {
-    // polar t draws (the log-weight draws of the t family, vbrng.c family 2):
-    // log q = t_const - (df + 1)/2 log1p(T^2 / df) - log sigma at the draw itself
-    // (x = mu + sigma T rounded moves it by ~1e-16 relative)
-    const int cnt = polar_row(rng, r, D, step, s_pol);
+    // Bailey t draws (the log-weight draws of the t family, bailey_t; vbrng.c
+    // family 2), log q = t_const - (df + 1)/2 log1p(T^2 / df) - log sigma at the
+    // draw itself (x = mu + sigma T rounded moves it by ~1e-16 relative).  One
+    // column pair per iteration of a rolled loop (the polynomial constants stay in
+    // registers; unrolled, they were re-made for every variate), x written to LDS,
+    // then read back as a register array for the target.
     const double c2 = -2.0 / df, hdf1 = 0.5 * (df + 1.0);
+    const int t = threadIdx.x;
+#pragma unroll 1
+    for (int j = 0; 2 * j < D; ++j) {
+      const u4 w = rng.draw((uint32_t)j, (uint32_t)r, step, kBaileyPurpose);
+      double la, lb;
+      const double ta = bailey_t(w.x, w.z, df, c2, s_sct, s_lt, la);
+      const double tb = bailey_t(w.y, w.w, df, c2, s_sct, s_lt, lb);
+      const int d = 2 * j;
+      const double xa = ta * s_sg[d] + s_mu[d];
+      lq += t_const - la * hdf1 - s_ls[d];
+      s_x[d * 256 + t] = xa;
+      if (d + 1 < D) {
+        const double xb = tb * s_sg[d + 1] + s_mu[d + 1];
+        lq += t_const - lb * hdf1 - s_ls[d + 1];
+        s_x[(d + 1) * 256 + t] = xb;
+        if (xs) xs[r * D + d + 1] = xb;
+      }
+      if (xs) xs[r * D + d] = xa;
+    }
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
-      x[d] = 0.0;
+      x[d] = d < D ? s_x[d * 256 + t] : 0.0;
       g[d] = 0.0;
-      if (d < D) {
-        const uint2 wd = s_pol[d * 256 + threadIdx.x];
-        double l1;
-        double T = polar_t(wd.x, wd.y, df, c2, s_lt, l1);
-        T = d < cnt ? T : 0.0;
-        l1 = d < cnt ? l1 : 0.0;
-        x[d] = T * s_sg[d] + s_mu[d];
-        lq += t_const - l1 * hdf1 - s_ls[d];
-        if (xs) xs[r * D + d] = x[d];
-      }
     }
   } else {
 #pragma unroll
@@ -2630,13 +2532,37 @@ hipError_t launch_sample(int fam, int D, long long n, const double* lam, double 
   return hipGetLastError();
 }
 
-hipError_t launch_sample_polar(int D, long long m, const double* lam, double df, double t_const,
-                               uint32_t k0, uint32_t k1, uint32_t stream, uint32_t step, double* x,
-                               double* lq, hipStream_t s) {
-  if (m == 0) return hipSuccess;
+// Bailey t samples x [m][D] of a mean-field t family (the log-weight draws of the
+// materialised path), one thread per (row, column pair) as sample_kernel
+__global__ __launch_bounds__(256) void sample_bailey_kernel(int D, long long n, const double* lam,
+                                                            double df, Rng rng, uint32_t step,
+                                                            double* x) {
+  __shared__ double2 s_sct[kSinCosN];
+  __shared__ double2 s_lt[kLogN + kLogU01N];
+  load_bm_tables(s_sct, s_lt);
+  __syncthreads();
+  const int npairs = (D + 1) / 2;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= n * npairs) return;
+  const long long r = idx / npairs;
+  const int j = (int)(idx % npairs);
+  const u4 w = rng.draw((uint32_t)j, (uint32_t)r, step, kBaileyPurpose);
+  const double c2 = -2.0 / df;
+  double l1;
+  const double ta = bailey_t(w.x, w.z, df, c2, s_sct, s_lt, l1);
+  const double tb = bailey_t(w.y, w.w, df, c2, s_sct, s_lt, l1);
+  x[r * D + 2 * j] = ta * exp(lam[D + 2 * j]) + lam[2 * j];
+  if (2 * j + 1 < D) x[r * D + 2 * j + 1] = tb * exp(lam[D + 2 * j + 1]) + lam[2 * j + 1];
+}
+
+hipError_t launch_sample_bailey(int D, long long m, const double* lam, double df, uint32_t k0,
+                                uint32_t k1, uint32_t stream, uint32_t step, double* x,
+                                hipStream_t s) {
+  const long long tot = m * ((D + 1) / 2);
+  if (tot == 0) return hipSuccess;
   const Rng rng{k0, k1, stream};
-  hipLaunchKernelGGL(sample_polar_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, D, m,
-                     lam, df, t_const, rng, step, x, lq);
+  hipLaunchKernelGGL(sample_bailey_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, D,
+                     m, lam, df, rng, step, x);
   return hipGetLastError();
 }
 
@@ -2868,14 +2794,7 @@ template <class TGT, bool TFAM, bool HOST>
 static void logw_launch(int D, long long m, const double* lam, double t_scale, double shape,
                         double df, double t_const, const double* noise, Rng rng, uint32_t step,
                         int rows, uint32_t stride, double* lw, double* xs, hipStream_t s) {
-  if constexpr (TGT::kSeparable && TFAM && !HOST) {
-    if (D > kBlockDMax) {
-      hipLaunchKernelGGL((logw_sep_polar_kernel<TGT>),
-                         dim3((unsigned)((m + 255) / 256), (unsigned)rows), dim3(256), 0, s, D, m,
-                         lam, df, t_const, rng, step, stride, lw, xs);
-      return;
-    }
-  } else if constexpr (TGT::kSeparable) {
+  if constexpr (TGT::kSeparable) {
     if (D > kBlockDMax) {
       hipLaunchKernelGGL((logw_sep_kernel<TGT, TFAM, HOST>),
                          dim3((unsigned)((m + 3) / 4), (unsigned)rows), dim3(256), 0, s, D, m,

@@ -127,8 +127,16 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
             experiments.log_weights(target, fj, smooth[j], n_bounds, return_samples=False,
                                     lw_out=lw[j])
     # the divergence statistics of all restarts in one batched reduction chain,
-    # then the O(D) bound algebra for all restarts at once on the host
+    # then the PSIS k-hats (psis.py:112-208's kss; the smoothed weights are not
+    # needed here) on a worker thread -- its C calls release the GIL and mostly
+    # wait for the device -- while this thread runs the O(D) bound algebra and the
+    # Monte Carlo warnings of all restarts on the host
     div = bounds.divergence_rows(lw)
+    khat_fn = lambda: psis.psis_khat(lw.t()) if len(ids) > 1 else np.array([psis.psis_khat(lw[0])])
+    # (a full-rank family's moments below call the library: no concurrent calls
+    # on the context, so the k-hats run first there)
+    khat_job = _psis_worker().submit(khat_fn) if bfam.kind != nat.FAMILY_FR_T else None
+    khat = khat_fn() if khat_job is None else None
     if bfam.kind == nat.FAMILY_FR_T:
         # full-rank q: the family's own moments and covariance (eigenvalues of
         # Sigma on the device), restart by restart, as all_bounds does
@@ -141,8 +149,8 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
                          res['mean_error'], res['std_error'], res['cov_error']])
     else:
         recs = bounds_records(ids, div, smooth, bfam)
-    # k-hat only (psis.py:112-208's kss): the smoothed weights are not needed here
-    khat = psis.psis_khat(lw.t()) if len(ids) > 1 else np.array([psis.psis_khat(lw[0])])
+    if khat_job is not None:
+        khat = khat_job.result()
     if timings is not None:
         _sync()
         t2 = time.perf_counter()
@@ -150,6 +158,19 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
         timings['bounds_psis_s'] = t2 - t1
     return np.array([np.concatenate([rec, [khat[j], vals[j, -1]], smooth[j]])
                      for j, rec in enumerate(recs)])
+
+
+_WORKER = []
+
+
+def _psis_worker():
+    """One persistent worker thread for the restart table's PSIS calls (made on
+    first use; a new thread per call costs more than the overlap gains)."""
+    if not _WORKER:
+        import concurrent.futures
+        _WORKER.append(concurrent.futures.ThreadPoolExecutor(max_workers=1,
+                                                             thread_name_prefix='viabel_amd_psis'))
+    return _WORKER[0]
 
 
 def bounds_records(ids, div, lams, fam):
