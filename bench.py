@@ -276,6 +276,10 @@ def coll_device(dev):
     return torch.device('cpu') if COLL_CPU else dev
 
 
+# the round whose committed counter passes (profiles/<round>/) price the bench line
+PROFILE_ROUND = 'r06'
+
+
 def load_traffic():
     p = os.path.join(ROOT, 'profiles', 'traffic.json')
     try:
@@ -291,7 +295,7 @@ def load_valu_busy():
     at), from the committed record scripts/gpu_valu_busy.sh wrote.  A measured
     counterpart to the instruction-count model's frac, which prices every VALU
     instruction at 4 cycles."""
-    p = os.path.join(ROOT, 'profiles', 'r05', 'valu_busy_headline.json')
+    p = os.path.join(ROOT, 'profiles', PROFILE_ROUND, 'valu_busy_headline.json')
     try:
         with open(p) as f:
             d = json.load(f)
@@ -300,7 +304,9 @@ def load_valu_busy():
     disp = d.get('dispatches') or []
     return {'busy': d.get('timed_dispatch_valu_busy'),
             'clock_ghz': disp[-1].get('clock_ghz') if disp else None,
-            'formula': d.get('formula'), 'source': 'profiles/r05/valu_busy_headline.json'}
+            'formula': d.get('formula'),
+            'source': 'profiles/%s/valu_busy_headline.json (raw counters: '
+                      'valu_busy_headline_counters.csv beside it)' % PROFILE_ROUND}
 
 
 def roofline_cfg3(launches, n, traffic):
@@ -495,9 +501,9 @@ def latency_roofline(step_s, d, n, chivi, host_layout, n_problems, note):
 def cfg5_stage_valu(stage_s, local, n_restarts):
     """VALU issue fraction of config 5's bounds / PSIS stage: the stage's
     SQ_INSTS_VALU from a committed counter pass over the same stage
-    (profiles/r05/cfg5/bounds_stage_pmc.json, scripts/gpu_cfg5_pmc.sh; 64
+    (profiles/<round>/cfg5/bounds_stage_pmc.json, scripts/gpu_cfg5_pmc.sh; 64
     restarts x M = 1e6, scaled to this rank's restarts) over the live stage time."""
-    p = os.path.join(ROOT, 'profiles', 'r05', 'cfg5', 'bounds_stage_pmc.json')
+    p = os.path.join(ROOT, 'profiles', PROFILE_ROUND, 'cfg5', 'bounds_stage_pmc.json')
     try:
         prof = json.load(open(p))
     except (OSError, ValueError):
@@ -509,8 +515,9 @@ def cfg5_stage_valu(stage_s, local, n_restarts):
     return {'valu_instr': vi, 'achieved': vi / stage_s / 1e9, 'peak': VALU_PEAK_GINSTR,
             'unit': 'G wave-instr/s', 'frac': vi / stage_s / 1e9 / VALU_PEAK_GINSTR,
             'logw_kernel_valu_frac': k.get('valu_frac'),
-            'source': 'SQ_INSTS_VALU of the stage (profiles/r05/cfg5/bounds_stage_pmc.json) / '
-                      'live stage seconds; the log-weight kernel fraction is from the profile'}
+            'source': 'SQ_INSTS_VALU of the stage (profiles/%s/cfg5/bounds_stage_pmc.json; raw '
+                      'counters bounds_stage_sq_counters.csv beside it) / live stage seconds; the '
+                      'log-weight kernel fraction is from the profile' % PROFILE_ROUND}
 
 
 def _cfg4_problem():

@@ -951,11 +951,13 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
   // parameter while the rows run (same order, oldest first), so the update adds
   // only the newest square (the same bits as the whole loop)
   const bool qpre = kPF && k_opt == 0 && !k_emit && W >= 1 && W <= kBlockQpreMaxW;
-  // KLVI: the copy wave sums step s + 1's window (but its newest slot) after step s's
+  // The copy wave sums step s + 1's window (but its newest slot) after step s's
   // reduction barrier, beside the update, instead of before that barrier, which it held
-  // (profiles/r05/copy_wave_ts.log); the update adds the previous gradient's square
-  // (gprev) and its own -- the same additions in the same order
-  const bool qnext = qpre && !k_chivi && W >= 2;
+  // (KLVI, profiles/r05/copy_wave_ts.log; CHIVI from round 6: its sums after the block-
+  // max barrier made the rows wait ~575 cycles at the reduction barrier,
+  // profiles/r06/block_ts.log); the update adds the previous gradient's square (gprev)
+  // and its own -- the same additions in the same order
+  const bool qnext = qpre && W >= 2;
   double* lam_g = a.lam + (long long)prob * P;
   double* ring_g = a.ring ? a.ring + (long long)prob * W * P : nullptr;
 
@@ -1550,18 +1552,56 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
         }
       };
       if (k_chivi) {
-        // CHIVI: the sums run after the block-max barrier, beside the rows' rescale and
+        // CHIVI: sum_d log sigma_d (and at a run's first step, or without qnext, the
+        // window sums) after the block-max barrier, beside the rows' rescale and
         // reduce-scatter, instead of holding that barrier (the copy wave arrived last
         // there: profiles/r05/copy_wave_ts.log); s_lam is still the pre-update lambda
-        // until the reduction barrier.  (KLVI keeps them before its first barrier, the
-        // reduction one, in a separate copy of the code: sharing one lambda changed the
-        // KLVI instances' code and cost config 1 3 %.)
+        // until the reduction barrier.  With qnext the next step's window sums run after
+        // the reduction barrier, beside the update (below).  (KLVI keeps its code in a
+        // separate copy: sharing one lambda changed the KLVI instances' code and cost
+        // config 1 3 %.)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         VB_CT(3);
         __builtin_amdgcn_s_barrier();   // the block-max barrier
         VB_CT(4);
-        presums();
+        if (!(qnext && s > 0)) {
+          presums();
+        } else {
+          cslot = cslot + 1 == W ? 0 : cslot + 1;
+          if (lane == 0) {   // sum_d log sigma_d for the value (same order as the rows' loop)
+            double sl = 0.0;
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) {
+              const double l = s_lam[D + d];
+              sl += d < D ? l : 0.0;
+            }
+            s_sl = sl;
+          }
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (qnext) {
+          __builtin_amdgcn_s_barrier();   // the reduction barrier
+          if (lane < P && s + 1 < a.n_steps) {
+            // as KLVI's qnext below: step s + 1's older slots but the newest, oldest first
+            const long long i1 = a.step0 + s + 1;
+            const int cnt = (i1 + 1 < W) ? (int)(i1 + 1) : W;
+            const int oldest = (cnt < W || cslot + 1 == W) ? 0 : cslot + 1;
+            double q = 0.0;
+            for (int k = 0; k + 2 < cnt; ++k) {
+              int Lk = oldest + k;
+              if (Lk >= W) Lk -= W;
+              const double t = s_ring[Lk * P + lane];
+              q = __dadd_rn(q, __dmul_rn(t, t));
+            }
+            s_qpre[(s + 1) & 1][lane] = q;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          }
+          __builtin_amdgcn_s_barrier();   // the end-of-step barrier
+#ifdef VB_BLOCK_TS
+          tc = clock64();
+#endif
+          continue;
+        }
       } else {
         if (qpre && lane < P && !(qnext && s > 0)) {
           const long long i = a.step0 + s;
@@ -1711,10 +1751,9 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) sl += d < D ? s_lam[D + d] : 0.0;
     }
-    // (block_kernel's copy wave: sum_d log sigma_d before the reduction barrier;
-    // CHIVI sums the step's window but its newest slot after the block-max barrier,
-    // KLVI the NEXT step's window but its two newest slots after the reduction
-    // barrier, beside the update -- qnext)
+    // (block_kernel's copy wave: sum_d log sigma_d before the reduction barrier, the
+    // NEXT step's window but its two newest slots after the reduction barrier, beside
+    // the update -- qnext, KLVI and CHIVI)
     if (copy && lane == 0) s_sl = sl;
     // accumulators: a cheap function of the last update (one LDS read and K adds; a
     // per-k read of s_lam[k % P] spent an integer division per accumulator and made
@@ -1730,10 +1769,6 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
         if (lane == 0) s_max[wid] = wm;
       }
       __syncthreads();
-      if (copy) {
-        const int cnt = s + 1 < W ? s + 1 : W;
-        window_sum(s + 1 - cnt, cnt - 1, s_qpre[s & 1]);
-      }
       double mq[kBlockMaxRowWaves];
 #pragma unroll
       for (int q = 0; q < kBlockMaxRowWaves; ++q) mq[q] = s_max[q];
@@ -1743,7 +1778,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
     }
     if (row_wave) wave_reduce_scatter<K>(acc, s_red[wid]);
     __syncthreads();
-    if (copy && !chivi) {
+    if (copy) {
       // step s + 1's window (min(s + 2, W) slots) without steps s and s + 1
       const int cnt1 = s + 2 < W ? s + 2 : W;
       window_sum(s + 2 - cnt1, cnt1 - 2, s_qpre[(s + 1) & 1]);
@@ -1766,8 +1801,8 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
       double q = 0.0;
       if (qpre) {
         const double qo = s_qpre[s & 1][p];
-        q = (!chivi && s > 0) ? __dadd_rn(__dadd_rn(qo, __dmul_rn(gprev, gprev)), __dmul_rn(gp, gp))
-                              : __dadd_rn(qo, __dmul_rn(gp, gp));
+        q = s > 0 ? __dadd_rn(__dadd_rn(qo, __dmul_rn(gprev, gprev)), __dmul_rn(gp, gp))
+                  : __dadd_rn(qo, __dmul_rn(gp, gp));
         gprev = gp;
       } else {
         const int cnt = (s + 1 < W) ? s + 1 : W;
