@@ -28,7 +28,8 @@ for i in $(seq 1 ${ROUNDS:-3}); do
 import json, sys
 d = json.loads([l for l in open('gpurun_out/ab_legs.json') if l.startswith('{')][-1])
 c = d['configs']
-out = {'lib': sys.argv[1], 'headline_us': round(d['ms_per_step'] * 1e3, 3)}
+out = {'lib': sys.argv[1], 'headline_us': round(d['ms_per_step'] * 1e3, 3),
+       'headline_launch_us': round(d['roofline']['launch_ms_mean'] * 1e3, 2)}
 for k in ('cfg1', 'cfg2'):
     if k in c: out[k + '_us'] = round(c[k].get('ms_per_step', float('nan')) * 1e3, 3)
 if 'cfg4' in c:

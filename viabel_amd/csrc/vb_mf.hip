@@ -1657,8 +1657,8 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
     }
 #ifdef VB_BLOCK_TS
     if (prob == 0 && lane == 0 && a.n_steps > 0)
-      printf("COPYTS steps=%d | vmcnt wait %.0f issue %.0f window sums %.0f log-sigma sum + drain %.0f first barrier wait %.0f\n",
-             a.n_steps, (double)ct[0] / a.n_steps, (double)ct[1] / a.n_steps, (double)ct[2] / a.n_steps,
+      printf("COPYTS hw_id=0x%x steps=%d | vmcnt wait %.0f issue %.0f window sums %.0f log-sigma sum + drain %.0f first barrier wait %.0f\n",
+             (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)), a.n_steps, (double)ct[0] / a.n_steps, (double)ct[1] / a.n_steps, (double)ct[2] / a.n_steps,
              (double)ct[3] / a.n_steps, (double)ct[4] / a.n_steps);
 #endif
 #undef VB_CT
@@ -1682,9 +1682,9 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
 #endif
 #undef VB_PH
 #ifdef VB_BLOCK_TS
-  if (prob == 0 && tid == 0 && a.n_steps > 0)
-    printf("BLOCKTS D=%d N=%d NT=%d RW=%d chivi=%d steps=%d cyc/step=%.0f | rows %.0f max+bar %.0f rs %.0f bar %.0f upd %.0f bar %.0f\n",
-           D, N, NT, RW, k_chivi ? 1 : 0, a.n_steps, (double)(clock64() - tb0) / a.n_steps,
+  if (prob == 0 && lane == 0 && row_wave && a.n_steps > 0)
+    printf("BLOCKTS wave=%d hw_id=0x%x D=%d N=%d NT=%d RW=%d chivi=%d steps=%d cyc/step=%.0f | rows %.0f max+bar %.0f rs %.0f bar %.0f upd %.0f bar %.0f\n",
+           wid, (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)), D, N, NT, RW, k_chivi ? 1 : 0, a.n_steps, (double)(clock64() - tb0) / a.n_steps,
            (double)bt[0] / a.n_steps, (double)bt[1] / a.n_steps, (double)bt[2] / a.n_steps,
            (double)bt[3] / a.n_steps, (double)bt[4] / a.n_steps, (double)bt[5] / a.n_steps);
 #endif
