@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 6: stream-K Newton-Schulz Y|Z launch (one block per CU) -- full-rank / config-4
+# / switch tests, interleaved config-4 A/B against VIABEL_AMD_GEMM_SK=0, then the
+# rocprofv3 one-step timeline of config 4.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r06p
+timeout -k 10 900 python -u -m pytest tests/test_gpu_fullrank.py tests/test_gpu_configs.py tests/test_gpu_headline.py "tests/test_gpu_switches.py::test_gemm_sk_off_matches_default" "tests/test_gpu_switches.py::test_full_rank_switch_off_matches_default" -x -q --timeout 300 --timeout-method thread > gpurun_out/r06p/pytest.log 2>&1
+rc=$?; tail -3 gpurun_out/r06p/pytest.log; [ $rc -ne 0 ] && exit $rc
+LEGS=cfg4 ROUNDS=3 LIBS="new+VIABEL_AMD_GEMM_SK=0 new" bash scripts/gpu_ab_legs.sh || exit $?
+OUT=gpurun_out/r06p/prof_fr bash scripts/gpu_cfg4_timeline.sh

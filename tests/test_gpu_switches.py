@@ -11,7 +11,8 @@ each side runs in a child process; the child writes its run's result
   FR_PCG_SS=0 (full rank: separate launches, full symmetric products, the schedule
   and the weights in their own kernels, the PCG's products and vector updates as
   separate launches): other reduction / contraction orders -> equal to 1e-9
-  of the largest entry over a short trajectory.
+  of the largest entry over a short trajectory.  VIABEL_AMD_GEMM_SK=0 (the
+  Newton-Schulz Y|Z pair without stream-K) likewise, at D = 512.
 * VIABEL_AMD_HOST_TRACE=1 (host timestamps of the column-pair launch path on
   stderr): the same bits, and the trace lines are there.
 * VIABEL_AMD_DIV_TWO_PASS=0 (divergence statistics in numpy's three passes at every
@@ -49,8 +50,8 @@ if kind == 'block':
     run = vb.DeviceRun(obj, 400, init, learning_rate=0.01)
     run.advance_philox(7, 3, 2, 0)
     run.advance_philox(393, 3, 2, 7)
-elif kind == 'fullrank':
-    D, N = 64, 32
+elif kind in ('fullrank', 'fullrank512'):
+    D, N = (512, 128) if kind == 'fullrank512' else (64, 32)
     rs = np.random.RandomState(9)
     tri = np.tril_indices(D)
     free = rs.randn(len(tri[0])) * 0.01
@@ -108,6 +109,19 @@ def test_block_pf_off_matches_default(tmp_path):
 def test_full_rank_switch_off_matches_default(tmp_path, switch):
     ref, _ = _run(tmp_path, 'fullrank', {}, 'default')
     out, _ = _run(tmp_path, 'fullrank', {switch: '0'}, 'off')
+    for k in ('lam', 'hist', 'vals'):
+        _close(out[k], ref[k], 1e-9)
+
+
+def test_gemm_sk_off_matches_default(tmp_path):
+    """VIABEL_AMD_GEMM_SK=0 (the Newton-Schulz Y|Z pair as one block per tile) against
+    the default stream-K launch at D = 512, where the pair's 272 tiles exceed the 256
+    CUs and stream-K runs: the split tiles add their two k parts in another order ->
+    equal to 1e-9 of the largest entry over 12 steps (as the other full-rank
+    switches)."""
+    ref, _ = _run(tmp_path, 'fullrank512', {}, 'default')
+    out, _ = _run(tmp_path, 'fullrank512', {'VIABEL_AMD_GEMM_SK': '0'}, 'off')
+    assert np.all(np.isfinite(ref['vals']))
     for k in ('lam', 'hist', 'vals'):
         _close(out[k], ref[k], 1e-9)
 

@@ -1403,6 +1403,11 @@ struct FrWork {
   // D
   Buf w, offd, scal, pv[4];
   Buf info, sched, fro_part, tpart[2], pq_part, rz_part, rr_part, ee_part;
+  // stream-K scratch of the Newton-Schulz Y|Z launches (GemmOp::sk_part / sk_flag):
+  // a partial tile and a flag per upper-triangle tile of the pair; sk_epoch tags
+  // each launch (flags start at 0)
+  Buf sk_part, sk_flag;
+  int sk_epoch = 0;
   FrSched* host_sched = nullptr;  // pinned copy of the schedule / status block
   const double* Yf = nullptr;     // final Newton-Schulz iterates (A^(1/2), A^(-1/2))
   const double* Zf = nullptr;
@@ -1510,6 +1515,13 @@ int reserve_d(FrWork* W, int D, hipStream_t st) {
   for (FrWork::Buf* b : {&W->fro_part, &W->tpart[0], &W->tpart[1], &W->pq_part, &W->rz_part})
     FR_HIP(b->reserve(sizeof(double) * 4 * nblk));
   for (FrWork::Buf* b : {&W->rr_part, &W->ee_part}) FR_HIP(b->reserve(sizeof(double) * nblk));
+  {
+    const size_t nt = (size_t)((D + 31) / 32), npair = nt * (nt + 1);   // tiles of the Y|Z pair
+    FR_HIP(W->sk_part.reserve(sizeof(double) * 1024 * npair));
+    FR_HIP(W->sk_flag.reserve(sizeof(int) * npair));
+    FR_HIP(hipMemsetAsync(W->sk_flag.p, 0, sizeof(int) * npair, st));
+    W->sk_epoch = 0;
+  }
   if (!W->sched.p) {
     FR_HIP(W->sched.reserve(sizeof(FrSched)));
     FR_HIP(hipMemsetAsync(W->sched.p, 0, sizeof(FrSched), st));
@@ -1747,6 +1759,13 @@ int fr_sqrt(FrWork* W, int D, const double* lam, hipStream_t st, bool warm, cons
       }
       g.conv_iter_out = &sc->ns_iter;
       g.conv_iter = k;
+    }
+    // stream-K scratch (gemm_group takes it where the tile count suits, D = 512)
+    const int epoch = ++W->sk_epoch > 0 ? W->sk_epoch : (W->sk_epoch = 1);
+    for (GemmOp& g : yz) {
+      g.sk_part = W->sk_part.d();
+      g.sk_flag = static_cast<int*>(W->sk_flag.p);
+      g.sk_epoch = epoch;
     }
     FR_HIP(gemm_group(yz, 2, st));
   }

@@ -129,6 +129,15 @@ struct GemmOp {
   // set by gemm_group: M, N multiples of 32, K of KTG, 16-byte aligned operand rows, no
   // kscale / dual product -> the LDS-DMA main loop
   int glds;
+  // stream-K (the grouped Newton-Schulz Y|Z product, gemm_group): when set on both ops
+  // of a symmetric pair whose tiles slightly outnumber the CUs, the k stages of all
+  // tiles are dealt evenly over one block per CU; a tile split between two blocks is
+  // finished by the block holding its first stages, which adds the partial tile the
+  // other block left in sk_part[tile] (flagged sk_flag[tile] = sk_epoch, a value
+  // distinct per launch).  Scratch: 1024 doubles and one int per tile of the pair.
+  double* sk_part;
+  int* sk_flag;
+  int sk_epoch;
 };
 
 // Up to two independent GEMMs of equal shape / transposes in one launch
@@ -385,7 +394,8 @@ __device__ unsigned long long g_gemm_ts[1024][24];
 // runs after the first stages are issued (a hook's loads then overlap them).
 template <bool TA, bool TB, bool KSC, class Mid>
 __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, double* lds,
-                                              d4 (&acc)[4], const double* ks, Mid&& mid) {
+                                              d4 (&acc)[4], const double* ks, Mid&& mid,
+                                              int st0 = 0, int nst = -1) {
   // A rows: m when not transposed (k contiguous), k when transposed.
   // B rows: n when transposed (k contiguous), k otherwise.
   constexpr bool AK = !TA, BK = TB;
@@ -394,11 +404,13 @@ __device__ __forceinline__ void mainloop_glds(const GemmOp& g, int i0, int j0, d
   const int wm = q >> 1, wn = q & 1;
   double* sA = lds;                 // [GS][TD]
   double* sB = lds + GS * TD;       // [GS][TD]
-  const int nt = g.K / KTG;
+  // (stream-K: the k stages [st0, st0 + nst) only)
+  const int nt = nst < 0 ? g.K / KTG : nst;
   // per-lane global sources: tile origin + fixed offsets; the origin moves by KTG
   // along k each tile (k is the row index of the "rows = k" layouts)
-  const double* a0 = g.A + (AK ? (long long)i0 * g.lda : (long long)i0);
-  const double* b0 = g.B + (BK ? (long long)j0 * g.ldb : (long long)j0);
+  const long long kb0 = (long long)st0 * KTG;
+  const double* a0 = g.A + (AK ? (long long)i0 * g.lda + kb0 : (long long)i0 + kb0 * g.lda);
+  const double* b0 = g.B + (BK ? (long long)j0 * g.ldb + kb0 : (long long)j0 + kb0 * g.ldb);
   long long aoff[NSUB], boff[NSUB];
 #pragma unroll
   for (int j = 0; j < NSUB; ++j) {
@@ -512,6 +524,16 @@ __device__ __forceinline__ void tri_tile(int b, int nt, int& bi, int& bj) {
 // main loop (e.g. issues loads whose latency then hides under it), post(lds)
 // after it; a non-null return of post is a block-local Newton-Schulz iteration-0
 // coefficient set used in place of GemmOp::ns0 (a schedule the block computed).
+// A stream-K part of a tile (gemm_f64_sk_kernel): k stages [st0, st0 + nst); mode 0 the
+// whole tile (nst < 0: all stages), 1 a later part whose partial tile goes to part and
+// flag, 2 the first part, which waits for the flag, adds the partial and finishes.
+struct SkPart {
+  int mode = 0, st0 = 0, nst = -1;
+  double* part = nullptr;
+  int* flag = nullptr;
+  int epoch = 0;
+};
+
 struct NoHook {
   static constexpr bool kKScale = false;   // pre() leaves K scales of A in LDS (kscale())
   static constexpr int kLds = 1;           // doubles of LDS scratch the hook uses
@@ -524,7 +546,7 @@ struct NoHook {
 template <bool TA, bool TB, bool KS, bool DUAL, int EPI = kEpiAll, class Hook = NoHook>
 __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int slot,
                                           double (*sA)[BUF], double (*sB)[BUF], double* lds,
-                                          Hook&& hook = Hook{}) {
+                                          Hook&& hook = Hook{}, const SkPart& sk = SkPart{}) {
   // feature f is compiled in when its bit is set; an exact set also drops the
   // run-time null test of its fields
   constexpr bool kExact = EPI != kEpiAll;
@@ -562,7 +584,7 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
     if (g.glds) {   // aligned shapes: LDS-DMA main loop (same k order, same bits)
       mainloop_glds<TA, TB, H::kKScale>(g, i0, j0, lds, acc, hook.kscale(), [&]() {
         if constexpr (kHook) hook.pre();
-      });
+      }, sk.st0, sk.nst);
       done = true;
     }
   }
@@ -664,6 +686,16 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
   }
   __syncthreads();
   VB_GEMM_TS(11);
+  if (sk.mode == 2 && t == 0) {
+    // the tile's later stages: wait (bounded) for the partner block's partial tile
+    int it = 0;
+    while (__hip_atomic_load(sk.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sk.epoch &&
+           it < (1 << 22)) {
+      __builtin_amdgcn_s_sleep(1);
+      ++it;
+    }
+  }
+  if (sk.mode == 2) __syncthreads();
   if (h == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -672,6 +704,27 @@ __device__ __forceinline__ void gemm_tile(const GemmOp& g, int bx, int by, int s
       for (int hh = 2; hh < KS_; ++hh) p += red[((hh - 1) * 16 + q * 4 + r) * 64 + lane];
       r4[r] += p;
     }
+    if (sk.mode == 1) {
+      // a later part: the partial tile (device-coherent stores) for the first part's
+      // block; the flag follows once every thread's stores have completed (below)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        __hip_atomic_store(sk.part + (q * 4 + r) * 64 + lane, r4[r], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (sk.mode == 2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        r4[r] += __hip_atomic_load(sk.part + (q * 4 + r) * 64 + lane, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (sk.mode == 1) {
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(sk.flag, sk.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (h == 0) {
     const int col = j0 + wn * 16 + (lane & 15);
     double sq = 0.0, dt = 0.0, qf = 0.0, rp[4] = {0.0, 0.0, 0.0, 0.0};
     const bool mirror = has(kEpiSym, g.sym) && bx != by;   // also store the tile transposed
@@ -808,6 +861,70 @@ __global__ __launch_bounds__(NTH) void gemm_f64_kernel(GemmGroup gg) {
   VB_GEMM_TS(15);
 }
 
+// Stream-K form of a symmetric pair (gg.op[0], gg.op[1]; both sym, LDS-DMA loop): the
+// n_tiles = 2 T upper-triangle tiles x nst k stages of work are dealt over gridDim.x
+// blocks, blocks [0, extra) taking base + 1 stages and the rest base, in the order
+// (op, tile, stage), nst <= base <= nst (+ 1): a block's stages are the later part of
+// one tile (mode 1, or the whole tile) and then the first part of the next (mode 2:
+// it finishes that tile with the later part's partial, which the next block computed
+// first).  So every block does at most nst + 1 stages instead of 16 CUs running two
+// whole tiles (272 tiles on 256 CUs at D = 512).  The skip test and the copy of a
+// converged iterate run as in gemm_f64_kernel, the copy dealt by tile (tiles b and
+// b + gridDim.x of block b).
+template <int EPI>
+__global__ __launch_bounds__(NTH) void gemm_f64_sk_kernel(GemmGroup gg, int T, int nst, int base,
+                                                          int extra) {
+  kernarg_warm(gg);
+  __shared__ __attribute__((aligned(16))) double smem[SMEM];
+  double(*sA)[BUF] = reinterpret_cast<double(*)[BUF]>(smem);
+  double(*sB)[BUF] = reinterpret_cast<double(*)[BUF]>(smem + 2 * BUF);
+  const int b = blockIdx.x, nt = (gg.op[0].N + BT - 1) / BT;
+  if (const int sk = gemm_skip<EPI>(gg.op[0], sB[1])) {
+    for (int tl = b; tl < 2 * T; tl += gridDim.x) {
+      const GemmOp& g = gg.op[tl / T];
+      bool first = false;
+      if (g.copy_src) {
+        if (g.copy_if_iter < 0) first = true;
+        else if (sk == 2) first = g.conv_iter == g.copy_if_iter;
+        else if (g.conv_iter_out) first = *g.conv_iter_out == g.copy_if_iter;
+      }
+      if (!first) continue;
+      int by, bx;
+      tri_tile(tl % T, nt, by, bx);
+      for (int e = threadIdx.x; e < BT * BT; e += NTH) {
+        const int row = by * BT + e / BT, col = bx * BT + e % BT;
+        if (row < g.M && col < g.N) {
+          g.C[(long long)row * g.ldc + col] = g.copy_src[(long long)row * g.ldc + col];
+          if (bx != by) g.C[(long long)col * g.ldc + row] = g.copy_src[(long long)col * g.ldc + row];
+        }
+      }
+    }
+    return;
+  }
+  const int len = b < extra ? base + 1 : base;
+  const int u0 = b < extra ? b * (base + 1) : extra * (base + 1) + (b - extra) * base;
+  auto run = [&](int tl, int st0, int n, int mode) {
+    const GemmOp& g = gg.op[tl / T];
+    int by, bx;
+    tri_tile(tl % T, nt, by, bx);
+    SkPart p;
+    p.mode = mode;
+    p.st0 = st0;
+    p.nst = n;
+    p.part = g.sk_part + (long long)tl * (BT * BT);
+    p.flag = g.sk_flag + tl;
+    p.epoch = g.sk_epoch;
+    gemm_tile<false, false, false, false, EPI>(g, bx, by, tl % T, sA, sB, smem, NoHook{}, p);
+  };
+  // the later stages of tile tA (or all of it), then the first stages of tile tA + 1
+  const int tA = u0 / nst, sA0 = u0 % nst, nA = min(nst - sA0, len);
+  run(tA, sA0, nA, (sA0 == 0 && nA == nst) ? 0 : 1);
+  if (len > nA) {
+    const int nB = len - nA;
+    run(tA + 1, 0, nB, nB == nst ? 0 : 2);
+  }
+}
+
 // The same kernel with a hook (see NoHook) built in registers from its
 // arguments (Hook(args)); one GemmOp, no skip / copy control (the hook's
 // kernels are plain products).
@@ -867,6 +984,29 @@ inline bool gemm_epi_exact_enabled() {
     return !(e && e[0] == '0');
   }();
   return on;
+}
+
+// VIABEL_AMD_GEMM_SK=0: the Newton-Schulz Y|Z pair as one block per tile instead of
+// stream-K over one block per CU (A/B switch; the same products, rounded in another
+// order where a tile is split)
+inline bool gemm_sk_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("VIABEL_AMD_GEMM_SK");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// compute units of the current device (stream-K grid), cached per device
+inline int gemm_cu_count() {
+  static int cached[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cached[dev] = n;
+  }
+  return cached[dev];
 }
 
 namespace gemm_detail {
@@ -944,6 +1084,21 @@ inline hipError_t gemm_group(const GemmOp* ops, int n, hipStream_t s) {
   const bool ks = g.kscale != nullptr, dual = g.A2 != nullptr;
   if (ks && dual) return hipErrorInvalidValue;
   gemm_flop_tally() += (double)grid.x * grid.y * grid.z * BT * BT * g.K * 2.0 * (dual ? 2 : 1);
+  // stream-K for the Newton-Schulz Y|Z pair (GemmOp::sk_part): the tiles' k stages
+  // over one block per CU when the tiles outnumber the CUs by at most 1 / nst
+  constexpr int kSkEpi = kEpiSym | kEpiAlphaDev | kEpiSkip;
+  if (n == 2 && gg.op[0].sk_part && gg.op[1].sk_part && gg.op[0].sym && gg.op[0].glds &&
+      gg.op[1].glds && !g.ta && !g.tb && gemm_epi_exact_enabled() && epi_mask(gg.op[0]) == kSkEpi &&
+      epi_mask(gg.op[1]) == kSkEpi && gemm_sk_enabled()) {
+    const int T = (int)grid.x, nst = g.K / KTG, cus = gemm_cu_count();
+    const long long units = 2LL * T * nst;
+    if (cus > 0 && 2 * T > cus && units <= (long long)cus * (nst + 1)) {
+      const int base = (int)(units / cus), extra = (int)(units % cus);
+      hipLaunchKernelGGL((gemm_f64_sk_kernel<kSkEpi>), dim3((unsigned)cus), dim3(NTH), 0, s, gg, T,
+                         nst, base, extra);
+      return hipGetLastError();
+    }
+  }
   // exact epilogue kernels: plain NN products whose ops share one listed set, and
   // the NT Sigma = L L^T products (the step's first launch)
   int epi = kEpiAll;
