@@ -12,4 +12,7 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CY
   -d $OUT -o run --output-format csv -- python3 bench.py --legs none --no-cpu-baseline --steps ${STEPS:-20} --warmup 5 \
   > $OUT.log 2>&1 || exit $?
 f=$(find $OUT -name "*counter_collection.csv" | head -1)
-python3 scripts/valu_busy.py "$f" > gpurun_out/valu_busy.json && cat gpurun_out/valu_busy.json
+# the raw counters travel with the summary (RAW: the committed copy it cites)
+RAW=${RAW:-gpurun_out/valu_busy_counters.csv}
+cp "$f" "$RAW" || exit 1
+python3 scripts/valu_busy.py "$RAW" > gpurun_out/valu_busy.json && cat gpurun_out/valu_busy.json

@@ -4,6 +4,10 @@ bench.py and DESIGN.md cite:
   profiles/<round>/driver_cmd_dispatches.csv     every sep_kernel / sep_values dispatch
                                                  (start-ordered, duration in us)
   profiles/<round>/pmc_per_dispatch.json         summed counters per sep_kernel dispatch
+  profiles/<round>/raw_counters/n<N>_<pass>_counters.csv
+                                                 the raw rocprofv3 counter CSV of every PMC
+                                                 pass (renamed: *counter_collection.csv is
+                                                 git-ignored as scratch)
   profiles/traffic.json                          per-launch models a + b * steps, per N:
       traffic_bytes = FETCH_SIZE x 2 (gfx950: FETCH_SIZE reports half the bytes of
       a wide streaming read, MI355X_MICROARCH.md) + WRITE_SIZE, KiB -> bytes;
@@ -68,6 +72,13 @@ def main(rnd='r02', src=os.path.join(ROOT, 'gpurun_out', 'prof2')):
                 dur = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
                 fo.write('%s,%s,%.2f\n' % (r['Dispatch_Id'], r['Kernel_Name'].split('(')[0], dur))
         print(open(os.path.join(dst, 'driver_cmd_dispatches.csv')).read())
+    raw = os.path.join(dst, 'raw_counters')
+    os.makedirs(raw, exist_ok=True)
+    for ns in ('128', '256'):
+        for kind in ('fetch', 'write', 'sq'):
+            for f in glob.glob(os.path.join(src, 'n%s_%s' % (ns, kind), '**',
+                                            '*counter_collection.csv'), recursive=True):
+                shutil.copy(f, os.path.join(raw, 'n%s_%s_counters.csv' % (ns, kind)))
     models, pmc = {}, {}
     for ns in ('128', '256'):
         disp = {}
@@ -96,7 +107,8 @@ def main(rnd='r02', src=os.path.join(ROOT, 'gpurun_out', 'prof2')):
     json.dump(pmc, open(os.path.join(dst, 'pmc_per_dispatch.json'), 'w'), indent=1)
     if models:
         out = {'source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU passes '
-                         '(profiles/%s/pmc_per_dispatch.json, scripts/profile_r02.sh); per '
+                         '(profiles/%s/pmc_per_dispatch.json, raw counters in raw_counters/ beside '
+                         'it, scripts/profile_r02.sh); per '
                          'sep_kernel launch of k steps writing h history rows: bytes = a + b k + c h, '
                          'VALU instructions = a + b k, over k in %s; '
                          'FETCH_SIZE doubled per the MI355X_MICROARCH.md gfx950 correction '

@@ -1062,6 +1062,19 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
     const bool rows = RO == 1 || (RO == 0 && row_wave);
     const long long i = a.step0 + s;
     const long long ri = a.rng_step0 + s;
+    // CHIVI: the update's step size and (qnext) the window's pre-sum of this step, formed
+    // / read at the step's start by the update threads: the schedule's division and an
+    // LDS round trip had sat on the update's serial chain after the reduction barrier
+    // (round-6 ISA of the config-2 instance; config 2 2.33 -> 2.25 us/step with the
+    // column reads below).  KLVI keeps them after the barrier: its rows are short, and
+    // the extra work at the step's start made wave 0 late (config 1 1.00 -> 1.11,
+    // profiles/r06/block_update_chain_ab.log).  s_qpre[s & 1] was written during step
+    // s - 1, before its end barrier.
+    double lr_i = 0.0, qo_pre = 0.0;
+    if (k_chivi && RO != 2 && tid < P && !k_emit && k_opt == 0) {
+      lr_i = a.lr.at(i);
+      if (qnext && s > 0) qo_pre = s_qpre[s & 1][tid];
+    }
     // sum_d log sigma_d of the pre-update lam: only the value needs it (log q
     // enters the rows without it: a per-step constant that cancels in the CHIVI
     // weights, added back to the value).  The copy wave computes it off the rows'
@@ -1386,9 +1399,11 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
       double t[kBlockMaxRowWaves];
 #pragma unroll
       for (int q = 0; q < kBlockMaxRowWaves; ++q) t[q] = s_red[q][k];
+      // (the absent waves' rows select 0 before the adds: the add chain carries no
+      // select; u + 0 = u)
       double u = t[0];
 #pragma unroll
-      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = q < RW ? u + t[q] : u;
+      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = u + (q < RW ? t[q] : 0.0);
       return u;
     };
     VB_PH(4);
@@ -1399,14 +1414,32 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
       // one column read and one division for both parameter kinds (the two
       // sides of a select, not of a branch: wave 0 holds both kinds)
       const bool mean = p < D;
-      const double c = colsum(mean ? p : DMAX + (p - D));
+      const int kc = mean ? p : DMAX + (p - D);
       const double sgp = s_sg[mean ? 0 : p - D];
       double gp;
       if (!k_chivi) {
-        const double cd = c * inv_dN;
+        const double cd = colsum(kc) * inv_dN;
         gp = mean ? -cd : -(1.0 + sgp * cd);
       } else {
-        const double Ssum = colsum(2 * DMAX);
+        // both columns' reads in flight together (the empty asm holds them until all
+        // eight are loaded): the compiler had moved the weight sum's reads into a branch
+        // of the log-sigma lanes after the first column's adds, then into the same
+        // registers -- two LDS round trips on the update's chain instead of one
+        double tc[kBlockMaxRowWaves], ts[kBlockMaxRowWaves];
+#pragma unroll
+        for (int q = 0; q < kBlockMaxRowWaves; ++q) {
+          tc[q] = s_red[q][kc];
+          ts[q] = s_red[q][2 * DMAX];
+        }
+        static_assert(kBlockMaxRowWaves == 4, "the asm operand list below");
+        asm volatile("" : "+v"(tc[0]), "+v"(tc[1]), "+v"(tc[2]), "+v"(tc[3]), "+v"(ts[0]),
+                          "+v"(ts[1]), "+v"(ts[2]), "+v"(ts[3]));
+        double c = tc[0], Ssum = ts[0];
+#pragma unroll
+        for (int q = 1; q < kBlockMaxRowWaves; ++q) {
+          c = c + (q < RW ? tc[q] : 0.0);
+          Ssum = Ssum + (q < RW ? ts[q] : 0.0);
+        }
         gp = (mean ? a.alpha * c : a.alpha * (sgp * c + Ssum)) * inv_dN;
       }
       if (k_emit) {
@@ -1440,7 +1473,8 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
           double q = 0.0;
           if (qpre) {
             if (qnext && s > 0)
-              q = __dadd_rn(__dadd_rn(s_qpre[s & 1][p], __dmul_rn(gprev, gprev)), __dmul_rn(gp, gp));
+              q = __dadd_rn(__dadd_rn(k_chivi ? qo_pre : s_qpre[s & 1][p], __dmul_rn(gprev, gprev)),
+                            __dmul_rn(gp, gp));
             else
               q = __dadd_rn(s_qold[p], __dmul_rn(gp, gp));
             gprev = gp;
@@ -1457,7 +1491,8 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
           // lam - lr g / sqrt(eps + q) with the refined rsqrt of the column-pair
           // kernel's update (~1 ulp) instead of an IEEE sqrt and division: ~30
           // instructions off the step's serial update chain
-          nl = __dsub_rn(s_lam[p], __dmul_rn(a.lr.at(i), gp) * rsqrt_pos(__dadd_rn(a.eps, q)));
+          nl = __dsub_rn(s_lam[p], __dmul_rn(k_chivi ? lr_i : a.lr.at(i), gp) *
+                                       rsqrt_pos(__dadd_rn(a.eps, q)));
           if (i >= a.hist_start) a.hist[((long long)prob * a.n_hist + (i - a.hist_start)) * P + p] = nl;
         }
         s_lam[p] = nl;  // only thread p reads/writes s_lam[p] / s_sg[p - D] until the barrier
@@ -1746,6 +1781,8 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
     }
   };
   for (int s = 0; s < n_steps; ++s) {
+    // (as block_kernel: the window pre-sum read at the step's start)
+    const double qo_pre = (qpre && tid < P) ? s_qpre[s & 1][tid] : 0.0;
     double sl = 0.0;
     if (!has_copy || copy) {
 #pragma unroll
@@ -1789,7 +1826,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
       for (int q = 0; q < kBlockMaxRowWaves; ++q) tq[q] = s_red[q][k];
       double u = tq[0];
 #pragma unroll
-      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = q < RW ? u + tq[q] : u;
+      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = u + (q < RW ? tq[q] : 0.0);
       return u;
     };
     if (tid < P) {
@@ -1800,7 +1837,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
       s_ring[slot * P + p] = gp;
       double q = 0.0;
       if (qpre) {
-        const double qo = s_qpre[s & 1][p];
+        const double qo = qo_pre;
         q = s > 0 ? __dadd_rn(__dadd_rn(qo, __dmul_rn(gprev, gprev)), __dmul_rn(gp, gp))
                   : __dadd_rn(qo, __dmul_rn(gp, gp));
         gprev = gp;
