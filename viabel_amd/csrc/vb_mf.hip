@@ -965,6 +965,9 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
   if (!k_emit)
     for (int q = tid; q < W * P; q += NT) s_ring[q] = ring_g[q];
   for (int d = tid; d < D; d += NT) s_sg[d] = exp_fast(lam_g[D + d]);
+  // the reduction rows of absent row waves hold zeros (never written after this), so
+  // every column sum adds all kBlockMaxRowWaves rows: no select on the update's chain
+  for (int q = RW * K + tid; q < kBlockMaxRowWaves * K; q += NT) (&s_red[0][0])[q] = 0.0;
 
   const Rng rng{a.k0, a.k1, (uint32_t)(a.stream + (uint32_t)prob * a.stream_stride)};
   const double c0 = TFAM ? 0.0 : 0.5 * D * (1.0 + kLog2Pi);
@@ -1399,11 +1402,10 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
       double t[kBlockMaxRowWaves];
 #pragma unroll
       for (int q = 0; q < kBlockMaxRowWaves; ++q) t[q] = s_red[q][k];
-      // (the absent waves' rows select 0 before the adds: the add chain carries no
-      // select; u + 0 = u)
+      // (the absent waves' rows hold zeros, set before the step loop: u + 0 = u)
       double u = t[0];
 #pragma unroll
-      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = u + (q < RW ? t[q] : 0.0);
+      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = u + t[q];
       return u;
     };
     VB_PH(4);
@@ -1437,8 +1439,8 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
         double c = tc[0], Ssum = ts[0];
 #pragma unroll
         for (int q = 1; q < kBlockMaxRowWaves; ++q) {
-          c = c + (q < RW ? tc[q] : 0.0);
-          Ssum = Ssum + (q < RW ? ts[q] : 0.0);
+          c = c + tc[q];
+          Ssum = Ssum + ts[q];
         }
         gp = (mean ? a.alpha * c : a.alpha * (sgp * c + Ssum)) * inv_dN;
       }
@@ -1762,6 +1764,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
   for (int q = tid; q < W * P; q += NT) s_ring[q] = 0.0;
   for (int d = tid; d < D; d += NT) s_sg[d] = 1.0;
   for (int p = tid; p < 2 * 2 * DMAX; p += NT) (&s_qpre[0][0])[p] = 0.0;
+  for (int q = RW * K + tid; q < kBlockMaxRowWaves * K; q += NT) (&s_red[0][0])[q] = 0.0;
   __syncthreads();
   int slot = 0;
   double val = 0.0, gprev = 0.0;
@@ -1826,7 +1829,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
       for (int q = 0; q < kBlockMaxRowWaves; ++q) tq[q] = s_red[q][k];
       double u = tq[0];
 #pragma unroll
-      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = u + (q < RW ? tq[q] : 0.0);
+      for (int q = 1; q < kBlockMaxRowWaves; ++q) u = u + tq[q];   // (absent rows: zeros)
       return u;
     };
     if (tid < P) {
