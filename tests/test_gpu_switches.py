@@ -15,6 +15,8 @@ each side runs in a child process; the child writes its run's result
   Newton-Schulz Y|Z pair without stream-K) likewise, at D = 512.
 * VIABEL_AMD_HOST_TRACE=1 (host timestamps of the column-pair launch path on
   stderr): the same bits, and the trace lines are there.
+* VIABEL_AMD_PSIS_WORKER=1 (restart table: the PSIS k-hats on a worker thread):
+  the same bits.
 * VIABEL_AMD_DIV_TWO_PASS=0 (divergence statistics in numpy's three passes at every
   size): equal to the two-pass Welford / Chan form to rounding.
 (VIABEL_AMD_PREDRAW, _BLOCK_SPLIT, _PREDRAW_OVERLAP, _GEMM_EPI_EXACT,
@@ -132,6 +134,34 @@ def test_host_trace_is_bitwise_default_and_prints(tmp_path):
     for k in ('lam', 'hist', 'vals'):
         np.testing.assert_array_equal(out[k], ref[k])
     assert 'sep advance' in err, err[-2000:]
+
+
+_RESTARTS_CHILD = '''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from viabel_amd import vb, targets, restarts
+fac = lambda: vb.mean_field_t_variational_family(10, 40.0, rng='philox')
+tab = restarts.run_restarts(fac, targets.eight_schools_ncp(), 6, 200, n_samples=100,
+                            n_bounds=200_000, learning_rate=.01, learning_rate_end=.001)
+np.save(sys.argv[2], tab)
+'''
+
+
+def test_psis_worker_switch_is_bitwise(tmp_path):
+    """VIABEL_AMD_PSIS_WORKER=1 (the restart table's PSIS k-hats on a worker thread
+    beside the host bound algebra) against the default serial order: the same calls
+    on the same device buffers, so the same table bit for bit."""
+    out = {}
+    for tag, env in (('serial', {}), ('worker', {'VIABEL_AMD_PSIS_WORKER': '1'})):
+        path = str(tmp_path / ('%s.npy' % tag))
+        e = dict(os.environ)
+        e.pop('VIABEL_AMD_PSIS_WORKER', None)
+        e.update(env)
+        subprocess.check_call([sys.executable, '-c', _RESTARTS_CHILD, ROOT, path], env=e,
+                              timeout=300)
+        out[tag] = np.load(path)
+    assert np.all(np.isfinite(out['serial'][:, 8]))
+    np.testing.assert_array_equal(out['worker'], out['serial'])
 
 
 _DIV_CHILD = '''

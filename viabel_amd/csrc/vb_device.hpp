@@ -452,6 +452,18 @@ __device__ __forceinline__ double bailey_t(uint32_t lo, uint32_t hi, double df, 
   return cs * sqrt_pos(df * em1);
 }
 
+// T of words (lo, hi) and y = T^2 / df (the log-q argument: log1p(y)), for callers that
+// multiply the (1 + y) of a row's variates and take one log of the product
+__device__ __forceinline__ double bailey_t_y(uint32_t lo, uint32_t hi, double df, double c2,
+                                             const double2* sct, const double2* ltab, double& y) {
+  const double a = hfma((double)(hi & 0xffu), 0x1p32, (double)lo);  // exact, 40 bits
+  const double u1 = hfma(a, 0x1p-40, 0x1p-41);                        // (a + 1/2) 2^-40
+  const double em1 = expm1_pos(c2 * log_u01_tab(u1, ltab));           // U1^(-2/df) - 1
+  const double cs = cospi_tab_u24(hi >> 8, sct);                      // cos(2 pi U2)
+  y = cs * cs * em1;
+  return cs * sqrt_pos(df * em1);
+}
+
 // ---- wave-level helpers (wave64) -------------------------------------------
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const uint64_t b = __double_as_longlong(v);

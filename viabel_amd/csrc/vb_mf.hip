@@ -2310,8 +2310,10 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
   __shared__ double2 s_sct[HOST ? 1 : kSinCosN];
   __shared__ double2 s_lt[HOST ? 1 : kLogN + kLogU01N];
   __shared__ double s_mu[DMAX], s_ls[DMAX], s_sg[DMAX];
-  // t family, Philox: the row's samples x, [DMAX][256] (see below)
+  // t family, Philox: the row's samples x, [DMAX][256] (see below), and the row's
+  // log-q constant sum_d (t_const - log sigma_d) (the same for every row of the block)
   __shared__ double s_x[(TFAM && !HOST) ? DMAX * 256 : 1];
+  __shared__ double s_lqc;
   // row q of a batched launch (vb_log_weights_rows): its own lambda, output
   // row, noise rows and Philox stream (stream + q * stride)
   const int q = blockIdx.y;
@@ -2330,6 +2332,14 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
   }
   if constexpr (!HOST) load_bm_tables(s_sct, s_lt);
   __syncthreads();
+  if constexpr (TFAM && !HOST) {
+    if (threadIdx.x == 0) {   // (d ascending: the order the rows once summed it in)
+      double c = 0.0;
+      for (int d = 0; d < D; ++d) c += t_const - s_ls[d];
+      s_lqc = c;
+    }
+    __syncthreads();
+  }
   const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
   if (r >= m) return;
   double x[DMAX], g[DMAX];
@@ -2341,26 +2351,40 @@ __global__ __launch_bounds__(256) void logw_row_kernel(int D, long long m, const
     // column pair per iteration of a rolled loop (the polynomial constants stay in
     // registers; unrolled, they were re-made for every variate), x written to LDS,
     // then read back as a register array for the target.
+    // The row's log1p(T_d^2 / df) terms as ONE log of the product of the (1 + T_d^2 /
+    // df), its binary exponent split off after every pair (a factor reaches 2^(82 / df)
+    // for U1 = 2^-41: small df would overflow a plain product).  The product's ~D
+    // roundings move the log by ~D ulp of its magnitude -- ~1e-15 absolute against the
+    // oracle's sum of log1p (vbrng.c family 2; tests/test_gpu_bailey.py at 1e-12).  Nine
+    // of ten table log1p per row at D = 10 become multiplies (round 6, config 5's bounds
+    // stage).
     const double c2 = -2.0 / df, hdf1 = 0.5 * (df + 1.0);
     const int t = threadIdx.x;
+    double pr = 1.0;
+    int pe = 0;
 #pragma unroll 1
     for (int j = 0; 2 * j < D; ++j) {
       const u4 w = rng.draw((uint32_t)j, (uint32_t)r, step, kBaileyPurpose);
-      double la, lb;
-      const double ta = bailey_t(w.x, w.z, df, c2, s_sct, s_lt, la);
-      const double tb = bailey_t(w.y, w.w, df, c2, s_sct, s_lt, lb);
+      double ya, yb;
+      const double ta = bailey_t_y(w.x, w.z, df, c2, s_sct, s_lt, ya);
+      const double tb = bailey_t_y(w.y, w.w, df, c2, s_sct, s_lt, yb);
       const int d = 2 * j;
       const double xa = ta * s_sg[d] + s_mu[d];
-      lq += t_const - la * hdf1 - s_ls[d];
+      pr = fma(pr, ya, pr);
       s_x[d * 256 + t] = xa;
       if (d + 1 < D) {
         const double xb = tb * s_sg[d + 1] + s_mu[d + 1];
-        lq += t_const - lb * hdf1 - s_ls[d + 1];
+        pr = fma(pr, yb, pr);
         s_x[(d + 1) * 256 + t] = xb;
         if (xs) xs[r * D + d + 1] = xb;
       }
       if (xs) xs[r * D + d] = xa;
+      int e;
+      pr = frexp(pr, &e);
+      pe += e;
     }
+    const double dpe = (double)pe;
+    lq = s_lqc - hdf1 * fma(dpe, 0.6931471805598903, fma(dpe, 5.497923018708371e-14, log_unit_tab(pr, s_lt)));
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
       x[d] = d < D ? s_x[d * 256 + t] : 0.0;

@@ -127,16 +127,19 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
             experiments.log_weights(target, fj, smooth[j], n_bounds, return_samples=False,
                                     lw_out=lw[j])
     # the divergence statistics of all restarts in one batched reduction chain,
-    # then the PSIS k-hats (psis.py:112-208's kss; the smoothed weights are not
-    # needed here) on a worker thread -- its C calls release the GIL and mostly
-    # wait for the device -- while this thread runs the O(D) bound algebra and the
-    # Monte Carlo warnings of all restarts on the host
+    # then the O(D) bound algebra and the Monte Carlo warnings of all restarts on the
+    # host, then the PSIS k-hats (psis.py:112-208's kss; the smoothed weights are not
+    # needed here).  VIABEL_AMD_PSIS_WORKER=1 runs the k-hats on a worker thread beside
+    # the bound algebra instead: the thread hand-off cost more than the ~0.15 ms of
+    # algebra it hides (config 5's stage 4.05-4.18 vs 3.81-3.90 ms,
+    # profiles/r06/cfg5/stage_logq_product_worker_ab.log)
     div = bounds.divergence_rows(lw)
     khat_fn = lambda: psis.psis_khat(lw.t()) if len(ids) > 1 else np.array([psis.psis_khat(lw[0])])
     # (a full-rank family's moments below call the library: no concurrent calls
     # on the context, so the k-hats run first there)
-    khat_job = _psis_worker().submit(khat_fn) if bfam.kind != nat.FAMILY_FR_T else None
-    khat = khat_fn() if khat_job is None else None
+    use_worker = bfam.kind != nat.FAMILY_FR_T and os.environ.get('VIABEL_AMD_PSIS_WORKER', '0') == '1'
+    khat_job = _psis_worker().submit(khat_fn) if use_worker else None
+    khat = khat_fn() if (khat_job is None and bfam.kind == nat.FAMILY_FR_T) else None
     if bfam.kind == nat.FAMILY_FR_T:
         # full-rank q: the family's own moments and covariance (eigenvalues of
         # Sigma on the device), restart by restart, as all_bounds does
@@ -151,6 +154,8 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
         recs = bounds_records(ids, div, smooth, bfam)
     if khat_job is not None:
         khat = khat_job.result()
+    elif khat is None:
+        khat = khat_fn()
     if timings is not None:
         _sync()
         t2 = time.perf_counter()
