@@ -1784,8 +1784,9 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
     }
   };
   for (int s = 0; s < n_steps; ++s) {
-    // (as block_kernel: the window pre-sum read at the step's start)
-    const double qo_pre = (qpre && tid < P) ? s_qpre[s & 1][tid] : 0.0;
+    // (as block_kernel: CHIVI reads the window pre-sum at the step's start, KLVI after
+    // the reduction barrier)
+    const double qo_pre = (chivi && qpre && tid < P) ? s_qpre[s & 1][tid] : 0.0;
     double sl = 0.0;
     if (!has_copy || copy) {
 #pragma unroll
@@ -1840,7 +1841,7 @@ __global__ __launch_bounds__(kBlockMaxThreads) void block_floor_kernel(int D, in
       s_ring[slot * P + p] = gp;
       double q = 0.0;
       if (qpre) {
-        const double qo = qo_pre;
+        const double qo = chivi ? qo_pre : s_qpre[s & 1][p];
         q = s > 0 ? __dadd_rn(__dadd_rn(qo, __dmul_rn(gprev, gprev)), __dmul_rn(gp, gp))
                   : __dadd_rn(qo, __dmul_rn(gp, gp));
         gprev = gp;
