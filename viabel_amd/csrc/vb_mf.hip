@@ -1236,8 +1236,12 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
         s01[0] = s_sg[0];
         s01[1] = s_sg[1];
         // pairs are active together (n is the same for both lanes): the DPP swaps
-        // inside row_half_of see their partner
-        for (int n = tid >> 1; n < N; n += RT >> 1) {
+        // inside row_half_of see their partner.  One sample per lane pair at most
+        // (block_layout's split rows have RT >= 2 N): for DMAX >= 4 without the loop --
+        // config 2 2.14 -> 2.05 us/step, config 5's fit 8.55 -> 8.0 ms; the DMAX = 2
+        // instance (config 1) measured 1.00 -> 1.02 without it and keeps the loop
+        // (profiles/r06/split_rows_no_loop_ab.log)
+        auto split_row = [&](int n) __attribute__((always_inline)) {
           double e[DMAX];
           double tl = 0.0;
           LdsRowWait<DMAX>::run(base + 8u * (unsigned)(n * D), base + 8u * (unsigned)(L.pf_lq + n),
@@ -1259,6 +1263,12 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
           if (need_lq && !pre_lq) lqs += dpp_f64<0xB1>(lqs);
           if (need_lq && pre_lq) lqs = tl;
           row_half_of(eh, e, lqs, h);
+        };
+        if constexpr (DMAX >= 4) {
+          const int n = tid >> 1;
+          if (n < N) split_row(n);
+        } else {
+          for (int n = tid >> 1; n < N; n += RT >> 1) split_row(n);
         }
       }
     } else if constexpr (kPF) {
