@@ -914,7 +914,9 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
   const bool copy_wave = kPF && wid == RW;   // the last wave (block_layout)
   const int NTw = kPF ? NT - 64 : NT;        // threads of the row / draw waves
   const int val_tid = NTw > 64 ? NTw - 64 : 0;  // value on another wave than the update
-  const bool pre_lq = HOST && a.noise_lq != nullptr;
+  // (the CHIVI HOT instance is launched only with the pre-drawn log q partials:
+  // block_dispatch_dm)
+  const bool pre_lq = HOST && (HOT == 2 ? true : a.noise_lq != nullptr);
   // copy wave: noise rows (and log q partials) of step s -> ring slot s % 3, as
   // wave-wide 16-byte LDS-DMA loads (4-byte ones when a source is not 16-byte
   // aligned); lanes past the end re-read the first element into the slot's slack
@@ -950,7 +952,11 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
   // adagrad window sums: the copy wave adds up the older W - 1 slots of every
   // parameter while the rows run (same order, oldest first), so the update adds
   // only the newest square (the same bits as the whole loop)
-  const bool qpre = kPF && k_opt == 0 && !k_emit && W >= 1 && W <= kBlockQpreMaxW;
+  // (the CHIVI HOT instance is launched only for windows the copy wave pre-sums:
+  // block_dispatch_dm; the general window loop then drops out of its code -- config 2
+  // 2.06 -> 1.81 us/step with the pre-drawn log q below; the same for the KLVI instance
+  // cost config 5's fit 7.8 -> 8.05 ms, profiles/r06/hot_compile_time_facts_ab.log)
+  const bool qpre = HOT == 2 ? true : (kPF && k_opt == 0 && !k_emit && W >= 1 && W <= kBlockQpreMaxW);
   // The copy wave sums step s + 1's window (but its newest slot) after step s's
   // reduction barrier, beside the update, instead of before that barrier, which it held
   // (KLVI, profiles/r05/copy_wave_ts.log; CHIVI from round 6: its sums after the block-
@@ -1503,8 +1509,8 @@ __global__ __launch_bounds__(HOST ? (SPLIT ? 320 : 256) : kBlockMaxThreads) void
           // lam - lr g / sqrt(eps + q) with the refined rsqrt of the column-pair
           // kernel's update (~1 ulp) instead of an IEEE sqrt and division: ~30
           // instructions off the step's serial update chain
-          nl = __dsub_rn(s_lam[p], __dmul_rn(k_chivi ? lr_i : a.lr.at(i), gp) *
-                                       rsqrt_pos(__dadd_rn(a.eps, q)));
+          const double lr_u = k_chivi ? lr_i : a.lr.at(i);
+          nl = __dsub_rn(s_lam[p], __dmul_rn(lr_u, gp) * rsqrt_pos(__dadd_rn(a.eps, q)));
           if (i >= a.hist_start) a.hist[((long long)prob * a.n_hist + (i - a.hist_start)) * P + p] = nl;
         }
         s_lam[p] = nl;  // only thread p reads/writes s_lam[p] / s_sg[p - D] until the barrier
@@ -2524,7 +2530,8 @@ static hipError_t block_dispatch_dm(int fam, bool host, const BlockArgs& a, int 
   if constexpr (DM <= kBlockSplitMaxD) {
     if (host && L.split) {
       // the benchmark modes with their flags compiled in (block_kernel's HOT)
-      const int hot = (!a.emit_grad && a.opt == 0 && !a.pd) ? (a.chivi ? 2 : 1) : 0;
+      const bool chivi_hot = a.noise_lq && a.W >= 1 && a.W <= kBlockQpreMaxW;
+      const int hot = (!a.emit_grad && a.opt == 0 && !a.pd) ? (a.chivi ? (chivi_hot ? 2 : 0) : 1) : 0;
 #define VB_SPLIT_LAUNCH(F, H) \
   hipLaunchKernelGGL((block_kernel<TGT, F, true, DM, true, true, H>), grid, block, 0, s, a)
       if (fam == 1) {
