@@ -15,6 +15,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <new>
 #include <set>
@@ -79,25 +80,122 @@ int foreign_ptr_error(const void* p) {
               at.device, cur);
 }
 
+// Device blocks of runs and contexts are cached by (device, size class) instead of
+// going back to hipFree: a run made and dropped per call (adagrad_optimize, the
+// restart table) paid one hipFree per buffer -- each one synchronises the device and
+// unmaps the block, ~0.8 ms for config 5's run -- and a hipMalloc per buffer on the
+// next call.  A block is returned only when no work can still use it (vb_run_destroy
+// and vb_ctx_destroy synchronise their streams first; a buffer that grows
+// synchronises the device before handing its old block back, as hipFree did).  The
+// cache is trimmed (hipFree of every cached block) when a hipMalloc fails, and at
+// exit by release_live_contexts, before the HIP runtime's own teardown; blocks
+// returned after that are freed directly.
+namespace devpool {
+std::mutex mu;
+std::multimap<std::pair<int, size_t>, void*>* cached = nullptr;   // never freed
+bool closed = false;
+
+// size class: powers of two up to 4 MB (at least 4 KB), then multiples of 2 MB
+size_t size_class(size_t b) {
+  if (b <= 4096) return 4096;
+  if (b <= (size_t(4) << 20)) {
+    size_t c = 8192;
+    while (c < b) c <<= 1;
+    return c;
+  }
+  const size_t g = size_t(2) << 20;
+  return (b + g - 1) / g * g;
+}
+
+void trim_locked() {
+  if (!cached) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (auto& kv : *cached) {
+    (void)hipSetDevice(kv.first.first);
+    (void)hipFree(kv.second);
+  }
+  cached->clear();
+  (void)hipSetDevice(cur);
+}
+
+void trim() {
+  std::lock_guard<std::mutex> lk(mu);
+  trim_locked();
+}
+
+// exit: free every cached block; later returns go straight to hipFree
+void close() {
+  std::lock_guard<std::mutex> lk(mu);
+  trim_locked();
+  closed = true;
+}
+
+hipError_t alloc(void** p, size_t bytes, size_t* cap, int* dev) {
+  (void)hipGetDevice(dev);
+  const size_t cls = size_class(bytes);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (cached) {
+      auto it = cached->find({*dev, cls});
+      if (it != cached->end()) {
+        *p = it->second;
+        cached->erase(it);
+        *cap = cls;
+        return hipSuccess;
+      }
+    }
+  }
+  hipError_t e = hipMalloc(p, cls);
+  if (e != hipSuccess) {   // blocks of other sizes may be what is missing
+    (void)hipGetLastError();
+    trim();
+    e = hipMalloc(p, cls);
+  }
+  if (e == hipSuccess) *cap = cls;
+  return e;
+}
+
+void give_back(void* p, size_t cap, int dev) {
+  std::lock_guard<std::mutex> lk(mu);
+  if (closed) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(dev);
+    (void)hipFree(p);
+    (void)hipSetDevice(cur);
+    return;
+  }
+  if (!cached) cached = new std::multimap<std::pair<int, size_t>, void*>();
+  cached->insert({{dev, cap}, p});
+}
+}  // namespace devpool
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  int dev = 0;
   int reserve(size_t bytes) {
     if (bytes <= cap) return VB_OK;
-    if (p) (void)hipFree(p);  // synchronises the device first (HIP)
+    if (p) {
+      (void)hipDeviceSynchronize();   // work queued on the old block finishes first
+      devpool::give_back(p, cap, dev);
+    }
     p = nullptr;
     cap = 0;
     if (bytes == 0) return VB_OK;
-    hipError_t e = hipMalloc(&p, bytes);
+    hipError_t e = devpool::alloc(&p, bytes, &cap, &dev);
     if (e != hipSuccess) {
       (void)hipGetLastError();
+      p = nullptr;
+      cap = 0;
       return fail(VB_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
     }
-    cap = bytes;
     return VB_OK;
   }
+  // (owners synchronise their streams before they drop their buffers)
   ~DevBuf() {
-    if (p) (void)hipFree(p);
+    if (p) devpool::give_back(p, cap, dev);
   }
   double* d() const { return static_cast<double*>(p); }
 };
@@ -193,6 +291,8 @@ void release_live_contexts() {
     (void)hipStreamSynchronize(c->stream);
     c->release_side();
   }
+  // every cached device block (runs and contexts still alive free theirs directly)
+  devpool::close();
 }
 
 void register_ctx(vb_ctx* c) {
@@ -1483,8 +1583,11 @@ int vb_run_result(vb_run* r, double* lam_out, double* hist_out, double* values_o
 int vb_run_destroy(vb_run* r) {
   if (!r) return VB_OK;
   if (r->ctx) {
+    // the run's buffers go back to the device cache: nothing may still use them
     (void)hipSetDevice(r->ctx->device);
     (void)hipStreamSynchronize(r->ctx->stream);
+    if (r->ctx->pd_stream) (void)hipStreamSynchronize(r->ctx->pd_stream);
+    if (r->ctx->blk_stream) (void)hipStreamSynchronize(r->ctx->blk_stream);
   }
   delete r;
   return VB_OK;

@@ -90,6 +90,7 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
     restart r draws from Philox stream 1 + r whatever the sharding) and
     summarise each with device log weights, bounds and PSIS.  `timings`, if a
     dict, receives the seconds of the fitting and of the bounds/PSIS stage."""
+    t_entry = time.perf_counter()
     from . import vb, bounds, psis, experiments
     fam = family_factory()
     if fam.rng != 'philox':
@@ -161,8 +162,14 @@ def _native_compute(ids, inits, family_factory, target, n_iters, n_samples, n_bo
         t2 = time.perf_counter()
         timings['fit_s'] = t1 - t0
         timings['bounds_psis_s'] = t2 - t1
-    return np.array([np.concatenate([rec, [khat[j], vals[j, -1]], smooth[j]])
-                     for j, rec in enumerate(recs)])
+        timings['pre_s'] = t0 - t_entry
+    # [records | k-hat | final value | lambda*] of every restart, one array op
+    # (a per-restart concatenate took ~0.3 ms at 64 restarts)
+    out = np.column_stack([np.asarray(recs, dtype=float), np.asarray(khat, dtype=float),
+                           np.asarray(vals, dtype=float)[:, -1], np.asarray(smooth, dtype=float)])
+    if timings is not None:
+        timings['post_s'] = time.perf_counter() - t2
+    return out
 
 
 _WORKER = []
@@ -254,6 +261,7 @@ def run_restarts(family_factory, target, n_restarts, n_iters, n_samples=100, n_b
         dist_on = dist.is_available() and dist.is_initialized()
     except ImportError:
         dist_on = False
+    t_in = time.perf_counter()
     rank, world = (dist.get_rank(group), dist.get_world_size(group)) if dist_on else (0, 1)
     fam0 = family_factory()
     P = fam0.var_param_dim
@@ -270,6 +278,10 @@ def run_restarts(family_factory, target, n_restarts, n_iters, n_samples=100, n_b
                  if ids else np.zeros((0, len(RECORD_HEAD) + P)))
     else:
         local = compute(ids, local_inits)
+    if timings is not None:
+        # this rank's whole call before the gather (the fit and bounds stages plus
+        # the host setup and the record table around them)
+        timings['local_s'] = time.perf_counter() - t_in
     width = len(RECORD_HEAD) + P
     if not dist_on:
         return np.asarray(local)[np.argsort(np.asarray(local)[:, 0])]
