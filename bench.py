@@ -406,7 +406,9 @@ def leg_cfg1(cpu):
     lam0 = np.array([0., 0., 1., 1.])
     fam = vb.mean_field_gaussian_variational_family(Dm, rng='philox')
     obj = vb.black_box_klvi(fam, targets.mixture(Dm), n)
-    vb.adagrad_optimize(200, obj, lam0)
+    # warm-up at the timed call's shapes (its buffers then come from the library's
+    # device block cache, as in any later call of a long-running program)
+    vb.adagrad_optimize(iters, obj, lam0)
     _sync()
     t0 = time.perf_counter()
     vb.adagrad_optimize(iters, obj, lam0)
@@ -446,7 +448,8 @@ def leg_cfg2(cpu):
     lam0[1] = -1.0
     fam = vb.mean_field_t_variational_family(Dm, 40.0, rng='philox')
     obj = vb.black_box_chivi(2.0, fam, targets.funnel(Dm), n)
-    vb.adagrad_optimize(200, obj, lam0, learning_rate_end=.001)
+    # (warm-up at the timed call's shapes, as config 1's)
+    vb.adagrad_optimize(iters, obj, lam0, learning_rate=.01, learning_rate_end=.001)
     _sync()
     t0 = time.perf_counter()
     vb.adagrad_optimize(iters, obj, lam0, learning_rate=.01, learning_rate_end=.001)
@@ -640,9 +643,11 @@ def leg_cfg5(cpu, host, rank, world, n_restarts=64, iters=5000, M=1_000_000):
     from viabel_amd import vb, targets, restarts
     fac = lambda: vb.mean_field_t_variational_family(10, 40.0, rng='philox')
     tgt = targets.eight_schools_ncp()
-    # warm-up: code objects, and the same [restarts][M] buffer shapes for the
-    # device allocator (a 20-iteration fit)
-    restarts.run_restarts(fac, tgt, n_restarts, 20, n_bounds=M)
+    # warm-up: code objects, and the timed call's buffer shapes for the device
+    # allocators (torch's for the [restarts][M] log weights, the library's block
+    # cache for the runs), i.e. the same call once untimed
+    restarts.run_restarts(fac, tgt, n_restarts, iters, n_samples=100, n_bounds=M,
+                          learning_rate=.01, learning_rate_end=.001)
     _sync()
     dist = torch.distributed if world > 1 else None
     # the restarts' initial parameters are the job's input, made before the timed
