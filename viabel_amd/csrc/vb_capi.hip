@@ -93,7 +93,11 @@ int foreign_ptr_error(const void* p) {
 namespace devpool {
 std::mutex mu;
 std::multimap<std::pair<int, size_t>, void*>* cached = nullptr;   // never freed
+size_t cached_bytes = 0;
 bool closed = false;
+// blocks beyond this much cached memory are freed when returned (other allocators,
+// torch's among them, share the device's HBM and cannot empty this cache)
+constexpr size_t kCacheMax = size_t(8) << 30;
 
 // size class: powers of two up to 4 MB (at least 4 KB), then multiples of 2 MB
 size_t size_class(size_t b) {
@@ -116,6 +120,7 @@ void trim_locked() {
     (void)hipFree(kv.second);
   }
   cached->clear();
+  cached_bytes = 0;
   (void)hipSetDevice(cur);
 }
 
@@ -141,6 +146,7 @@ hipError_t alloc(void** p, size_t bytes, size_t* cap, int* dev) {
       if (it != cached->end()) {
         *p = it->second;
         cached->erase(it);
+        cached_bytes -= cls;
         *cap = cls;
         return hipSuccess;
       }
@@ -158,7 +164,7 @@ hipError_t alloc(void** p, size_t bytes, size_t* cap, int* dev) {
 
 void give_back(void* p, size_t cap, int dev) {
   std::lock_guard<std::mutex> lk(mu);
-  if (closed) {
+  if (closed || cached_bytes + cap > kCacheMax) {
     int cur = 0;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(dev);
@@ -168,6 +174,7 @@ void give_back(void* p, size_t cap, int dev) {
   }
   if (!cached) cached = new std::multimap<std::pair<int, size_t>, void*>();
   cached->insert({{dev, cap}, p});
+  cached_bytes += cap;
 }
 }  // namespace devpool
 
