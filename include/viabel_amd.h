@@ -258,6 +258,14 @@ int vb_block_floor(vb_ctx* ctx, int32_t D, int32_t N, int32_t chivi, int32_t hos
  * smoothed_out [n_problems][P] = mean of the history rows (vb.py:386-387). */
 int vb_run_result(vb_run* run, double* lam_out, double* hist_out,
                   double* values_out, double* smoothed_out);
+/* Progress snapshot of problem 0's objective values (the reference's progress bar,
+ * vb.py:378-381, without stalling the device): vb_run_values_async queues a copy of
+ * values[0 .. count) into a pinned buffer of the run behind the work already queued
+ * and returns at once; the caller may queue further advances; vb_run_values_wait
+ * waits for that copy only, writes the count values to out and count_out.  One
+ * snapshot per context is pending at a time (the context's pinned buffer). */
+int vb_run_values_async(vb_run* run, int64_t count);
+int vb_run_values_wait(vb_run* run, double* out, int64_t* count_out);
 int vb_run_destroy(vb_run* run);
 
 /* One adagrad step (vb.py:364-374) for a caller-supplied gradient (foreign

@@ -84,6 +84,8 @@ _SIGNATURES = {
                        ctypes.c_int64, c_double_p, P(ctypes.c_void_p)], ctypes.c_int),
     'vb_run_advance': ([ctypes.c_void_p, ctypes.c_int64, P(Noise)], ctypes.c_int),
     'vb_run_steps_done': ([ctypes.c_void_p, c_int64_p], ctypes.c_int),
+    'vb_run_values_async': ([ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
+    'vb_run_values_wait': ([ctypes.c_void_p, c_double_p, c_int64_p], ctypes.c_int),
     'vb_run_fr_retries': ([ctypes.c_void_p, c_int64_p], ctypes.c_int),
     'vb_peak_probe': ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
                        c_double_p], ctypes.c_int),

@@ -478,6 +478,19 @@ class DeviceRun:
         nat.check(nat.lib().vb_run_result(self.handle, None, None, nat.dptr(vals), None))
         return vals[0]
 
+    def values_async(self, count):
+        """Queue a snapshot of problem 0's first `count` values behind the work
+        already queued (vb_run_values_async); values_wait() returns it."""
+        nat.check(nat.lib().vb_run_values_async(self.handle, int(count)))
+
+    def values_wait(self):
+        """Wait for the last values_async snapshot only and return it."""
+        import ctypes
+        out = np.empty(max(1, self.n_iters))
+        n = ctypes.c_int64()
+        nat.check(nat.lib().vb_run_values_wait(self.handle, nat.dptr(out), ctypes.byref(n)))
+        return out[:n.value]
+
     def steps_done(self):
         """Steps the library has run (vb_run_steps_done): the truth after an
         interrupt, whatever the caller's own counter says."""
@@ -533,19 +546,45 @@ def _native_adagrad(n_iters, obj, init_param, window, learning_rate, epsilon,
     bar = _progress(n_iters)
     done = 0
     step0 = fam.step if fam.rng == 'philox' else None
+    shown = 0
+
+    def show():
+        # the snapshot queued after the previous chunk: waiting for it leaves the
+        # chunk queued since then running (the device never idles for the bar)
+        nonlocal shown
+        vals = run.values_wait()
+        upto = len(vals)
+        bar.update(upto - shown)
+        shown = upto
+        bar.set_description('Average Loss = {:,.5g}'.format(
+            np.mean(vals[max(0, upto - 1 - 1000):upto])))
+
     try:
-        while done < n_iters:
-            cs = min(chunk, n_iters - done)
-            if fam.rng == 'philox':
+        if bar is not None and fam.rng == 'philox':
+            pending = False
+            while done < n_iters:
+                cs = min(chunk, n_iters - done)
                 run.advance_philox(cs, fam.seed, fam.stream, step0 + done)
-            else:
-                run.advance_host(np.stack([obj._eps_one_call() for _ in range(cs)])[None])
-            done += cs
-            if bar is not None:
-                vals = run.values()
-                bar.update(cs)
-                bar.set_description('Average Loss = {:,.5g}'.format(
-                    np.mean(vals[max(0, done - 1 - 1000):done])))
+                done += cs
+                if pending:
+                    show()
+                run.values_async(done)
+                pending = True
+            if pending:
+                show()
+        else:
+            while done < n_iters:
+                cs = min(chunk, n_iters - done)
+                if fam.rng == 'philox':
+                    run.advance_philox(cs, fam.seed, fam.stream, step0 + done)
+                else:
+                    run.advance_host(np.stack([obj._eps_one_call() for _ in range(cs)])[None])
+                done += cs
+                if bar is not None:
+                    vals = run.values()
+                    bar.update(cs)
+                    bar.set_description('Average Loss = {:,.5g}'.format(
+                        np.mean(vals[max(0, done - 1 - 1000):done])))
     except KeyboardInterrupt:
         pass
     finally:
